@@ -1,0 +1,347 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched quorum engine (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+One step = one pass of the hot path over this rank's resident batch.  The
+headline workload (default, BASELINE configs[1]) is 64M groups x 5-voter
+MajorityConfig CommittedIndex + VoteResult (+ TallyVotes counts) per GPU;
+groups are sharded across ranks (weak scaling, no data-path collective; one
+RCCL all-reduce of the statistics vector after the timed region).
+
+Rank 0 prints ONE JSON line with the metric, the roofline of the dominant
+kernel (HIP events on the launch stream), and the CPU baseline (oracle port,
+rank 0 at N=1 only, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from etcd_amd import engine  # noqa: E402
+
+METRIC = "quorum group-evals/sec at 1/2/4/8 MI355X; % HBM peak; speedup vs Go host"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: (description, groups per GPU, slots, kind)
+    "config2_n5": ("64M groups x 5-voter MajorityConfig CommittedIndex+VoteResult+TallyVotes",
+                   1 << 26, 5, "majority"),
+    "config2_n7": ("64M groups x 7-voter MajorityConfig CommittedIndex+VoteResult+TallyVotes",
+                   1 << 26, 7, "majority"),
+    "config3_joint": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked) "
+                      "CommittedIndex+VoteResult+TallyVotes", 1 << 27, 10, "joint"),
+    "config4_repl": ("32M groups x 5 voters lockstep replication round (MaybeUpdate, "
+                     "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
+    "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
+                     1 << 21, 5, "elec"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="config2_n5", choices=sorted(WORKLOADS))
+    ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-aux", action="store_true", help="skip the secondary workloads")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-groups", type=int, default=1 << 21)
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(device_ids=[self.local])
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_stats(self, folded):
+        """RCCL all-reduce of the uint64 statistics vector (sum; the int64
+        wraparound equals uint64 modular addition)."""
+        if self.world > 1:
+            dist.all_reduce(folded, op=dist.ReduceOp.SUM)
+        return folded
+
+
+# ---------------------------------------------------------------------------
+# workload setup: returns (step_fn, bytes_per_unit, units_per_step, unit_name)
+# ---------------------------------------------------------------------------
+def setup(name, G, S, kind, d, stats):
+    goff = d.rank * G
+    if kind in ("majority", "joint"):
+        masks = () if kind == "majority" else ("inc", "out", "learner")
+        b = engine.SlotBatch(G, S, d.dev, masks=masks, group_offset=goff)
+        if kind == "joint":
+            engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5)
+        else:
+            engine.gen_groups(b, 0x5EED)
+        out = engine.Outputs(G, d.dev)
+        gs = b.struct()
+        os_ = out.struct(stats)
+        import ctypes as C
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+
+        def step():
+            engine.check("qe_commit_vote", lib.qe_commit_vote(C.byref(gs), C.byref(os_), stream))
+
+        # algorithmic bytes per group: every input read once, every output
+        # written once; +2 B TallyVotes counts we also write
+        bpg = b.bytes_per_group(with_outputs=True) + 2
+        if kind == "joint":
+            # config 3 counts only the union slots' Match: 19 + 8u + 2 (tally)
+            inc = b.inc.to(torch.int32)
+            uni = (inc | b.out.to(torch.int32))
+            u = torch.zeros(G, dtype=torch.int64, device=d.dev)
+            for s in range(S):
+                u += (uni >> s) & 1
+            mean_u = float(u.double().mean().item())
+            bpg = 3 * 2 + 2 * 2 + 8 * mean_u + 9 + 2
+        return step, bpg, G, "group-evals", {"batch": b, "out": out}
+    if kind == "repl":
+        b = engine.SlotBatch(G, S, d.dev, masks=(), votes=False, group_offset=goff)
+        engine.gen_groups(b, 0x5EED, p_absent=0)
+        rows = b.match_rows()
+        lo = rows.min(dim=0).values
+        hi = rows.max(dim=0).values
+        st = engine.ReplicationState(b, lo.clone(), lo + (hi - lo) // 2, hi + 1024)
+        # responses: followers ack a bit beyond their match (pre-generated,
+        # resident in HBM; re-reading the same batch each round is a valid
+        # duplicate-MsgAppResp workload with identical per-round work)
+        rb = engine.SlotBatch(G, S, d.dev, masks=(), votes=False, group_offset=goff)
+        engine.gen_groups(rb, 0xACC, p_absent=0)
+        resp = b.match.clone() + (rb.match & 1023)
+        del rb
+        full = (1 << S) - 1
+        rm = torch.full((G,), full & 0b11110, dtype=torch.uint8, device=d.dev)
+        acks = torch.full((G,), 0b00111, dtype=torch.uint8, device=d.dev)
+        read_ok = torch.empty(G, dtype=torch.uint8, device=d.dev)
+        import ctypes as C
+        s_ = st.struct()
+        m_ = engine.QeReplMsgs(engine._ptr(resp), engine._ptr(rm), engine._ptr(acks),
+                               engine._ptr(read_ok), None)
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            engine.check("qe_replication_round",
+                         lib.qe_replication_round(C.byref(s_), C.byref(m_), sp, stream))
+
+        bpg = 40 * S + 26 + 1  # SURVEY.md §8(d) config 4 (+ ReadIndex out byte)
+        return step, bpg, G, "group-rounds", {"b": b, "st": st, "resp": resp}
+    if kind == "elec":
+        b = engine.SlotBatch(G, S, d.dev, masks=("inc",), votes=False, group_offset=goff)
+        engine.gen_groups(b, 0x5EED)
+        est = engine.ElectionState(b, engine.first_voter_slot(b))
+        steps_per_launch = 64
+        counter = {"step0": 0}
+        import ctypes as C
+        s_ = est.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            p = engine.QeElectionParams(0xE1EC, counter["step0"], steps_per_launch, 13107, 32768, 0)
+            engine.check("qe_election_steps", lib.qe_election_steps(C.byref(s_), C.byref(p), sp, stream))
+            counter["step0"] += steps_per_launch
+
+        # HBM bytes per group-step: state in+out / steps (register-resident)
+        bpg = (8 + 1 + 1 + 1 + 1 + 1 + 8 + 1 + 1 + 1) / steps_per_launch
+        return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
+    raise ValueError(kind)
+
+
+def time_steps(step, d, steps, warmup):
+    for _ in range(warmup):
+        step()
+    d.barrier()
+    torch.cuda.synchronize(d.dev)
+    stream = torch.cuda.current_stream(d.dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    d.barrier()
+    torch.cuda.synchronize(d.dev)
+    wall = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    return wall, kern_ms
+
+
+def cpu_baseline(args, S=5):
+    """Oracle port timed on this host's cores over a bounded sample."""
+    from oracle import orc
+    G = args.cpu_groups
+    hb = orc.Batch(G, S, masks=())
+    orc.gen_batch(hb, 0x5EED, threads=args.cpu_threads)
+    commit = np.zeros(G, np.uint64)
+    vote = np.zeros(G, np.uint8)
+    L = orc.lib()
+    w = L.orc_gf_build(G, S, G, orc.P(hb.match), None, None, None, orc.P(hb.voted),
+                       orc.P(hb.granted))
+    try:
+        L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, args.cpu_threads)  # warm-up
+        t1 = L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, args.cpu_threads)
+        reps = max(1, int(1.5 / max(t1, 1e-6)))
+        t = L.orc_gf_run(w, orc.P(commit), orc.P(vote), reps, args.cpu_threads)
+        gf_rate = G * reps / t
+    finally:
+        L.orc_gf_free(w)
+    # the SoA restatement (strongest CPU variant)
+    L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
+                  orc.P(commit), orc.P(vote), 1, args.cpu_threads)
+    t1 = L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
+                       orc.P(commit), orc.P(vote), 1, args.cpu_threads)
+    reps2 = max(1, int(1.5 / max(t1, 1e-6)))
+    t2 = L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
+                       orc.P(commit), orc.P(vote), reps2, args.cpu_threads)
+    soa_rate = G * reps2 / t2
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": gf_rate, "unit": "group-evals/s", "cores": args.cpu_threads, "kind": "port",
+        "sample": (f"{G} groups x 5 voters x {reps} passes: Go-faithful map/AckedIndexer loop "
+                   f"(oracle/quorum_oracle.c orc_gf_run, CommittedIndex+VoteResult per group), "
+                   f"OpenMP {args.cpu_threads} threads, {cpu_model}"),
+        "soa_value": soa_rate,
+        "soa_sample": f"{G} groups x {reps2} passes, SoA restatement (orc_soa_run)",
+    }
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data.get(workload, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def run_workload(name, args, d, steps, warmup):
+    desc, G, S, kind = WORKLOADS[name]
+    if args.groups and name == args.workload:
+        G = args.groups
+    stats = engine.stats_buffer(d.dev)
+    step, bpu, units, unit_name, keep = setup(name, G, S, kind, d, stats)
+    torch.cuda.synchronize(d.dev)
+    wall, kern_ms = time_steps(step, d, steps, warmup)
+    ms_step = d.max(wall * 1000.0 / steps)
+    kern_avg = d.max(float(np.mean(kern_ms)))
+    folded = d.sum_stats(engine.stats_reduce(stats))
+    st = engine.stats_dict(folded)
+    value = units * d.world / (ms_step / 1000.0)
+    achieved = bpu * units / (kern_avg / 1000.0) / 1e9
+    del keep
+    torch.cuda.empty_cache()
+    return {
+        "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
+        "unit": f"{unit_name}/s", "value": value, "ms_per_step": ms_step,
+        "kernel_ms": kern_avg, "bytes_per_unit": bpu,
+        "achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
+        "invariant_violations": st["invariant_violations"], "checksum": st["checksum"],
+        "stats": st,
+    }
+
+
+def main():
+    args = parse()
+    d = Dist()
+    main_res = run_workload(args.workload, args, d, args.steps, args.warmup)
+    aux = {}
+    if not args.no_aux:
+        for name in WORKLOADS:
+            if name == args.workload:
+                continue
+            r = run_workload(name, args, d, max(3, args.steps // 4), 2)
+            aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
+                                           "achieved_GBs", "hbm_frac", "invariant_violations")}
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if d.rank == 0:
+        desc, G, S, kind = WORKLOADS[args.workload]
+        traffic = load_traffic(args.workload)
+        line = {
+            "metric": METRIC,
+            "value": main_res["value"],
+            "unit": "group-evals/s" if kind in ("majority", "joint") else main_res["unit"],
+            "n_gpus": d.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": main_res["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: counter-based splitmix64 generator, inputs resident in HBM",
+            "config": {
+                "workload": f"{args.workload}: {desc}",
+                "groups_per_gpu": main_res["groups_per_gpu"],
+                "global_groups": main_res["groups_per_gpu"] * d.world,
+                "voters": S,
+                "parallelism": f"group-sharded x{d.world} (no data-path collective; "
+                               f"RCCL all-reduce of 16 stats counters after the run)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": main_res["achieved_GBs"],
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": main_res["hbm_frac"],
+                "traffic": traffic,
+                "kernel": "qe::k_commit_vote" if kind in ("majority", "joint") else kind,
+                "kernel_ms": main_res["kernel_ms"],
+                "bytes_per_unit": main_res["bytes_per_unit"],
+            },
+            "cpu_baseline": cpu,
+            "checks": {"invariant_violations": main_res["invariant_violations"],
+                       "stats_checksum": main_res["checksum"]},
+            "aux": aux,
+        }
+        print(json.dumps(line))
+    if d.world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

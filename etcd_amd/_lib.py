@@ -1,0 +1,133 @@
+"""ctypes binding of the C ABI in include/etcd_quorum.h (libetcd_quorum.so).
+
+This is the same surface a cgo binding would use.  The
+library is the product: if it is missing this module raises at import time
+-- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
+
+QE_OK = 0
+QE_EINVAL = -22
+QE_ERANGE = -34
+QE_EHIP = -1000
+QE_INDEX_INF = (1 << 64) - 1
+QE_MAX_SLOTS = 16
+QE_VOTE_PENDING, QE_VOTE_LOST, QE_VOTE_WON = 1, 2, 3
+QE_STATE_FOLLOWER, QE_STATE_CANDIDATE, QE_STATE_LEADER = 0, 1, 2
+QE_STATS_COUNTERS = 16
+QE_STATS_SHARDS = 64
+QE_STATS_WORDS = QE_STATS_COUNTERS * QE_STATS_SHARDS
+
+STAT_NAMES = [
+    "groups", "commit_inf", "commit_sum", "commit_zero", "vote_won", "vote_lost",
+    "vote_pending", "granted", "rejected", "commit_advanced", "read_released", "elections",
+    "leaders", "stepdowns", "invariant_violations", "checksum",
+]
+
+u64, u32, vp = C.c_uint64, C.c_uint32, C.c_void_p
+
+
+class QeGroups(C.Structure):
+    _fields_ = [
+        ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("reserved", u32),
+        ("stride", u64), ("match", vp), ("inc_mask", vp), ("out_mask", vp),
+        ("learner_mask", vp), ("voted", vp), ("granted", vp),
+    ]
+
+
+class QeOutputs(C.Structure):
+    _fields_ = [("commit", vp), ("vote", vp), ("granted_count", vp), ("rejected_count", vp),
+                ("stats", vp)]
+
+
+class QeReplState(C.Structure):
+    _fields_ = [
+        ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("reserved", u32),
+        ("stride", u64), ("match", vp), ("next", vp), ("committed", vp), ("term_start", vp),
+        ("last_index", vp), ("inc_mask", vp), ("out_mask", vp),
+    ]
+
+
+class QeReplMsgs(C.Structure):
+    _fields_ = [("resp_index", vp), ("resp_mask", vp), ("read_acks", vp), ("read_ok", vp),
+                ("commit_advanced", vp)]
+
+
+class QeElectionState(C.Structure):
+    _fields_ = [
+        ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("reserved", u32),
+        ("term", vp), ("state", vp), ("voted", vp), ("granted", vp), ("self_slot", vp),
+        ("inc_mask", vp), ("out_mask", vp), ("learner_mask", vp),
+    ]
+
+
+class QeElectionParams(C.Structure):
+    _fields_ = [("seed", u64), ("step0", u64), ("steps", u32), ("p_drop_q16", u32),
+                ("p_grant_q16", u32), ("reserved", u32)]
+
+
+class QeGenParams(C.Structure):
+    _fields_ = [
+        ("seed", u64), ("group_offset", u64), ("dist", u32), ("p_absent_q16", u32),
+        ("p_voted_q16", u32), ("p_granted_q16", u32), ("n_inc", u32), ("n_out", u32),
+        ("mask_mode", u32), ("reserved", u32),
+    ]
+
+
+# Every symbol include/etcd_quorum.h declares, with its prototype.
+PROTOTYPES = {
+    "qe_abi_version": (C.c_int, []),
+    "qe_strerror": (C.c_char_p, [C.c_int]),
+    "qe_mask_bytes": (C.c_size_t, [u32]),
+    "qe_tune": (C.c_int, [C.c_char_p, C.c_int]),
+    "qe_commit_vote": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeOutputs), vp]),
+    "qe_committed_index": (C.c_int, [C.POINTER(QeGroups), vp, vp]),
+    "qe_vote_result": (C.c_int, [C.POINTER(QeGroups), vp, vp]),
+    "qe_quorum_active": (C.c_int, [C.POINTER(QeGroups), vp, vp, vp]),
+    "qe_record_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp]),
+    "qe_replication_round": (C.c_int, [C.POINTER(QeReplState), C.POINTER(QeReplMsgs), vp, vp]),
+    "qe_election_steps": (C.c_int, [C.POINTER(QeElectionState), C.POINTER(QeElectionParams),
+                                    vp, vp]),
+    "qe_stats_reduce": (C.c_int, [vp, vp, vp]),
+    "qe_gen_groups": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeGenParams), vp]),
+}
+
+
+class QuorumEngineError(RuntimeError):
+    def __init__(self, fn, status):
+        msg = _LIB.qe_strerror(status).decode() if _LIB is not None else str(status)
+        super().__init__(f"{fn} failed: {status} ({msg})")
+        self.status = status
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"etcd_amd: HIP library {LIB_PATH} is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in PROTOTYPES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.qe_abi_version() != 1:
+        raise ImportError("etcd_amd: ABI version mismatch")
+    return lib
+
+
+_LIB = None
+_LIB = _load()
+
+
+def lib():
+    return _LIB
+
+
+def check(fn, status):
+    if status != QE_OK:
+        raise QuorumEngineError(fn, status)
+    return status

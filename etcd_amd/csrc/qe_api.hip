@@ -1,0 +1,324 @@
+// qe_api.hip — C ABI of include/etcd_quorum.h: argument checks, alignment
+// selection of the vectorised path and launch of the MI355X kernels.
+#include <stdio.h>
+#include <string.h>
+
+#include "qe_dispatch.hpp"
+
+namespace qe {
+
+int g_blocks_per_cu = 8;
+int g_nontemporal = 0;
+
+static thread_local char g_errbuf[256];
+
+int hip_status(hipError_t e) {
+  if (e == hipSuccess) return QE_OK;
+  snprintf(g_errbuf, sizeof(g_errbuf), "HIP error %d: %s", static_cast<int>(e),
+           hipGetErrorString(e));
+  return QE_EHIP;
+}
+
+static inline bool al(const void *p, size_t a) {
+  return (reinterpret_cast<uintptr_t>(p) % a) == 0;
+}
+
+static unsigned simple_grid(uint64_t G) {
+  const uint64_t cap = static_cast<uint64_t>(num_cus()) * 8;
+  const uint64_t need = (G + kBlock - 1) / kBlock;
+  return static_cast<unsigned>(need < cap ? (need ? need : 1) : cap);
+}
+
+__global__ void k_stats_reduce(const uint64_t *stats, uint64_t *out) {
+  const int c = threadIdx.x;
+  if (c < QE_STATS_COUNTERS) {
+    uint64_t s = 0;
+    for (int k = 0; k < QE_STATS_SHARDS; k++) s += stats[k * QE_STATS_COUNTERS + c];
+    out[c] = s;
+  }
+}
+
+
+#define QE_SWITCH(S, CALL)                                                              \
+  switch (S) {                                                                          \
+    case 1: return CALL(1); case 2: return CALL(2); case 3: return CALL(3);             \
+    case 4: return CALL(4); case 5: return CALL(5); case 6: return CALL(6);             \
+    case 7: return CALL(7); case 8: return CALL(8); case 9: return CALL(9);             \
+    case 10: return CALL(10); case 11: return CALL(11); case 12: return CALL(12);       \
+    case 13: return CALL(13); case 14: return CALL(14); case 15: return CALL(15);       \
+    case 16: return CALL(16);                                                           \
+    default: return QE_EINVAL;                                                          \
+  }
+
+static int dispatch_cv(uint32_t S, const CVArgs &a, int mode, bool vec, hipStream_t st) {
+#define QE_C(n) dispatch_cv_##n(a, mode, vec, st)
+  QE_SWITCH(S, QE_C)
+#undef QE_C
+}
+
+static int dispatch_repl(uint32_t S, const RArgs &a, bool masked, bool joint, bool vec,
+                         hipStream_t st) {
+#define QE_C(n) dispatch_repl_##n(a, masked, joint, vec, st)
+  QE_SWITCH(S, QE_C)
+#undef QE_C
+}
+
+static int dispatch_elec(uint32_t S, const EArgs &a, hipStream_t st) {
+#define QE_C(n) dispatch_elec_##n(a, st)
+  QE_SWITCH(S, QE_C)
+#undef QE_C
+}
+
+}  // namespace qe
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace qe;
+
+extern "C" {
+
+int qe_abi_version(void) { return QE_ABI_VERSION; }
+
+const char *qe_strerror(int status) {
+  switch (status) {
+    case QE_OK: return "ok";
+    case QE_EINVAL: return "invalid argument";
+    case QE_ERANGE: return "out of range";
+    case QE_EHIP: return g_errbuf[0] ? g_errbuf : "HIP error";
+    default: return "unknown status";
+  }
+}
+
+size_t qe_mask_bytes(uint32_t num_slots) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return 0;
+  return num_slots <= 8 ? 1 : 2;
+}
+
+// Optional tuning knobs (not part of the reference semantics):
+//   "blocks_per_cu"  persistent-grid workgroups per CU (1..32, default 8)
+//   "nontemporal"    0/1: non-temporal match loads in qe_commit_vote
+int qe_tune(const char *key, int value) {
+  if (!key) return QE_EINVAL;
+  if (!strcmp(key, "blocks_per_cu")) {
+    if (value < 1 || value > 32) return QE_ERANGE;
+    g_blocks_per_cu = value;
+    return QE_OK;
+  }
+  if (!strcmp(key, "nontemporal")) {
+    g_nontemporal = value ? 1 : 0;
+    return QE_OK;
+  }
+  return QE_EINVAL;
+}
+
+static int check_groups(const qe_groups *g) {
+  if (!g) return QE_EINVAL;
+  if (g->num_slots == 0 || g->num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (g->reserved != 0) return QE_EINVAL;
+  if (g->num_groups && g->stride < g->num_groups) return QE_EINVAL;
+  if (g->out_mask && !g->inc_mask) return QE_EINVAL;
+  return QE_OK;
+}
+
+int qe_commit_vote(const qe_groups *g, const qe_outputs *out, void *stream) {
+  int rc = check_groups(g);
+  if (rc) return rc;
+  if (!out) return QE_EINVAL;
+  if (g->num_groups == 0) return QE_OK;
+  if (!g->match) return QE_EINVAL;
+  CVArgs a{};
+  a.G = g->num_groups;
+  a.goff = g->group_offset;
+  a.stride = g->stride;
+  a.match = g->match;
+  a.inc = g->inc_mask;
+  a.out = g->out_mask;
+  a.learner = g->learner_mask;
+  a.voted = g->voted;
+  a.granted = g->granted;
+  a.commit = out->commit;
+  a.vote = out->vote;
+  a.gcount = out->granted_count;
+  a.rcount = out->rejected_count;
+  a.stats = out->stats;
+  const int mode = g->out_mask ? 2 : (g->inc_mask ? 1 : 0);
+  const size_t mb = qe_mask_bytes(g->num_slots);
+  bool vec = al(g->match, 16) && (g->stride % 2 == 0) && al(out->commit, 16);
+  const void *masks[] = {g->inc_mask, g->out_mask, g->learner_mask, g->voted, g->granted};
+  for (const void *m : masks) vec = vec && al(m, 2 * mb);
+  const uint8_t *bytes[] = {out->vote, out->granted_count, out->rejected_count};
+  for (const uint8_t *b : bytes) vec = vec && al(b, 2);
+  return dispatch_cv(g->num_slots, a, mode, vec, static_cast<hipStream_t>(stream));
+}
+
+int qe_committed_index(const qe_groups *g, uint64_t *commit, void *stream) {
+  if (!g || !commit) return QE_EINVAL;
+  qe_groups gg = *g;
+  gg.voted = nullptr;
+  gg.granted = nullptr;
+  qe_outputs o{};
+  o.commit = commit;
+  return qe_commit_vote(&gg, &o, stream);
+}
+
+int qe_vote_result(const qe_groups *g, uint8_t *vote, void *stream) {
+  int rc = check_groups(g);
+  if (rc) return rc;
+  if (!vote) return QE_EINVAL;
+  if (g->num_groups == 0) return QE_OK;
+  const uint32_t full = (1u << g->num_slots) - 1u;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = simple_grid(g->num_groups);
+  if (g->num_slots <= 8)
+    hipLaunchKernelGGL(k_vote_result<uint8_t>, dim3(grid), dim3(kBlock), 0, st, g->num_groups,
+                       full, g->inc_mask, g->out_mask, g->voted, g->granted, vote);
+  else
+    hipLaunchKernelGGL(k_vote_result<uint16_t>, dim3(grid), dim3(kBlock), 0, st,
+                       g->num_groups, full, g->inc_mask, g->out_mask, g->voted, g->granted,
+                       vote);
+  return hip_status(hipGetLastError());
+}
+
+int qe_quorum_active(const qe_groups *g, const void *recent_active, uint8_t *active,
+                     void *stream) {
+  int rc = check_groups(g);
+  if (rc) return rc;
+  if (!recent_active || !active) return QE_EINVAL;
+  if (g->num_groups == 0) return QE_OK;
+  const uint32_t full = (1u << g->num_slots) - 1u;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = simple_grid(g->num_groups);
+  if (g->num_slots <= 8)
+    hipLaunchKernelGGL(k_quorum_active<uint8_t>, dim3(grid), dim3(kBlock), 0, st,
+                       g->num_groups, full, g->inc_mask, g->out_mask, g->learner_mask,
+                       recent_active, active);
+  else
+    hipLaunchKernelGGL(k_quorum_active<uint16_t>, dim3(grid), dim3(kBlock), 0, st,
+                       g->num_groups, full, g->inc_mask, g->out_mask, g->learner_mask,
+                       recent_active, active);
+  return hip_status(hipGetLastError());
+}
+
+int qe_record_votes(uint64_t num_groups, uint32_t num_slots, void *voted, void *granted,
+                    const void *resp_mask, const void *resp_value, void *stream) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (num_groups == 0) return QE_OK;
+  if (!voted || !granted || !resp_mask || !resp_value) return QE_EINVAL;
+  const uint32_t full = (1u << num_slots) - 1u;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = simple_grid(num_groups);
+  if (num_slots <= 8)
+    hipLaunchKernelGGL(k_record_votes<uint8_t>, dim3(grid), dim3(kBlock), 0, st, num_groups,
+                       full, voted, granted, resp_mask, resp_value);
+  else
+    hipLaunchKernelGGL(k_record_votes<uint16_t>, dim3(grid), dim3(kBlock), 0, st, num_groups,
+                       full, voted, granted, resp_mask, resp_value);
+  return hip_status(hipGetLastError());
+}
+
+int qe_replication_round(const qe_repl_state *s, const qe_repl_msgs *m, uint64_t *stats,
+                         void *stream) {
+  if (!s || !m) return QE_EINVAL;
+  if (s->num_slots == 0 || s->num_slots > QE_MAX_SLOTS || s->reserved) return QE_EINVAL;
+  if (s->num_groups == 0) return QE_OK;
+  if (s->stride < s->num_groups) return QE_EINVAL;
+  if (!s->match || !s->next || !s->committed || !s->term_start || !s->last_index ||
+      !m->resp_index)
+    return QE_EINVAL;
+  if (s->out_mask && !s->inc_mask) return QE_EINVAL;
+  RArgs a{};
+  a.G = s->num_groups;
+  a.goff = s->group_offset;
+  a.stride = s->stride;
+  a.match = s->match;
+  a.next = s->next;
+  a.committed = s->committed;
+  a.term_start = s->term_start;
+  a.last_index = s->last_index;
+  a.resp = m->resp_index;
+  a.inc = s->inc_mask;
+  a.out = s->out_mask;
+  a.resp_mask = m->resp_mask;
+  a.read_acks = m->read_acks;
+  a.read_ok = m->read_ok;
+  a.adv = m->commit_advanced;
+  a.stats = stats;
+  const size_t mb = qe_mask_bytes(s->num_slots);
+  bool vec = (s->stride % 2 == 0);
+  const void *p16[] = {s->match, s->next, s->committed, s->term_start, s->last_index,
+                       m->resp_index};
+  for (const void *p : p16) vec = vec && al(p, 16);
+  const void *pm[] = {s->inc_mask, s->out_mask, m->resp_mask, m->read_acks};
+  for (const void *p : pm) vec = vec && al(p, 2 * mb);
+  vec = vec && al(m->read_ok, 2) && al(m->commit_advanced, 2);
+  return dispatch_repl(s->num_slots, a, s->inc_mask != nullptr, s->out_mask != nullptr, vec,
+                       static_cast<hipStream_t>(stream));
+}
+
+int qe_election_steps(const qe_election_state *s, const qe_election_params *p, uint64_t *stats,
+                      void *stream) {
+  if (!s || !p) return QE_EINVAL;
+  if (s->num_slots == 0 || s->num_slots > QE_MAX_SLOTS || s->reserved) return QE_EINVAL;
+  if (s->num_groups == 0) return QE_OK;
+  if (!s->term || !s->state || !s->voted || !s->granted || !s->self_slot) return QE_EINVAL;
+  if (s->out_mask && !s->inc_mask) return QE_EINVAL;
+  if (p->p_drop_q16 > 65536 || p->p_grant_q16 > 65536) return QE_ERANGE;
+  EArgs a{};
+  a.G = s->num_groups;
+  a.goff = s->group_offset;
+  a.term = s->term;
+  a.state = s->state;
+  a.voted = s->voted;
+  a.granted = s->granted;
+  a.self_slot = s->self_slot;
+  a.inc = s->inc_mask;
+  a.out = s->out_mask;
+  a.learner = s->learner_mask;
+  a.seed = p->seed;
+  a.step0 = p->step0;
+  a.steps = p->steps;
+  a.p_drop = p->p_drop_q16;
+  a.p_grant = p->p_grant_q16;
+  a.stats = stats;
+  return dispatch_elec(s->num_slots, a, static_cast<hipStream_t>(stream));
+}
+
+int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream) {
+  if (!stats || !out) return QE_EINVAL;
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     stats, out);
+  return hip_status(hipGetLastError());
+}
+
+int qe_gen_groups(const qe_groups *g, const qe_gen_params *p, void *stream) {
+  int rc = check_groups(g);
+  if (rc) return rc;
+  if (!p) return QE_EINVAL;
+  if (g->num_groups == 0) return QE_OK;
+  if (p->p_absent_q16 > 65536 || p->p_voted_q16 > 65536 || p->p_granted_q16 > 65536)
+    return QE_ERANGE;
+  GArgs a{};
+  a.G = g->num_groups;
+  a.goff = g->group_offset;
+  a.stride = g->stride;
+  a.S = g->num_slots;
+  a.match = const_cast<uint64_t *>(g->match);
+  a.inc = const_cast<void *>(g->inc_mask);
+  a.out = const_cast<void *>(g->out_mask);
+  a.learner = const_cast<void *>(g->learner_mask);
+  a.voted = const_cast<void *>(g->voted);
+  a.granted = const_cast<void *>(g->granted);
+  a.p = *p;
+  // qe_gen_params.group_offset adds to qe_groups.group_offset.
+  a.goff = g->group_offset + p->group_offset;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = simple_grid(g->num_groups);
+  if (g->num_slots <= 8)
+    hipLaunchKernelGGL(k_gen<uint8_t>, dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_gen<uint16_t>, dim3(grid), dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+// qe_device.hpp — device-side building blocks of the batched quorum engine
+// (gfx950).  Pure integer work: 64-bit compare/select networks, popcount vote
+// logic, a counter-based hash.  No MFMA: the path is HBM-bound.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qe {
+
+constexpr uint64_t kInf = ~0ull;
+constexpr uint64_t kPhi = 0x9E3779B97F4A7C15ull;
+constexpr uint32_t kVotePending = 1, kVoteLost = 2, kVoteWon = 3;
+
+// splitmix64 finalizer; identical to oracle/quorum_oracle.c:orc_mix64.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t hash4(uint64_t seed, uint64_t gid, uint32_t lane,
+                                          uint32_t stream) {
+  uint64_t k = (static_cast<uint64_t>(stream) << 32) | lane;
+  return mix64(mix64(seed + gid * kPhi) ^ (k * 0xD6E8FEB86659FD93ull));
+}
+
+__device__ __forceinline__ uint32_t popc(uint32_t x) { return __builtin_popcount(x); }
+
+// ---------------------------------------------------------------------------
+// Sorting networks (Batcher odd-even merge sort for arbitrary n, built at
+// compile time).  Only the comparators that feed the selected rank survive
+// dead-code elimination, so `select_fixed<N>` costs a partial network.
+// ---------------------------------------------------------------------------
+struct CE {
+  int a, b;
+};
+
+template <int N>
+struct Batcher {
+  static constexpr int count() {
+    int c = 0;
+    for (int p = 1; p < N; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < N; j += 2 * k)
+          for (int i = 0; i < k && i < N - j - k; i++)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) c++;
+    return c;
+  }
+  static constexpr int kSize = count();
+  struct Net {
+    CE e[kSize > 0 ? kSize : 1];
+  };
+  static constexpr Net make() {
+    Net n{};
+    int c = 0;
+    for (int p = 1; p < N; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < N; j += 2 * k)
+          for (int i = 0; i < k && i < N - j - k; i++)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) n.e[c++] = CE{i + j, i + j + k};
+    return n;
+  }
+  static constexpr Net kNet = make();
+};
+
+__device__ __forceinline__ void cmpx(uint64_t &a, uint64_t &b) {
+  const bool sw = b < a;
+  const uint64_t lo = sw ? b : a;
+  const uint64_t hi = sw ? a : b;
+  a = lo;
+  b = hi;
+}
+
+__device__ __forceinline__ void cmpx_p(uint64_t &a, uint32_t &pa, uint64_t &b, uint32_t &pb) {
+  const bool sw = b < a;
+  const uint64_t lo = sw ? b : a, hi = sw ? a : b;
+  const uint32_t plo = sw ? pb : pa, phi = sw ? pa : pb;
+  a = lo;
+  b = hi;
+  pa = plo;
+  pb = phi;
+}
+
+// (N/2+1)-th largest of N values = ascending position N-(N/2+1)
+// (raft/quorum/majority.go:165-171).  v is clobbered.
+template <int N>
+__device__ __forceinline__ uint64_t select_fixed(uint64_t (&v)[N]) {
+  constexpr auto net = Batcher<N>::kNet;
+#pragma unroll
+  for (int c = 0; c < Batcher<N>::kSize; c++) cmpx(v[net.e[c].a], v[net.e[c].b]);
+  return v[N - (N / 2 + 1)];
+}
+
+// Masked joint selection.  Slot values are sorted once with a 2-bit payload
+// (bit0: member of JointConfig[0], bit1: member of JointConfig[1]); walking
+// from the top, the k-th member of a half is that half's (n/2+1)-th largest
+// acked index.  An empty half yields inf (majority.go:128-132), and the joint
+// result is the min of the halves (joint.go:49-56).
+template <int S>
+__device__ __forceinline__ uint64_t joint_committed(uint64_t (&v)[S], uint32_t inc,
+                                                    uint32_t out) {
+  uint32_t pay[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) pay[s] = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
+  constexpr auto net = Batcher<S>::kNet;
+#pragma unroll
+  for (int c = 0; c < Batcher<S>::kSize; c++)
+    cmpx_p(v[net.e[c].a], pay[net.e[c].a], v[net.e[c].b], pay[net.e[c].b]);
+  const uint32_t n0 = popc(inc), n1 = popc(out);
+  const uint32_t k0 = n0 / 2 + 1, k1 = n1 / 2 + 1;
+  uint32_t c0 = 0, c1 = 0;
+  uint64_t r0 = n0 ? 0 : kInf, r1 = n1 ? 0 : kInf;
+#pragma unroll
+  for (int p = S - 1; p >= 0; p--) {
+    const uint32_t m0 = pay[p] & 1u, m1 = pay[p] >> 1;
+    c0 += m0;
+    c1 += m1;
+    r0 = (m0 && c0 == k0) ? v[p] : r0;
+    r1 = (m1 && c1 == k1) ? v[p] : r1;
+  }
+  return r0 < r1 ? r0 : r1;
+}
+
+// MajorityConfig.VoteResult over slot bitmaps (raft/quorum/majority.go:178-210).
+__device__ __forceinline__ uint32_t majority_vote(uint32_t member, uint32_t voted,
+                                                  uint32_t granted) {
+  const uint32_t n = popc(member);
+  const uint32_t yes = popc(member & voted & granted);
+  const uint32_t no = popc(member & voted & ~granted);
+  const uint32_t missing = n - yes - no;
+  const uint32_t q = n / 2 + 1;
+  const uint32_t r = yes >= q ? kVoteWon : (yes + missing >= q ? kVotePending : kVoteLost);
+  return n == 0 ? kVoteWon : r;
+}
+
+// JointConfig.VoteResult (raft/quorum/joint.go:61-75).
+__device__ __forceinline__ uint32_t joint_vote(uint32_t inc, uint32_t out, uint32_t voted,
+                                               uint32_t granted) {
+  const uint32_t r1 = majority_vote(inc, voted, granted);
+  const uint32_t r2 = majority_vote(out, voted, granted);
+  if (r1 == r2) return r1;
+  return (r1 == kVoteLost || r2 == kVoteLost) ? kVoteLost : kVotePending;
+}
+
+// ---------------------------------------------------------------------------
+// Wave / block reductions for the statistics counters.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint32_t lo = static_cast<uint32_t>(x), hi = static_cast<uint32_t>(x >> 32);
+    lo = __shfl_xor(lo, off, 64);
+    hi = __shfl_xor(hi, off, 64);
+    x += (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  return x;
+}
+
+// Adds NC per-thread counters into the sharded stats buffer: wave sums, then
+// LDS across the block's waves, then NC lanes of wave 0 issue one atomic each.
+template <int NC, int BLOCK>
+__device__ __forceinline__ void block_stats_add(uint64_t (&c)[NC], const int (&idx)[NC],
+                                                uint64_t *stats) {
+  __shared__ uint64_t red[BLOCK / 64][NC];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NC; i++) {
+    const uint64_t s = wave_sum_u64(c[i]);
+    if (lane == 0) red[w][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NC) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < BLOCK / 64; k++) s += red[k][threadIdx.x];
+    int which = 0;
+#pragma unroll
+    for (int i = 0; i < NC; i++)
+      if (i == static_cast<int>(threadIdx.x)) which = idx[i];
+    const int shard = blockIdx.x & 63;  // QE_STATS_SHARDS
+    atomicAdd(reinterpret_cast<unsigned long long *>(stats + shard * 16 + which),
+              static_cast<unsigned long long>(s));
+  }
+}
+
+}  // namespace qe

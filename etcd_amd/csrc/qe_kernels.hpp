@@ -1,0 +1,599 @@
+// qe_kernels.hpp — MI355X (gfx950) kernels of the batched quorum engine.
+//
+// One lane owns one pair of adjacent groups: every slot row of the SoA match
+// array is read with 16-byte loads, so one wave instruction moves 1 KiB of a
+// slot row and all 64 lanes' loads fall in eight contiguous 128-byte lines.
+// A wave iterates over tiles of 64*PAIRS pairs; the grid is persistent
+// (a few workgroups per CU) and strides over tiles.  See DESIGN.md §2-§3.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <type_traits>
+
+#include "../../include/etcd_quorum.h"
+#include "qe_device.hpp"
+
+namespace qe {
+
+constexpr int kBlock = 256;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------------------
+// Tuning knobs (qe_tune): occupancy of the persistent grid.
+// ---------------------------------------------------------------------------
+extern int g_blocks_per_cu;
+extern int g_nontemporal;
+
+inline int num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
+inline unsigned grid_for(uint64_t work_waves) {
+  const uint64_t cap = static_cast<uint64_t>(num_cus()) * g_blocks_per_cu;
+  const uint64_t need = (work_waves + (kBlock / 64) - 1) / (kBlock / 64);
+  uint64_t g = need < cap ? need : cap;
+  return static_cast<unsigned>(g ? g : 1);
+}
+
+// ---------------------------------------------------------------------------
+// Loads/stores of a pair of adjacent groups.
+// ---------------------------------------------------------------------------
+template <bool VEC, bool NT>
+__device__ __forceinline__ void ld_u64_pair(const uint64_t *p, uint64_t g0, uint64_t G,
+                                            uint64_t &lo, uint64_t &hi) {
+  if (VEC && g0 + 1 < G) {
+    const u64x2 *q = reinterpret_cast<const u64x2 *>(p + g0);
+    u64x2 x = NT ? __builtin_nontemporal_load(q) : *q;
+    lo = x.x;
+    hi = x.y;
+  } else {
+    lo = g0 < G ? p[g0] : 0;
+    hi = g0 + 1 < G ? p[g0 + 1] : 0;
+  }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void st_u64_pair(uint64_t *p, uint64_t g0, uint64_t G, uint64_t lo,
+                                            uint64_t hi) {
+  if (VEC && g0 + 1 < G) {
+    u64x2 x;
+    x.x = lo;
+    x.y = hi;
+    *reinterpret_cast<u64x2 *>(p + g0) = x;
+  } else {
+    if (g0 < G) p[g0] = lo;
+    if (g0 + 1 < G) p[g0 + 1] = hi;
+  }
+}
+
+// Mask pairs: uint8 masks load as one uint16, uint16 masks as one uint32.
+template <typename MT, bool VEC>
+__device__ __forceinline__ void ld_mask_pair(const void *p, uint64_t g0, uint64_t G,
+                                             uint32_t &lo, uint32_t &hi) {
+  const MT *m = static_cast<const MT *>(p);
+  if (VEC && g0 + 1 < G) {
+    if constexpr (sizeof(MT) == 1) {
+      const uint32_t x = *reinterpret_cast<const uint16_t *>(m + g0);
+      lo = x & 0xFFu;
+      hi = x >> 8;
+    } else {
+      const uint32_t x = *reinterpret_cast<const uint32_t *>(m + g0);
+      lo = x & 0xFFFFu;
+      hi = x >> 16;
+    }
+  } else {
+    lo = g0 < G ? m[g0] : 0u;
+    hi = g0 + 1 < G ? m[g0 + 1] : 0u;
+  }
+}
+
+template <typename MT, bool VEC>
+__device__ __forceinline__ void st_mask_pair(void *p, uint64_t g0, uint64_t G, uint32_t lo,
+                                             uint32_t hi) {
+  MT *m = static_cast<MT *>(p);
+  if (VEC && g0 + 1 < G) {
+    if constexpr (sizeof(MT) == 1) {
+      *reinterpret_cast<uint16_t *>(m + g0) = static_cast<uint16_t>(lo | (hi << 8));
+    } else {
+      *reinterpret_cast<uint32_t *>(m + g0) = lo | (hi << 16);
+    }
+  } else {
+    if (g0 < G) m[g0] = static_cast<MT>(lo);
+    if (g0 + 1 < G) m[g0 + 1] = static_cast<MT>(hi);
+  }
+}
+
+// uint8 outputs: a pair is one uint16 store.
+template <bool VEC>
+__device__ __forceinline__ void st_u8_pair(uint8_t *p, uint64_t g0, uint64_t G, uint32_t lo,
+                                           uint32_t hi) {
+  if (VEC && g0 + 1 < G) {
+    *reinterpret_cast<uint16_t *>(p + g0) = static_cast<uint16_t>(lo | (hi << 8));
+  } else {
+    if (g0 < G) p[g0] = static_cast<uint8_t>(lo);
+    if (g0 + 1 < G) p[g0 + 1] = static_cast<uint8_t>(hi);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused CommittedIndex + VoteResult + TallyVotes (qe_commit_vote).
+// MODE 0: fixed MajorityConfig of all S slots (compile-time rank)
+// MODE 1: masked MajorityConfig (inc_mask)
+// MODE 2: JointConfig (inc_mask, out_mask)
+// ---------------------------------------------------------------------------
+struct CVArgs {
+  uint64_t G, goff, stride;
+  const uint64_t *match;
+  const void *inc, *out, *learner, *voted, *granted;
+  uint64_t *commit;
+  uint8_t *vote, *gcount, *rcount;
+  uint64_t *stats;
+};
+
+enum { C_GROUPS, C_INF, C_SUM, C_ZERO, C_WON, C_LOST, C_PEND, C_GR, C_RJ, C_VIOL, C_CSUM, C_N };
+
+template <int S, int MODE>
+__device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint32_t out,
+                                           uint32_t learner, uint32_t voted, uint32_t granted,
+                                           uint64_t &commit, uint32_t &vote, uint32_t &gc,
+                                           uint32_t &rc) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  if constexpr (MODE == 0) {
+    commit = select_fixed<S>(v);
+    inc = kFull;
+    out = 0;
+  } else if constexpr (MODE == 1) {
+    out = 0;
+    commit = joint_committed<S>(v, inc, 0u);
+  } else {
+    commit = joint_committed<S>(v, inc, out);
+  }
+  vote = joint_vote(inc, out, voted, granted);
+  const uint32_t voters = (inc | out) & ~learner;
+  gc = popc(voted & granted & voters);
+  rc = popc(voted & ~granted & voters);
+}
+
+template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NT>
+__global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * kBlock) >> 6;
+  const uint64_t G = a.G;
+  const uint64_t npairs = (G + 1) >> 1;
+  constexpr uint64_t kTile = 64ull * PAIRS;
+  const uint64_t ntiles = (npairs + kTile - 1) / kTile;
+  const bool want_stats = a.stats != nullptr;
+
+  uint64_t cnt[C_N];
+#pragma unroll
+  for (int i = 0; i < C_N; i++) cnt[i] = 0;
+
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    uint64_t v[PAIRS][2][S];
+    uint32_t mi[PAIRS][2], mo[PAIRS][2], ml[PAIRS][2], vd[PAIRS][2], gr[PAIRS][2];
+    // ---- issue every load of the tile first (bytes in flight) ----
+#pragma unroll
+    for (int j = 0; j < PAIRS; j++) {
+      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+#pragma unroll
+      for (int s = 0; s < S; s++)
+        ld_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, v[j][0][s], v[j][1][s]);
+      if constexpr (MODE >= 1) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[j][0], mi[j][1]);
+      else mi[j][0] = mi[j][1] = kFull;
+      if constexpr (MODE == 2) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[j][0], mo[j][1]);
+      else mo[j][0] = mo[j][1] = 0;
+      if (a.learner) ld_mask_pair<MT, VEC>(a.learner, g0, G, ml[j][0], ml[j][1]);
+      else ml[j][0] = ml[j][1] = 0;
+      if (a.voted) {
+        ld_mask_pair<MT, VEC>(a.voted, g0, G, vd[j][0], vd[j][1]);
+        if (a.granted) ld_mask_pair<MT, VEC>(a.granted, g0, G, gr[j][0], gr[j][1]);
+        else gr[j][0] = gr[j][1] = 0;
+      } else {
+        vd[j][0] = vd[j][1] = gr[j][0] = gr[j][1] = 0;
+      }
+    }
+    // ---- compute + store ----
+#pragma unroll
+    for (int j = 0; j < PAIRS; j++) {
+      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+      uint64_t c[2];
+      uint32_t vt[2], gc[2], rc[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t inc = mi[j][h] & kFull, out = mo[j][h] & kFull, lrn = ml[j][h] & kFull;
+        const uint32_t vv = vd[j][h] & kFull, gg = gr[j][h] & kFull;
+        eval_group<S, MODE>(v[j][h], inc, out, lrn, vv, gg, c[h], vt[h], gc[h], rc[h]);
+        if (want_stats && g0 + h < G) {
+          cnt[C_GROUPS] += 1;
+          cnt[C_INF] += (c[h] == kInf);
+          cnt[C_SUM] += (c[h] == kInf) ? 0 : c[h];
+          cnt[C_ZERO] += (c[h] == 0);
+          cnt[C_WON] += (vt[h] == kVoteWon);
+          cnt[C_LOST] += (vt[h] == kVoteLost);
+          cnt[C_PEND] += (vt[h] == kVotePending);
+          cnt[C_GR] += gc[h];
+          cnt[C_RJ] += rc[h];
+          cnt[C_VIOL] += ((lrn & (inc | out)) != 0);
+          const uint64_t tag = static_cast<uint64_t>(vt[h] | (gc[h] << 2) | (rc[h] << 7)) << 52;
+          cnt[C_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
+        }
+      }
+      if (a.commit) st_u64_pair<VEC>(a.commit, g0, G, c[0], c[1]);
+      if (a.vote) st_u8_pair<VEC>(a.vote, g0, G, vt[0], vt[1]);
+      if (a.gcount) st_u8_pair<VEC>(a.gcount, g0, G, gc[0], gc[1]);
+      if (a.rcount) st_u8_pair<VEC>(a.rcount, g0, G, rc[0], rc[1]);
+    }
+  }
+  if (want_stats) {
+    const int idx[C_N] = {QE_STAT_GROUPS,     QE_STAT_COMMIT_INF,   QE_STAT_COMMIT_SUM,
+                          QE_STAT_COMMIT_ZERO, QE_STAT_VOTE_WON,    QE_STAT_VOTE_LOST,
+                          QE_STAT_VOTE_PENDING, QE_STAT_GRANTED,    QE_STAT_REJECTED,
+                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
+    block_stats_add<C_N, kBlock>(cnt, idx, a.stats);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Lockstep replication round (qe_replication_round).
+// ---------------------------------------------------------------------------
+struct RArgs {
+  uint64_t G, goff, stride;
+  uint64_t *match, *next, *committed;
+  const uint64_t *term_start, *last_index, *resp;
+  const void *inc, *out, *resp_mask, *read_acks;
+  uint8_t *read_ok, *adv;
+  uint64_t *stats;
+};
+
+enum { R_GROUPS, R_SUM, R_ADV, R_READ, R_VIOL, R_CSUM, R_N };
+
+template <int S, bool JOINT, bool MASKED, typename MT, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * kBlock) >> 6;
+  const uint64_t G = a.G;
+  const uint64_t npairs = (G + 1) >> 1;
+  const uint64_t ntiles = (npairs + 63) / 64;
+  const bool want_stats = a.stats != nullptr;
+  uint64_t cnt[R_N];
+#pragma unroll
+  for (int i = 0; i < R_N; i++) cnt[i] = 0;
+
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = 2 * (t * 64 + lane);
+    uint64_t m[2][S], n[2][S], r[2][S];
+    uint32_t mi[2], mo[2], rm[2], ack[2];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      ld_u64_pair<VEC, false>(a.match + s * a.stride, g0, G, m[0][s], m[1][s]);
+      ld_u64_pair<VEC, false>(a.next + s * a.stride, g0, G, n[0][s], n[1][s]);
+      ld_u64_pair<VEC, false>(a.resp + s * a.stride, g0, G, r[0][s], r[1][s]);
+    }
+    if (MASKED) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[0], mi[1]);
+    else mi[0] = mi[1] = kFull;
+    if (JOINT) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[0], mo[1]);
+    else mo[0] = mo[1] = 0;
+    if (a.resp_mask) ld_mask_pair<MT, VEC>(a.resp_mask, g0, G, rm[0], rm[1]);
+    else rm[0] = rm[1] = 0;
+    if (a.read_acks) ld_mask_pair<MT, VEC>(a.read_acks, g0, G, ack[0], ack[1]);
+    else ack[0] = ack[1] = 0;
+    uint64_t ts[2], li[2], cm[2];
+    ld_u64_pair<VEC, false>(a.term_start, g0, G, ts[0], ts[1]);
+    ld_u64_pair<VEC, false>(a.last_index, g0, G, li[0], li[1]);
+    ld_u64_pair<VEC, false>(a.committed, g0, G, cm[0], cm[1]);
+
+    uint32_t ro[2], adv[2];
+    uint64_t sel[2][S];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      // Progress.MaybeUpdate on every responding slot (progress.go:144-153)
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const bool resp = (rm[h] >> s) & 1u;
+        const uint64_t x = r[h][s];
+        m[h][s] = (resp && m[h][s] < x) ? x : m[h][s];
+        n[h][s] = (resp && n[h][s] < x + 1) ? x + 1 : n[h][s];
+        sel[h][s] = m[h][s];
+      }
+      const uint32_t inc = mi[h] & kFull, out = mo[h] & kFull;
+      const uint64_t mci = (!JOINT && !MASKED) ? select_fixed<S>(sel[h])
+                                               : joint_committed<S>(sel[h], inc, out);
+      // raftLog.maybeCommit with term(i)==Term <=> term_start<=i<=last_index
+      adv[h] = (mci > cm[h] && mci >= ts[h] && mci <= li[h]) ? 1u : 0u;
+      cm[h] = adv[h] ? mci : cm[h];
+      const uint32_t acks = ack[h] & kFull;
+      ro[h] = a.read_acks ? (joint_vote(inc, out, acks, acks) == kVoteWon) : 0u;
+      if (want_stats && g0 + h < G) {
+        cnt[R_GROUPS] += 1;
+        cnt[R_SUM] += cm[h];
+        cnt[R_ADV] += adv[h];
+        cnt[R_READ] += ro[h];
+        cnt[R_VIOL] += (mci > li[h]);
+        const uint64_t tag = (static_cast<uint64_t>(ro[h]) << 62) | (static_cast<uint64_t>(adv[h]) << 61);
+        cnt[R_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ cm[h] ^ tag);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      st_u64_pair<VEC>(a.match + s * a.stride, g0, G, m[0][s], m[1][s]);
+      st_u64_pair<VEC>(a.next + s * a.stride, g0, G, n[0][s], n[1][s]);
+    }
+    st_u64_pair<VEC>(a.committed, g0, G, cm[0], cm[1]);
+    if (a.read_ok) st_u8_pair<VEC>(a.read_ok, g0, G, ro[0], ro[1]);
+    if (a.adv) st_u8_pair<VEC>(a.adv, g0, G, adv[0], adv[1]);
+  }
+  if (want_stats) {
+    const int idx[R_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
+                          QE_STAT_READ_RELEASED, QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
+    block_stats_add<R_N, kBlock>(cnt, idx, a.stats);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Randomized election simulation (qe_election_steps).  Group state stays in
+// registers across `steps` fused steps; ALU/RNG-bound.
+// ---------------------------------------------------------------------------
+struct EArgs {
+  uint64_t G, goff;
+  uint64_t *term;
+  uint8_t *state;
+  void *voted, *granted;
+  const uint8_t *self_slot;
+  const void *inc, *out, *learner;
+  uint64_t seed, step0;
+  uint32_t steps, p_drop, p_grant;
+  uint64_t *stats;
+};
+
+enum { E_GROUPS, E_ELEC, E_LEAD, E_DOWN, E_WON, E_LOST, E_PEND, E_GR, E_RJ, E_VIOL, E_CSUM, E_N };
+
+__device__ __forceinline__ void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd,
+                                           uint32_t gr, uint32_t gbefore, uint32_t &sta,
+                                           uint64_t (&cnt)[E_N]) {
+  const uint32_t voters = (mi | mo) & ~ml;
+  const uint32_t gcn = popc(vd & gr & voters), rcn = popc(vd & ~gr & voters);
+  const uint32_t res = joint_vote(mi, mo, vd, gr);
+  const uint32_t sym = joint_vote(mo, mi, vd, gr);
+  const uint32_t n0 = popc(mi), n1 = popc(mo);
+  const bool won_ok = (n0 == 0 || popc(gr & vd & mi) >= n0 / 2 + 1) &&
+                      (n1 == 0 || popc(gr & vd & mo) >= n1 / 2 + 1);
+  cnt[E_VIOL] += (sym != res) + (res == kVoteWon && !won_ok) + (gcn < gbefore);
+  cnt[E_GR] += gcn;
+  cnt[E_RJ] += rcn;
+  cnt[E_WON] += (res == kVoteWon);
+  cnt[E_LEAD] += (res == kVoteWon);
+  cnt[E_LOST] += (res == kVoteLost);
+  cnt[E_DOWN] += (res == kVoteLost);
+  cnt[E_PEND] += (res == kVotePending);
+  sta = res == kVoteWon ? QE_STATE_LEADER : (res == kVoteLost ? QE_STATE_FOLLOWER : sta);
+}
+
+template <int S, typename MT>
+__global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * kBlock;
+  uint64_t cnt[E_N];
+#pragma unroll
+  for (int i = 0; i < E_N; i++) cnt[i] = 0;
+  const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
+  const MT *lrnp = static_cast<const MT *>(a.learner);
+  MT *vdp = static_cast<MT *>(a.voted), *grp = static_cast<MT *>(a.granted);
+
+  for (uint64_t g = tid; g < a.G; g += nthreads) {
+    const uint64_t gid = a.goff + g;
+    const uint32_t mi = incp ? (incp[g] & kFull) : kFull;
+    const uint32_t mo = outp ? (outp[g] & kFull) : 0u;
+    const uint32_t ml = lrnp ? (lrnp[g] & kFull) : 0u;
+    const uint32_t self = 1u << (a.self_slot[g] % S);
+    const uint32_t prog = mi | mo | ml;
+    const bool promotable = (self & (mi | mo)) != 0 && (self & ml) == 0;
+    uint64_t t = a.term[g];
+    uint32_t sta = a.state[g];
+    uint32_t vd = vdp[g] & kFull, gr = grp[g] & kFull;
+    const uint32_t others = prog & ~self;
+    for (uint32_t k = 0; promotable && k < a.steps; k++) {
+      const uint64_t step = a.step0 + k;
+      if (sta != QE_STATE_CANDIDATE) {
+        // hup -> campaign: becomeCandidate (term+1, ResetVotes), self-vote.
+        t += 1;
+        vd = self;
+        gr = self;
+        sta = QE_STATE_CANDIDATE;
+        cnt[E_ELEC] += 1;
+        elec_tally(mi, mo, ml, vd, gr, 0u, sta, cnt);
+      } else {
+        const uint64_t h = hash4(a.seed, gid, static_cast<uint32_t>(step),
+                                 3u + static_cast<uint32_t>(step >> 32));
+        uint32_t resp = 0, val = 0;
+#pragma unroll
+        for (int j = 0; j < (S + 1) / 2; j++) {
+          const uint64_t hs = mix64(h + static_cast<uint64_t>(j + 1) * kPhi);
+#pragma unroll
+          for (int e = 0; e < 2; e++) {
+            const int s = 2 * j + e;
+            if (s >= S) break;
+            const uint32_t d = static_cast<uint32_t>(hs >> (32 * e));
+            const bool deliver = ((others >> s) & 1u) && (d & 0xFFFFu) >= a.p_drop;
+            resp |= deliver ? (1u << s) : 0u;
+            val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
+          }
+        }
+        const uint32_t gbefore = popc(gr & vd & ~ml & (mi | mo));
+        const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
+        vd |= fresh;
+        gr |= fresh & val;
+        elec_tally(mi, mo, ml, vd, gr, gbefore, sta, cnt);
+      }
+      cnt[E_GROUPS] += 1;
+    }
+    a.term[g] = t;
+    a.state[g] = static_cast<uint8_t>(sta);
+    vdp[g] = static_cast<MT>(vd);
+    grp[g] = static_cast<MT>(gr);
+    const uint64_t tag = (static_cast<uint64_t>(sta) << 62) | (static_cast<uint64_t>(vd) << 40) |
+                         (static_cast<uint64_t>(gr) << 24);
+    cnt[E_CSUM] += mix64((gid * kPhi) ^ t ^ tag);
+  }
+  if (a.stats) {
+    const int idx[E_N] = {QE_STAT_GROUPS,    QE_STAT_ELECTIONS,  QE_STAT_LEADERS,
+                          QE_STAT_STEPDOWNS, QE_STAT_VOTE_WON,   QE_STAT_VOTE_LOST,
+                          QE_STAT_VOTE_PENDING, QE_STAT_GRANTED, QE_STAT_REJECTED,
+                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
+    block_stats_add<E_N, kBlock>(cnt, idx, a.stats);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small bitmap kernels: QuorumActive, RecordVote.
+// ---------------------------------------------------------------------------
+template <typename MT>
+__global__ __launch_bounds__(kBlock) void k_quorum_active(uint64_t G, uint32_t full,
+                                                          const void *inc, const void *out,
+                                                          const void *learner,
+                                                          const void *recent, uint8_t *active) {
+  const MT *pi = static_cast<const MT *>(inc), *po = static_cast<const MT *>(out);
+  const MT *pl = static_cast<const MT *>(learner), *pr = static_cast<const MT *>(recent);
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t mi = pi ? (pi[g] & full) : full, mo = po ? (po[g] & full) : 0u;
+    const uint32_t ml = pl ? (pl[g] & full) : 0u;
+    const uint32_t present = (mi | mo | ml) & ~ml;  // votes[id] for non-learners
+    const uint32_t ra = pr[g] & present;
+    active[g] = joint_vote(mi, mo, present, ra) == kVoteWon;
+  }
+}
+
+template <typename MT>
+__global__ __launch_bounds__(kBlock) void k_vote_result(uint64_t G, uint32_t full,
+                                                        const void *inc, const void *out,
+                                                        const void *voted, const void *granted,
+                                                        uint8_t *vote) {
+  const MT *pi = static_cast<const MT *>(inc), *po = static_cast<const MT *>(out);
+  const MT *pv = static_cast<const MT *>(voted), *pg = static_cast<const MT *>(granted);
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t mi = pi ? (pi[g] & full) : full, mo = po ? (po[g] & full) : 0u;
+    const uint32_t vd = pv ? (pv[g] & full) : 0u;
+    const uint32_t gr = (pv && pg) ? (pg[g] & full) : 0u;
+    vote[g] = static_cast<uint8_t>(joint_vote(mi, mo, vd, gr));
+  }
+}
+
+template <typename MT>
+__global__ __launch_bounds__(kBlock) void k_record_votes(uint64_t G, uint32_t full, void *voted,
+                                                         void *granted, const void *resp,
+                                                         const void *value) {
+  MT *pv = static_cast<MT *>(voted), *pg = static_cast<MT *>(granted);
+  const MT *pr = static_cast<const MT *>(resp), *px = static_cast<const MT *>(value);
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t vd = pv[g], fresh = pr[g] & full & ~vd;
+    pv[g] = static_cast<MT>(vd | fresh);
+    pg[g] = static_cast<MT>(pg[g] | (fresh & px[g]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic generator (bit-identical with oracle/quorum_oracle.c).
+// ---------------------------------------------------------------------------
+struct GArgs {
+  uint64_t G, goff, stride;
+  uint32_t S;
+  uint64_t *match;
+  void *inc, *out, *learner, *voted, *granted;
+  qe_gen_params p;
+};
+
+__device__ __forceinline__ uint32_t rotl_s(uint32_t m, uint32_t r, uint32_t S) {
+  const uint32_t full = (1u << S) - 1u;
+  m &= full;
+  if (r == 0) return m;
+  return ((m << r) | (m >> (S - r))) & full;
+}
+
+template <typename MT>
+__global__ __launch_bounds__(kBlock) void k_gen(GArgs a) {
+  const uint32_t S = a.S;
+  const uint32_t full = (1u << S) - 1u;
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint64_t gid = a.goff + g;
+    const uint64_t hb = hash4(a.p.seed, gid, 0xFFFFu, 0);
+    uint32_t mi, mo, ml;
+    if (a.p.mask_mode == 0) {
+      uint32_t ni = a.p.n_inc ? a.p.n_inc : S;
+      if (ni > S) ni = S;
+      uint32_t no = a.p.n_out > S ? S : a.p.n_out;
+      if (no == 0) {
+        mi = (1u << ni) - 1u;
+        mo = 0;
+        ml = full & ~mi;
+      } else {
+        const uint32_t omin = (ni + no > S) ? ni + no - S : 0;
+        const uint32_t omax = ni < no ? ni : no;
+        const uint32_t o = omin + static_cast<uint32_t>((hb >> 8) % (omax - omin + 1));
+        const uint32_t uni = ni + no - o;
+        mi = (1u << ni) - 1u;
+        mo = ((1u << no) - 1u) << (ni - o);
+        ml = full & ~((1u << uni) - 1u);
+      }
+      const uint32_t r = static_cast<uint32_t>((hb >> 16) % S);
+      mi = rotl_s(mi, r, S);
+      mo = rotl_s(mo, r, S);
+      ml = rotl_s(ml, r, S);
+    } else {
+      const uint64_t hm = hash4(a.p.seed, gid, 0xFFFEu, 0);
+      mi = static_cast<uint32_t>(hm) & full;
+      mo = ((hm >> 48) & 3u) == 0 ? 0u : (static_cast<uint32_t>(hm >> 16) & full);
+      ml = static_cast<uint32_t>(hm >> 32) & full;
+      if (((hm >> 50) & 7u) != 0) ml &= ~(mi | mo);
+    }
+    if (a.inc) static_cast<MT *>(a.inc)[g] = static_cast<MT>(mi);
+    if (a.out) static_cast<MT *>(a.out)[g] = static_cast<MT>(mo);
+    if (a.learner) static_cast<MT *>(a.learner)[g] = static_cast<MT>(ml);
+    if (a.match) {
+      for (uint32_t s = 0; s < S; s++) {
+        const uint64_t h = hash4(a.p.seed, gid, s, 1);
+        uint64_t v;
+        if (static_cast<uint32_t>(h & 0xFFFFu) < a.p.p_absent_q16) v = 0;
+        else if (a.p.dist == 0) v = (hb >> 2) + ((h >> 40) & 0xFFFFu);
+        else if (a.p.dist == 1) v = h >> 1;
+        else v = (h >> 40) & 3u;
+        a.match[s * a.stride + g] = v;
+      }
+    }
+    if (a.voted || a.granted) {
+      uint32_t vd = 0, gr = 0;
+      for (uint32_t s = 0; s < S; s++) {
+        const uint64_t h = hash4(a.p.seed, gid, s, 2);
+        if (static_cast<uint32_t>(h & 0xFFFFu) < a.p.p_voted_q16) {
+          vd |= 1u << s;
+          if (static_cast<uint32_t>((h >> 16) & 0xFFFFu) < a.p.p_granted_q16) gr |= 1u << s;
+        }
+      }
+      if (a.voted) static_cast<MT *>(a.voted)[g] = static_cast<MT>(vd);
+      if (a.granted) static_cast<MT *>(a.granted)[g] = static_cast<MT>(gr);
+    }
+  }
+}
+
+}  // namespace qe

@@ -1,0 +1,255 @@
+"""Device-buffer layer over the C ABI: slot-SoA batches held in HBM as torch
+tensors (torch is plumbing here: allocation, streams, distributed), and thin
+callers of every qe_* entry point.
+
+Layout: match is [S][stride] uint64 (stored as int64 bits),
+masks/bitmaps are uint8 for S <= 8 and uint16 (stored as int16) for S <= 16.
+`stride` is rounded up to 64 groups so every slot row starts 512-byte aligned
+and the 16-byte vector path is always taken.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (QeElectionParams, QeElectionState, QeGenParams, QeGroups, QeOutputs,
+                   QeReplMsgs, QeReplState, check)
+
+ROW_ALIGN = 64
+
+
+def mask_torch_dtype(S):
+    return torch.uint8 if S <= 8 else torch.int16
+
+
+def mask_np_dtype(S):
+    return np.uint8 if S <= 8 else np.uint16
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _np_u64(t):
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+class SlotBatch:
+    """G Raft groups in slot-SoA form on one device (the qe_groups view)."""
+
+    def __init__(self, G, S, device="cuda", masks=("inc", "out", "learner"), votes=True,
+                 group_offset=0, stride=None):
+        if not 1 <= S <= _lib.QE_MAX_SLOTS:
+            raise ValueError(f"num_slots must be 1..{_lib.QE_MAX_SLOTS}")
+        self.G, self.S = int(G), int(S)
+        self.device = torch.device(device)
+        self.group_offset = int(group_offset)
+        self.stride = int(stride) if stride else max(ROW_ALIGN, -(-self.G // ROW_ALIGN) * ROW_ALIGN)
+        md = mask_torch_dtype(S)
+        dev = self.device
+        self.match = torch.zeros(self.S * self.stride, dtype=torch.int64, device=dev)
+        self.inc = torch.zeros(self.G, dtype=md, device=dev) if "inc" in masks else None
+        self.out = torch.zeros(self.G, dtype=md, device=dev) if "out" in masks else None
+        self.learner = torch.zeros(self.G, dtype=md, device=dev) if "learner" in masks else None
+        self.voted = torch.zeros(self.G, dtype=md, device=dev) if votes else None
+        self.granted = torch.zeros(self.G, dtype=md, device=dev) if votes else None
+
+    # -- views --------------------------------------------------------------
+    def struct(self):
+        return QeGroups(self.G, self.group_offset, self.S, 0, self.stride, _ptr(self.match),
+                        _ptr(self.inc), _ptr(self.out), _ptr(self.learner), _ptr(self.voted),
+                        _ptr(self.granted))
+
+    def bytes_per_group(self, with_outputs=True):
+        """Algorithmic bytes one qe_commit_vote evaluation moves per group."""
+        mb = 1 if self.S <= 8 else 2
+        b = 8 * self.S
+        b += mb * sum(x is not None for x in (self.inc, self.out, self.learner, self.voted,
+                                                self.granted))
+        if with_outputs:
+            b += 8 + 1
+        return b
+
+    def match_rows(self):
+        """[S][G] view of the match array."""
+        return self.match.view(self.S, self.stride)[:, : self.G]
+
+    # -- host transfer ------------------------------------------------------
+    def load_host(self, match, inc=None, out=None, learner=None, voted=None, granted=None):
+        """match: uint64 array [S][G] (or [S][stride]); masks: [G] arrays."""
+        m = np.ascontiguousarray(np.asarray(match, dtype=np.uint64)).reshape(self.S, -1)
+        rows = self.match_rows()
+        rows.copy_(torch.from_numpy(m[:, : self.G].view(np.int64).copy()).to(self.device))
+        md = mask_np_dtype(self.S)
+        for name, arr in (("inc", inc), ("out", out), ("learner", learner), ("voted", voted),
+                          ("granted", granted)):
+            dst = getattr(self, name)
+            if arr is None or dst is None:
+                continue
+            a = np.ascontiguousarray(np.asarray(arr).astype(md))
+            if md == np.uint16:
+                a = a.view(np.int16)
+            dst.copy_(torch.from_numpy(a).to(self.device))
+        return self
+
+    def host(self):
+        """Return a dict of numpy arrays (match as [S][G] uint64)."""
+        md = mask_np_dtype(self.S)
+        out = {"match": self.match_rows().cpu().numpy().view(np.uint64)}
+        for name in ("inc", "out", "learner", "voted", "granted"):
+            t = getattr(self, name)
+            out[name] = None if t is None else t.cpu().numpy().view(md)
+        return out
+
+
+def stats_buffer(device="cuda"):
+    return torch.zeros(_lib.QE_STATS_WORDS, dtype=torch.int64, device=device)
+
+
+def stats_reduce(stats):
+    """Fold the shards of a stats buffer on device -> int64[16] tensor."""
+    out = torch.empty(_lib.QE_STATS_COUNTERS, dtype=torch.int64, device=stats.device)
+    check("qe_stats_reduce", _lib.lib().qe_stats_reduce(_ptr(stats), _ptr(out),
+                                                         _stream(stats.device)))
+    return out
+
+
+def stats_dict(folded):
+    v = folded.detach().cpu().numpy().view(np.uint64)
+    return {name: int(v[i]) for i, name in enumerate(_lib.STAT_NAMES)}
+
+
+def gen_groups(batch, seed, dist=0, p_absent=3277, p_voted=52429, p_granted=39322, n_inc=0,
+               n_out=0, mask_mode=0):
+    """Fill `batch` with the counter-based synthetic generator."""
+    p = QeGenParams(seed, 0, dist, p_absent, p_voted, p_granted, n_inc, n_out, mask_mode, 0)
+    g = batch.struct()
+    check("qe_gen_groups", _lib.lib().qe_gen_groups(C.byref(g), C.byref(p),
+                                                     _stream(batch.device)))
+    return batch
+
+
+class Outputs:
+    def __init__(self, G, device, commit=True, vote=True, tally=True):
+        self.commit = torch.empty(G, dtype=torch.int64, device=device) if commit else None
+        self.vote = torch.empty(G, dtype=torch.uint8, device=device) if vote else None
+        self.granted = torch.empty(G, dtype=torch.uint8, device=device) if tally else None
+        self.rejected = torch.empty(G, dtype=torch.uint8, device=device) if tally else None
+
+    def struct(self, stats=None):
+        return QeOutputs(_ptr(self.commit), _ptr(self.vote), _ptr(self.granted),
+                         _ptr(self.rejected), _ptr(stats))
+
+
+def commit_vote(batch, outputs=None, stats=None):
+    """ProgressTracker.Committed + TallyVotes for every group (qe_commit_vote)."""
+    if outputs is None:
+        outputs = Outputs(batch.G, batch.device)
+    g = batch.struct()
+    o = outputs.struct(stats)
+    check("qe_commit_vote", _lib.lib().qe_commit_vote(C.byref(g), C.byref(o),
+                                                       _stream(batch.device)))
+    return outputs
+
+
+def committed_index(batch, commit=None):
+    commit = torch.empty(batch.G, dtype=torch.int64, device=batch.device) if commit is None else commit
+    g = batch.struct()
+    check("qe_committed_index", _lib.lib().qe_committed_index(C.byref(g), _ptr(commit),
+                                                               _stream(batch.device)))
+    return commit
+
+
+def vote_result(batch, vote=None):
+    vote = torch.empty(batch.G, dtype=torch.uint8, device=batch.device) if vote is None else vote
+    g = batch.struct()
+    check("qe_vote_result", _lib.lib().qe_vote_result(C.byref(g), _ptr(vote),
+                                                       _stream(batch.device)))
+    return vote
+
+
+def quorum_active(batch, recent_active, active=None):
+    active = torch.empty(batch.G, dtype=torch.uint8, device=batch.device) if active is None else active
+    g = batch.struct()
+    check("qe_quorum_active", _lib.lib().qe_quorum_active(C.byref(g), _ptr(recent_active),
+                                                           _ptr(active), _stream(batch.device)))
+    return active
+
+
+def record_votes(batch, resp_mask, resp_value):
+    check("qe_record_votes", _lib.lib().qe_record_votes(
+        batch.G, batch.S, _ptr(batch.voted), _ptr(batch.granted), _ptr(resp_mask),
+        _ptr(resp_value), _stream(batch.device)))
+
+
+class ReplicationState:
+    """Leader-side Progress state of G groups for qe_replication_round."""
+
+    def __init__(self, batch, committed, term_start, last_index, nxt=None):
+        self.batch = batch
+        self.match = batch.match
+        self.next = nxt if nxt is not None else batch.match.clone() + 1
+        self.committed = committed
+        self.term_start = term_start
+        self.last_index = last_index
+
+    def struct(self):
+        b = self.batch
+        return QeReplState(b.G, b.group_offset, b.S, 0, b.stride, _ptr(self.match),
+                           _ptr(self.next), _ptr(self.committed), _ptr(self.term_start),
+                           _ptr(self.last_index), _ptr(b.inc), _ptr(b.out))
+
+
+def replication_round(state, resp_index, resp_mask, read_acks=None, read_ok=None, adv=None,
+                      stats=None):
+    m = QeReplMsgs(_ptr(resp_index), _ptr(resp_mask), _ptr(read_acks), _ptr(read_ok), _ptr(adv))
+    s = state.struct()
+    check("qe_replication_round", _lib.lib().qe_replication_round(
+        C.byref(s), C.byref(m), _ptr(stats), _stream(state.batch.device)))
+
+
+class ElectionState:
+    """Per-group candidate state for qe_election_steps."""
+
+    def __init__(self, batch, self_slot):
+        G, dev = batch.G, batch.device
+        self.batch = batch
+        self.term = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.state = torch.zeros(G, dtype=torch.uint8, device=dev)
+        self.voted = torch.zeros(G, dtype=mask_torch_dtype(batch.S), device=dev)
+        self.granted = torch.zeros(G, dtype=mask_torch_dtype(batch.S), device=dev)
+        self.self_slot = self_slot
+
+    def struct(self):
+        b = self.batch
+        return QeElectionState(b.G, b.group_offset, b.S, 0, _ptr(self.term), _ptr(self.state),
+                               _ptr(self.voted), _ptr(self.granted), _ptr(self.self_slot),
+                               _ptr(b.inc), _ptr(b.out), _ptr(b.learner))
+
+
+def first_voter_slot(batch):
+    """self_slot = lowest slot of JointConfig[0] (device computation)."""
+    inc = batch.inc.to(torch.int32) & ((1 << batch.S) - 1)
+    slot = torch.zeros(batch.G, dtype=torch.uint8, device=batch.device)
+    found = torch.zeros(batch.G, dtype=torch.bool, device=batch.device)
+    for s in range(batch.S):
+        bit = ((inc >> s) & 1).bool() & ~found
+        slot = torch.where(bit, torch.full_like(slot, s), slot)
+        found |= bit
+    return slot
+
+
+def election_steps(est, seed, step0, steps, p_drop=13107, p_grant=32768, stats=None):
+    p = QeElectionParams(seed, step0, steps, p_drop, p_grant, 0)
+    s = est.struct()
+    check("qe_election_steps", _lib.lib().qe_election_steps(C.byref(s), C.byref(p), _ptr(stats),
+                                                             _stream(est.batch.device)))
+
+
+def tune(key, value):
+    check("qe_tune", _lib.lib().qe_tune(key.encode(), int(value)))

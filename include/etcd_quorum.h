@@ -1,0 +1,276 @@
+/*
+ * etcd_quorum.h — C ABI of the MI355X batched Raft quorum engine.
+ *
+ * This is the drop-in boundary for etcd's raft/quorum + raft/tracker hot path
+ * (reference: /root/reference/raft, etcd 3.6.0-pre).  The per-group Go API
+ * (MajorityConfig / JointConfig / ProgressTracker) stays the semantic
+ * reference; every entry point below evaluates the same decision for G
+ * independent Raft groups in one call on the GPU.  See INTEGRATION.md for the
+ * cgo binding a maintainer adds next to raft/quorum.
+ *
+ * Data model ("slot SoA")
+ *   A group's peers (voters of both halves, learners) are packed into S <= 16
+ *   slots.  Slot order is arbitrary: every function here is an order-free set
+ *   function of the (voter set, per-voter value) pairs, exactly like the Go
+ *   code which iterates maps (raft/quorum/majority.go:155-161 fills then sorts).
+ *
+ *   match    uint64 [S][stride]   Progress.Match per slot; "absent" (no acked
+ *                                 index, AckedIndexer.found == false) is 0,
+ *                                 which CommittedIndex treats identically
+ *                                 (raft/quorum/majority.go:150-161).
+ *   masks    per-group slot bitmaps; element type is uint8_t when S <= 8 and
+ *            uint16_t when 9 <= S <= 16 (qe_mask_bytes(S)).
+ *            inc_mask  = JointConfig[0] (incoming voters)
+ *            out_mask  = JointConfig[1] (outgoing voters; NULL = not joint)
+ *            learner_mask = tracker.Config.Learners (optional)
+ *            voted / granted = ProgressTracker.Votes: bit s of voted set iff
+ *            slot s has a recorded vote, bit s of granted = that vote's value.
+ *            A NULL inc_mask means "all S slots are voters" (fixed-size
+ *            MajorityConfig, the BenchmarkMajorityConfig_CommittedIndex shape).
+ *
+ * Conventions
+ *   - Index infinity (math.MaxUint64, raft/quorum/quorum.go:25-30) is
+ *     QE_INDEX_INF.
+ *   - VoteResult uses the reference's numeric encoding
+ *     VotePending=1, VoteLost=2, VoteWon=3 (raft/quorum/quorum.go:48-58).
+ *   - All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless
+ *     the parameter says host.  The library allocates nothing and retains
+ *     nothing; `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *     asynchronous on `stream` and reentrant on distinct buffers.
+ *   - Return value: QE_OK or a negative QE_E* code.  num_groups == 0 is a
+ *     successful no-op.  Semantic "panics" of the reference become counters
+ *     in the optional stats buffer, never aborts.
+ *   - Alignment: match/next/commit arrays 16-byte aligned and stride even
+ *     take the vectorised path; anything else is still correct (scalar path).
+ */
+#ifndef ETCD_QUORUM_H
+#define ETCD_QUORUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QE_ABI_VERSION 1
+
+#define QE_INDEX_INF UINT64_MAX
+#define QE_MAX_SLOTS 16
+
+/* quorum.VoteResult (raft/quorum/quorum.go:48-58) */
+#define QE_VOTE_PENDING 1
+#define QE_VOTE_LOST 2
+#define QE_VOTE_WON 3
+
+/* Raft StateType subset used by the election simulation (raft/raft.go:
+ * StateFollower=0, StateCandidate=1, StateLeader=2, StatePreCandidate=3). */
+#define QE_STATE_FOLLOWER 0
+#define QE_STATE_CANDIDATE 1
+#define QE_STATE_LEADER 2
+
+/* Status codes */
+#define QE_OK 0
+#define QE_EINVAL (-22)  /* null pointer / bad size / S out of range   */
+#define QE_ERANGE (-34)  /* value out of supported range                */
+#define QE_EHIP (-1000)  /* HIP launch / runtime error                  */
+
+/* Aggregate statistics.  A stats buffer is uint64[QE_STATS_WORDS]; kernels
+ * add into QE_STATS_SHARDS shards of QE_STATS_COUNTERS counters (one 128-byte
+ * line per shard) to avoid a single hot atomic line.  qe_stats_reduce() folds
+ * the shards.  Counters accumulate across calls until the caller zeroes the
+ * buffer, so one all-reduce at the end of a run aggregates a whole job. */
+#define QE_STATS_COUNTERS 16
+#define QE_STATS_SHARDS 64
+#define QE_STATS_WORDS (QE_STATS_COUNTERS * QE_STATS_SHARDS)
+enum qe_stat {
+  QE_STAT_GROUPS = 0,        /* groups evaluated                              */
+  QE_STAT_COMMIT_INF = 1,    /* CommittedIndex == inf (empty config)          */
+  QE_STAT_COMMIT_SUM = 2,    /* sum of finite committed indexes (mod 2^64)    */
+  QE_STAT_COMMIT_ZERO = 3,   /* CommittedIndex == 0 (nothing committed)       */
+  QE_STAT_VOTE_WON = 4,
+  QE_STAT_VOTE_LOST = 5,
+  QE_STAT_VOTE_PENDING = 6,
+  QE_STAT_GRANTED = 7,       /* sum of TallyVotes granted                      */
+  QE_STAT_REJECTED = 8,      /* sum of TallyVotes rejected                     */
+  QE_STAT_COMMIT_ADVANCED = 9,   /* replication: commit advanced this round    */
+  QE_STAT_READ_RELEASED = 10,    /* replication: ReadIndex quorum reached      */
+  QE_STAT_ELECTIONS = 11,        /* election sim: campaigns started            */
+  QE_STAT_LEADERS = 12,          /* election sim: elections won                */
+  QE_STAT_STEPDOWNS = 13,        /* election sim: elections lost               */
+  QE_STAT_INVARIANT_VIOLATIONS = 14, /* learner∩voter≠∅, mci>lastIndex, ...  */
+  QE_STAT_CHECKSUM = 15          /* mixed hash of all outputs (order-free)     */
+};
+
+/* A batch of G groups in slot-SoA form (see header comment). */
+typedef struct qe_groups {
+  uint64_t num_groups;       /* G                                            */
+  uint64_t group_offset;     /* global id of group 0 (checksum key; shards)  */
+  uint32_t num_slots;        /* S, 1..16                                     */
+  uint32_t reserved;         /* must be 0                                    */
+  uint64_t stride;           /* elements between slot rows of match (>= G)   */
+  const uint64_t *match;     /* [S][stride] acked index per slot, 0 = absent */
+  const void *inc_mask;      /* [G] JointConfig[0]; NULL = all S slots       */
+  const void *out_mask;      /* [G] JointConfig[1]; NULL = non-joint         */
+  const void *learner_mask;  /* [G] Learners; NULL = none                    */
+  const void *voted;         /* [G] vote recorded bitmap; NULL = no votes    */
+  const void *granted;       /* [G] vote value bitmap; NULL = all "no"       */
+} qe_groups;
+
+/* Outputs of the fused evaluation.  Any pointer may be NULL to skip it. */
+typedef struct qe_outputs {
+  uint64_t *commit;          /* [G] JointConfig.CommittedIndex               */
+  uint8_t *vote;             /* [G] JointConfig.VoteResult (1/2/3)           */
+  uint8_t *granted_count;    /* [G] TallyVotes granted                       */
+  uint8_t *rejected_count;   /* [G] TallyVotes rejected                      */
+  uint64_t *stats;           /* uint64[QE_STATS_WORDS] accumulated, or NULL  */
+} qe_outputs;
+
+/* ---- introspection ---------------------------------------------------- */
+int qe_abi_version(void);
+const char *qe_strerror(int status);
+size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
+
+/* Optional launch tuning (no reference counterpart; never changes results):
+ *   "blocks_per_cu"  persistent-grid workgroups per CU, 1..32 (default 8)
+ *   "nontemporal"    0/1 non-temporal match loads in qe_commit_vote        */
+int qe_tune(const char *key, int value);
+
+/* ---- quorum decisions -------------------------------------------------- */
+
+/* Fused ProgressTracker.Committed + TallyVotes for every group:
+ *   commit[g] = Voters.CommittedIndex(match)           tracker.go:177-179,
+ *               joint.go:49-56, majority.go:126-172
+ *   vote[g]   = Voters.VoteResult(votes)               tracker.go:286,
+ *               joint.go:61-75, majority.go:178-210
+ *   granted/rejected_count[g] = TallyVotes counts over non-learner voters
+ *               tracker.go:267-285
+ * Replaces one AckedIndexer-driven CommittedIndex call plus one
+ * VoteResult(map) call per group (raft/quorum/majority.go:126, :178). */
+int qe_commit_vote(const qe_groups *groups, const qe_outputs *out,
+                   void *stream);
+
+/* JointConfig.CommittedIndex only (MajorityConfig when out_mask == NULL).
+ * raft/quorum/joint.go:49-56, raft/quorum/majority.go:126-172. */
+int qe_committed_index(const qe_groups *groups, uint64_t *commit,
+                       void *stream);
+
+/* JointConfig.VoteResult only; `voted`/`granted` give the votes map.
+ * raft/quorum/joint.go:61-75, raft/quorum/majority.go:178-210. */
+int qe_vote_result(const qe_groups *groups, uint8_t *vote, void *stream);
+
+/* ProgressTracker.QuorumActive (raft/tracker/tracker.go:215-225): every
+ * non-learner voter votes Progress.RecentActive; active[g] = 1 iff the
+ * result is VoteWon.  `recent_active` is a [G] slot bitmap (mask type). */
+int qe_quorum_active(const qe_groups *groups, const void *recent_active,
+                     uint8_t *active, void *stream);
+
+/* ProgressTracker.RecordVote (raft/tracker/tracker.go:258-263) for a batch of
+ * vote responses: for each group, slots in `resp_mask` cast vote
+ * `resp_value`; the first recorded vote per slot sticks.  Updates
+ * voted/granted in place (mask-typed [G] arrays). */
+int qe_record_votes(uint64_t num_groups, uint32_t num_slots, void *voted,
+                    void *granted, const void *resp_mask,
+                    const void *resp_value, void *stream);
+
+/* ---- lockstep replication round (BASELINE config 4) -------------------- */
+
+/* Device-resident leader-side state of G groups. */
+typedef struct qe_repl_state {
+  uint64_t num_groups;
+  uint64_t group_offset;     /* global id of group 0 (checksum key)          */
+  uint32_t num_slots;
+  uint32_t reserved;
+  uint64_t stride;           /* slot-row stride of match/next               */
+  uint64_t *match;           /* [S][stride] Progress.Match (rw)             */
+  uint64_t *next;            /* [S][stride] Progress.Next  (rw)             */
+  uint64_t *committed;       /* [G] raftLog.committed (rw)                  */
+  const uint64_t *term_start;/* [G] first index of the leader's term         */
+  const uint64_t *last_index;/* [G] raftLog.lastIndex()                      */
+  const void *inc_mask;      /* [G] as in qe_groups                          */
+  const void *out_mask;      /* [G] or NULL                                  */
+} qe_repl_state;
+
+/* One round of MsgAppResp / MsgHeartbeatResp handling per group. */
+typedef struct qe_repl_msgs {
+  const uint64_t *resp_index;/* [S][stride] MsgAppResp.Index per slot        */
+  const void *resp_mask;     /* [G] slots whose (non-reject) MsgAppResp came */
+  const void *read_acks;     /* [G] ReadIndex heartbeat acks (incl. self), or NULL */
+  uint8_t *read_ok;          /* [G] out: VoteResult(acks)==VoteWon, or NULL */
+  uint8_t *commit_advanced;  /* [G] out: maybeCommit() returned true, or NULL */
+} qe_repl_msgs;
+
+/* For each group: Progress.MaybeUpdate(resp) on every responding slot
+ * (raft/tracker/progress.go:144-153), then raft.maybeCommit
+ * (raft/raft.go:585-588 -> raft/log.go:325-331 -> commitTo log.go:233-241)
+ * with the synthetic log model term(i)==Term <=> term_start<=i<=last_index,
+ * then the ReadIndex quorum check VoteResult(acks)==VoteWon
+ * (raft/raft.go:1300, raft/read_only.go:68-76). */
+int qe_replication_round(const qe_repl_state *st, const qe_repl_msgs *msgs,
+                         uint64_t *stats, void *stream);
+
+/* ---- randomized election simulation (BASELINE config 5) ---------------- */
+
+typedef struct qe_election_state {
+  uint64_t num_groups;
+  uint64_t group_offset;     /* global id of group 0 (RNG key; sharding)     */
+  uint32_t num_slots;
+  uint32_t reserved;
+  uint64_t *term;            /* [G] rw                                       */
+  uint8_t *state;            /* [G] rw QE_STATE_*                            */
+  void *voted;               /* [G] rw mask-typed                            */
+  void *granted;             /* [G] rw mask-typed                            */
+  const uint8_t *self_slot;  /* [G] candidate's own slot                     */
+  const void *inc_mask;      /* [G]                                          */
+  const void *out_mask;      /* [G] or NULL                                  */
+  const void *learner_mask;  /* [G] or NULL (learners vote; never counted)   */
+} qe_election_state;
+
+typedef struct qe_election_params {
+  uint64_t seed;
+  uint64_t step0;            /* global step number of the first step         */
+  uint32_t steps;            /* fused steps per launch (state in registers)  */
+  uint32_t p_drop_q16;       /* P(response dropped) * 65536                  */
+  uint32_t p_grant_q16;      /* P(vote granted | delivered) * 65536          */
+  uint32_t reserved;
+} qe_election_params;
+
+/* `steps` election steps per group: Leader/Follower campaign
+ * (term+1, ResetVotes, self RecordVote; raft/raft.go:785-803), Candidate
+ * receives one round of MsgVoteResp (drops/grants from a counter-based RNG)
+ * -> RecordVote -> TallyVotes -> VoteWon: Leader, VoteLost: Follower
+ * (raft/raft.go:837-845, :1399-1414).  Invariant checks go to stats. */
+int qe_election_steps(const qe_election_state *st,
+                      const qe_election_params *p, uint64_t *stats,
+                      void *stream);
+
+/* ---- statistics -------------------------------------------------------- */
+
+/* out[QE_STATS_COUNTERS] (device) = sum over shards of stats (device). */
+int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream);
+
+/* ---- synthetic inputs (counter-based, bit-identical to oracle/) -------- */
+
+typedef struct qe_gen_params {
+  uint64_t seed;
+  uint64_t group_offset;     /* global id of group 0                         */
+  uint32_t dist;             /* 0 clustered, 1 uniform (Int63), 2 small ties */
+  uint32_t p_absent_q16;     /* P(slot has no acked index) * 65536           */
+  uint32_t p_voted_q16;      /* P(slot voted) * 65536                        */
+  uint32_t p_granted_q16;    /* P(granted | voted) * 65536                   */
+  uint32_t n_inc;            /* joint: incoming voters (0 = all S slots)     */
+  uint32_t n_out;            /* joint: outgoing voters (0 = non-joint)       */
+  uint32_t mask_mode;        /* 0 structured (config 3), 1 arbitrary random  */
+  uint32_t reserved;
+} qe_gen_params;
+
+/* Fill a qe_groups batch (the pointers inside `g` are written through; the
+ * const qualifiers of qe_groups are cast away).  Masks pointers that are
+ * NULL in `g` are skipped. */
+int qe_gen_groups(const qe_groups *g, const qe_gen_params *p, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ETCD_QUORUM_H */

@@ -1,0 +1,127 @@
+"""The C-ABI boundary: the library loads, exports every symbol
+include/etcd_quorum.h declares, its struct layouts agree with the ctypes
+mirror (checked by compiling the header with gcc), and argument errors are
+reported as status codes without touching the GPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from etcd_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "etcd_quorum.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(qe_\w+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for f in ["qe_commit_vote", "qe_committed_index", "qe_vote_result", "qe_quorum_active",
+              "qe_record_votes", "qe_replication_round", "qe_election_steps",
+              "qe_stats_reduce", "qe_gen_groups", "qe_abi_version", "qe_strerror",
+              "qe_mask_bytes", "qe_tune"]:
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = set(re.findall(r"\s[TW]\s+(qe_\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+    # ctypes prototypes cover the whole surface
+    assert set(declared_functions()) == set(_lib.PROTOTYPES)
+
+
+LAYOUT_PROG = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "etcd_quorum.h"
+#define F(T, m) printf(#T " " #m " %zu\n", offsetof(T, m));
+#define Z(T) printf(#T " sizeof %zu\n", sizeof(T));
+int main(void) {
+  Z(qe_groups) F(qe_groups, num_groups) F(qe_groups, group_offset) F(qe_groups, num_slots)
+  F(qe_groups, stride) F(qe_groups, match) F(qe_groups, granted)
+  Z(qe_outputs) F(qe_outputs, stats)
+  Z(qe_repl_state) F(qe_repl_state, stride) F(qe_repl_state, out_mask)
+  Z(qe_repl_msgs) F(qe_repl_msgs, commit_advanced)
+  Z(qe_election_state) F(qe_election_state, term) F(qe_election_state, learner_mask)
+  Z(qe_election_params) F(qe_election_params, steps) F(qe_election_params, p_grant_q16)
+  Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
+  return 0;
+}
+"""
+
+CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
+          "qe_repl_state": _lib.QeReplState, "qe_repl_msgs": _lib.QeReplMsgs,
+          "qe_election_state": _lib.QeElectionState,
+          "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams}
+
+
+def test_struct_layout_matches_header(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_PROG)
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)])
+    for line in subprocess.check_output([str(exe)], text=True).splitlines():
+        t, m, v = line.split()
+        cls = CTYPES[t]
+        if m == "sizeof":
+            assert C.sizeof(cls) == int(v), t
+        else:
+            assert getattr(cls, m).offset == int(v), (t, m)
+
+
+def test_constants_and_introspection():
+    L = _lib.lib()
+    assert L.qe_abi_version() == 1
+    assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
+    assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
+    assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0
+    assert L.qe_strerror(0) == b"ok"
+    assert L.qe_strerror(_lib.QE_EINVAL) == b"invalid argument"
+    src = open(HEADER).read()
+    for name, val in [("QE_VOTE_PENDING", 1), ("QE_VOTE_LOST", 2), ("QE_VOTE_WON", 3),
+                      ("QE_STATS_COUNTERS", 16), ("QE_STATS_SHARDS", 64), ("QE_EINVAL", -22)]:
+        m = re.search(rf"#define {name} \(?(-?\d+)\)?", src)
+        assert m and int(m.group(1)) == val, name
+
+
+def test_argument_errors_without_gpu():
+    """Validation happens before any HIP call, so these run on CPU."""
+    L = _lib.lib()
+    o = _lib.QeOutputs()
+    assert L.qe_commit_vote(None, C.byref(o), None) == _lib.QE_EINVAL
+    g = _lib.QeGroups(num_groups=10, num_slots=0, stride=10)
+    assert L.qe_commit_vote(C.byref(g), C.byref(o), None) == _lib.QE_EINVAL
+    g = _lib.QeGroups(num_groups=10, num_slots=17, stride=10)
+    assert L.qe_commit_vote(C.byref(g), C.byref(o), None) == _lib.QE_EINVAL
+    g = _lib.QeGroups(num_groups=10, num_slots=5, stride=5)  # stride < G
+    assert L.qe_commit_vote(C.byref(g), C.byref(o), None) == _lib.QE_EINVAL
+    g = _lib.QeGroups(num_groups=0, num_slots=5, stride=0)  # empty batch is a no-op
+    assert L.qe_commit_vote(C.byref(g), C.byref(o), None) == _lib.QE_OK
+    g = _lib.QeGroups(num_groups=4, num_slots=5, stride=4, out_mask=C.c_void_p(64))
+    assert L.qe_commit_vote(C.byref(g), C.byref(o), None) == _lib.QE_EINVAL  # out w/o inc
+    assert L.qe_record_votes(4, 0, None, None, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_replication_round(None, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_election_steps(None, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_tune(b"blocks_per_cu", 0) == _lib.QE_ERANGE
+    assert L.qe_tune(b"nope", 1) == _lib.QE_EINVAL
+    p = _lib.QeElectionParams(p_drop_q16=70000)
+    st = _lib.QeElectionState(num_groups=1, num_slots=3, term=C.c_void_p(64),
+                              state=C.c_void_p(64), voted=C.c_void_p(64),
+                              granted=C.c_void_p(64), self_slot=C.c_void_p(64))
+    assert L.qe_election_steps(C.byref(st), C.byref(p), None, None) == _lib.QE_ERANGE
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    code = ("import os; os.environ['QE_LIB']='/nonexistent/lib.so'\n"
+            "try:\n import etcd_amd\nexcept ImportError as e:\n print('IMPORTERROR', e)\n")
+    out = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT)
+    assert "IMPORTERROR" in out.stdout, out.stdout + out.stderr

@@ -1,0 +1,437 @@
+"""GPU parity: every entry point of the C ABI against the CPU oracle, bit
+for bit, on the golden fixtures and on seeded synthetic batches (all slot
+counts 1..16, majority / masked / joint configs, tie-heavy and uniform value
+distributions, ragged G, learners, invariant violations)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import quorum_ref as Q
+from tests.golden_util import INF, case_acked, case_votes, datadriven_cases, raft_tables
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from etcd_amd import engine
+    return engine
+
+
+def gpu_batch(eng, G, S, seed, goff=0, masks=("inc", "out", "learner"), votes=True, **gen):
+    b = eng.SlotBatch(G, S, DEV, masks=masks, votes=votes, group_offset=goff)
+    eng.gen_groups(b, seed, **gen)
+    return b
+
+
+def host_batch(orc, b):
+    h = b.host()
+    hb = orc.Batch(b.G, b.S, masks=tuple(n for n in ("inc", "out", "learner") if h[n] is not None),
+                   votes=h["voted"] is not None)
+    hb.match[:] = h["match"].reshape(-1)
+    for n in ("inc", "out", "learner", "voted", "granted"):
+        if h[n] is not None:
+            getattr(hb, n)[:] = h[n]
+    return hb
+
+
+def check_commit_vote(eng, orc, b, goff=0):
+    stats = eng.stats_buffer(DEV)
+    out = eng.commit_vote(b, stats=stats)
+    folded = eng.stats_reduce(stats)
+    torch.cuda.synchronize()
+    hb = host_batch(orc, b)
+    commit, vote, gc, rc, ostats = orc.commit_vote(hb, goff=goff)
+    np.testing.assert_array_equal(out.commit.cpu().numpy().view(np.uint64), commit)
+    np.testing.assert_array_equal(out.vote.cpu().numpy(), vote)
+    np.testing.assert_array_equal(out.granted.cpu().numpy(), gc)
+    np.testing.assert_array_equal(out.rejected.cpu().numpy(), rc)
+    got = folded.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got, ostats)
+    return commit, vote
+
+
+# --------------------------------------------------------------------------
+# golden fixtures through the reference-API mirror
+# --------------------------------------------------------------------------
+def test_golden_datadriven_through_mirror(eng):
+    import etcd_amd as E
+    cases = datadriven_cases()
+    com = [c for c in cases if c["cmd"] == "committed"]
+    vot = [c for c in cases if c["cmd"] == "vote"]
+    got = E.CommittedIndexBatch([E.JointConfig(c["cfg"], c["cfgj"]) for c in com],
+                                [E.MapAckIndexer(case_acked(c)) for c in com], DEV)
+    assert [int(x) for x in got] == [c["expect"] for c in com]
+    # symmetry (datadriven_test.go:218-221)
+    got2 = E.CommittedIndexBatch([E.JointConfig(c["cfgj"], c["cfg"]) for c in com],
+                                 [E.MapAckIndexer(case_acked(c)) for c in com], DEV)
+    assert got2 == got
+    gotv = E.VoteResultBatch([E.JointConfig(c["cfg"], c["cfgj"]) for c in vot],
+                             [case_votes(c) for c in vot], DEV)
+    assert [int(x) for x in gotv] == [c["expect"] for c in vot]
+    assert str(gotv[0]) in ("VotePending", "VoteLost", "VoteWon")
+    # per-group methods (batch of one) on a few cases
+    for c in com[:6]:
+        mc = E.MajorityConfig(c["cfg"])
+        if not c["joint"]:
+            assert int(mc.CommittedIndex(E.MapAckIndexer(case_acked(c)), DEV)) == c["expect"]
+    assert str(E.Index(INF)) == "∞"
+
+
+def test_golden_through_fixed_majority_kernel(eng, orc):
+    """Non-joint golden cases through MODE 0 (no masks): voters occupy all S
+    slots, so each distinct voter count is its own batch."""
+    by_n = {}
+    for c in datadriven_cases():
+        if c["joint"] or not c["cfg"]:
+            continue
+        by_n.setdefault(len(c["cfg"]), []).append(c)
+    for n, cs in by_n.items():
+        b = eng.SlotBatch(len(cs), n, DEV, masks=(), votes=True)
+        match = np.zeros((n, len(cs)), np.uint64)
+        vd = np.zeros(len(cs), np.uint64)
+        gr = np.zeros(len(cs), np.uint64)
+        for i, c in enumerate(cs):
+            ids = sorted(c["cfg"])
+            l, v = case_acked(c), case_votes(c)
+            for s, vid in enumerate(ids):
+                match[s, i] = l.get(vid, 0)
+                if vid in v:
+                    vd[i] |= 1 << s
+                    gr[i] |= (1 << s) if v[vid] else 0
+        b.load_host(match, voted=vd, granted=gr)
+        out = eng.commit_vote(b)
+        commit = out.commit.cpu().numpy().view(np.uint64)
+        vote = out.vote.cpu().numpy()
+        for i, c in enumerate(cs):
+            want = c["expect"]
+            assert (int(commit[i]) if c["cmd"] == "committed" else int(vote[i])) == want, c["source"]
+
+
+def test_tracker_mirror(eng):
+    import etcd_amd as E
+    pt = E.MakeProgressTracker(256)
+    pt.Voters = E.JointConfig({1, 2, 3}, {3, 4, 5})
+    pt.Learners = {6}
+    for vid, m in [(1, 10), (2, 7), (3, 9), (4, 3), (5, 8), (6, 100)]:
+        pt.Progress[vid] = E.Progress(Match=m, Next=m + 1, IsLearner=(vid == 6),
+                                      RecentActive=vid in (1, 2, 6))
+    # c0 {10,7,9} -> 9 ; c1 {9,3,8} -> 8 ; joint -> 8
+    assert pt.Committed(DEV) == 8
+    pt.RecordVote(1, True)
+    pt.RecordVote(1, False)   # first vote sticks
+    pt.RecordVote(6, True)    # learner vote: not counted
+    pt.RecordVote(4, False)
+    g, r, res = pt.TallyVotes(DEV)
+    assert (g, r) == (1, 1) and res == E.VotePending
+    # recent: 1,2 active in c0 (won), c1 {3,4,5} none active -> lost
+    assert pt.QuorumActive(DEV) is False
+    pt.Progress[5].RecentActive = True
+    pt.Progress[3].RecentActive = True
+    assert pt.QuorumActive(DEV) is True
+
+
+# --------------------------------------------------------------------------
+# generator parity
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("S,n_inc,n_out,mask_mode,dist", [
+    (3, 0, 0, 0, 0), (5, 0, 0, 0, 1), (7, 0, 0, 0, 2), (10, 5, 5, 0, 0), (16, 7, 9, 0, 2),
+    (8, 0, 0, 1, 0), (13, 0, 0, 1, 1)])
+def test_generator_bit_identical(eng, orc, S, n_inc, n_out, mask_mode, dist):
+    G = 4099
+    b = gpu_batch(eng, G, S, 0xABCD + S, goff=77, dist=dist, n_inc=n_inc, n_out=n_out,
+                  mask_mode=mask_mode)
+    h = b.host()
+    hb = orc.Batch(G, S)
+    orc.gen_batch(hb, 0xABCD + S, goff=77, dist=dist, n_inc=n_inc, n_out=n_out,
+                  mask_mode=mask_mode)
+    np.testing.assert_array_equal(h["match"], hb.match.reshape(S, G))
+    for n in ("inc", "out", "learner", "voted", "granted"):
+        np.testing.assert_array_equal(h[n], getattr(hb, n), err_msg=n)
+
+
+# --------------------------------------------------------------------------
+# qe_commit_vote parity
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("S", list(range(1, 17)))
+def test_commit_vote_fixed_majority_all_slots(eng, orc, S):
+    for dist in (0, 1, 2):
+        b = gpu_batch(eng, 30001, S, 1000 + S * 7 + dist, masks=(), dist=dist)
+        check_commit_vote(eng, orc, b)
+
+
+@pytest.mark.parametrize("S", list(range(1, 17)))
+def test_commit_vote_masked_and_joint(eng, orc, S):
+    for mask_mode in (0, 1):
+        for dist in (0, 2):
+            n_inc = max(1, S // 2)
+            n_out = max(1, S - n_inc) if S > 1 else 1
+            b = gpu_batch(eng, 20011, S, 77 * S + mask_mode * 3 + dist, goff=S * 1000,
+                          dist=dist, n_inc=n_inc, n_out=n_out, mask_mode=mask_mode)
+            check_commit_vote(eng, orc, b, goff=S * 1000)
+            # masked majority only (inc mask, no out mask)
+            b2 = gpu_batch(eng, 5003, S, 5 + S, masks=("inc", "learner"), dist=dist,
+                           n_inc=n_inc, mask_mode=mask_mode)
+            check_commit_vote(eng, orc, b2)
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 63, 64, 65, 127, 128, 129, 255, 257, 1000])
+def test_commit_vote_ragged_sizes(eng, orc, G):
+    for S, masks in ((5, ()), (10, ("inc", "out", "learner"))):
+        b = gpu_batch(eng, G, S, G * 31 + S, masks=masks, n_inc=5, n_out=5, dist=2)
+        check_commit_vote(eng, orc, b)
+
+
+def test_commit_vote_scalar_path_odd_stride(eng, orc):
+    """stride odd -> slot rows not 16-B aligned -> scalar (non-vector) path."""
+    G, S = 1001, 7
+    b = eng.SlotBatch(G, S, DEV, masks=("inc", "out"), stride=1003)
+    eng.gen_groups(b, 99, n_inc=4, n_out=3)
+    check_commit_vote(eng, orc, b)
+
+
+def test_commit_vote_extremes(eng, orc):
+    """Values at the top of the uint64 range (inf-1, 2^63), all-absent and
+    empty configs (CommittedIndex = inf, VoteResult = VoteWon)."""
+    G, S = 512, 6
+    rng = np.random.default_rng(3)
+    match = rng.choice(np.array([0, 1, (1 << 63), INF - 1, INF, 12345], dtype=np.uint64),
+                       size=(S, G))
+    inc = rng.integers(0, 1 << S, G)
+    inc[:8] = 0
+    out = rng.integers(0, 1 << S, G)
+    out[8:16] = 0
+    b = eng.SlotBatch(G, S, DEV, masks=("inc", "out", "learner"))
+    b.load_host(match, inc=inc, out=out, learner=np.zeros(G), voted=rng.integers(0, 64, G),
+                granted=rng.integers(0, 64, G))
+    commit, vote = check_commit_vote(eng, orc, b)
+    assert all(int(c) == INF for c in commit[:8][(out[:8] == 0)])
+
+
+def test_committed_index_and_vote_result_entry_points(eng, orc):
+    b = gpu_batch(eng, 7777, 9, 4242, n_inc=5, n_out=4, dist=0)
+    commit = eng.committed_index(b)
+    vote = eng.vote_result(b)
+    hb = host_batch(orc, b)
+    c_ref, v_ref, _, _, _ = orc.commit_vote(hb)
+    np.testing.assert_array_equal(commit.cpu().numpy().view(np.uint64), c_ref)
+    np.testing.assert_array_equal(vote.cpu().numpy(), v_ref)
+
+
+def test_full_size_config2_bit_exact(eng, orc):
+    """BASELINE config 2 at full size: 64M groups x 5 voters, every group
+    compared with the OpenMP oracle, plus the stats vector."""
+    G, S = 1 << 26, 5
+    b = gpu_batch(eng, G, S, 0x5EED, masks=())
+    check_commit_vote(eng, orc, b)
+
+
+def test_full_size_config3_properties(eng, orc):
+    """BASELINE config 3 at full size (128M joint 5+5 groups): the order-free
+    stats vector (incl. checksum) matches the oracle, and the result is
+    symmetric in the halves (swap inc/out)."""
+    G, S = 1 << 27, 10
+    b = gpu_batch(eng, G, S, 0xC0FFEE, n_inc=5, n_out=5)
+    stats = eng.stats_buffer(DEV)
+    out = eng.Outputs(G, DEV, tally=False)
+    eng.commit_vote(b, out, stats=stats)
+    got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+    c1 = out.commit.clone()
+    b.inc, b.out = b.out, b.inc
+    eng.commit_vote(b, out)
+    assert torch.equal(c1, out.commit)
+    b.inc, b.out = b.out, b.inc
+    del c1, out
+    hb = host_batch(orc, b)
+    del b
+    torch.cuda.empty_cache()
+    _, _, _, _, ostats = orc.commit_vote(hb)
+    np.testing.assert_array_equal(got, ostats)
+
+
+# --------------------------------------------------------------------------
+# QuorumActive / RecordVote
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("S", [1, 3, 5, 8, 9, 12, 16])
+def test_quorum_active_and_record_votes(eng, orc, S):
+    G = 10007
+    b = gpu_batch(eng, G, S, 55 + S, mask_mode=1)
+    rng = np.random.default_rng(S)
+    md = eng.mask_torch_dtype(S)
+    npd = eng.mask_np_dtype(S)
+    recent = rng.integers(0, 1 << S, G).astype(npd)
+    rec_t = torch.from_numpy(recent.view(np.int16) if S > 8 else recent).to(DEV, dtype=md)
+    act = eng.quorum_active(b, rec_t).cpu().numpy()
+    h = b.host()
+    want = orc.quorum_active(G, S, h["inc"], h["out"], h["learner"], recent)
+    np.testing.assert_array_equal(act, want)
+    # RecordVote twice: the first vote sticks
+    voted, granted = h["voted"].copy(), h["granted"].copy()
+    for rnd in range(2):
+        resp = rng.integers(0, 1 << S, G).astype(npd)
+        val = rng.integers(0, 1 << S, G).astype(npd)
+        tr = torch.from_numpy(resp.view(np.int16) if S > 8 else resp).to(DEV, dtype=md)
+        tv = torch.from_numpy(val.view(np.int16) if S > 8 else val).to(DEV, dtype=md)
+        eng.record_votes(b, tr, tv)
+        orc.record_votes(G, S, voted, granted, resp, val)
+    h2 = b.host()
+    np.testing.assert_array_equal(h2["voted"], voted)
+    np.testing.assert_array_equal(h2["granted"], granted)
+
+
+# --------------------------------------------------------------------------
+# Replication round (config 4)
+# --------------------------------------------------------------------------
+def _repl_setup(eng, G, S, seed, joint):
+    masks = ("inc", "out") if joint else ()
+    b = eng.SlotBatch(G, S, DEV, masks=masks, votes=False)
+    eng.gen_groups(b, seed, dist=0, p_absent=0, n_inc=(S + 1) // 2 if joint else 0,
+                   n_out=S // 2 + 1 if joint else 0)
+    base = b.match_rows().clone()
+    lo = base.min(dim=0).values
+    hi = base.max(dim=0).values
+    committed = lo.clone()
+    last_index = hi + 64
+    term_start = lo + (hi - lo) // 2
+    st = eng.ReplicationState(b, committed, term_start, last_index)
+    return b, st
+
+
+@pytest.mark.parametrize("S,joint", [(3, False), (5, False), (7, False), (5, True), (10, True),
+                                     (16, True)])
+def test_replication_rounds(eng, orc, S, joint):
+    G = 20011
+    b, st = _repl_setup(eng, G, S, 0x1234 + S, joint)
+    rng = np.random.default_rng(S)
+    h = {k: v.cpu().numpy().view(np.uint64).copy() for k, v in
+         (("match", b.match), ("next", st.next), ("committed", st.committed),
+          ("term_start", st.term_start), ("last_index", st.last_index))}
+    hm = b.host()
+    md = eng.mask_torch_dtype(S)
+    npd = eng.mask_np_dtype(S)
+    for rnd in range(4):
+        resp = (h["match"].reshape(S, -1)[:, :G] + rng.integers(0, 40, (S, G)).astype(np.uint64))
+        resp_full = np.zeros((S, b.stride), np.uint64)
+        resp_full[:, :G] = resp
+        rmask = rng.integers(0, 1 << S, G).astype(npd)
+        acks = rng.integers(0, 1 << S, G).astype(npd)
+        t_resp = torch.from_numpy(resp_full.reshape(-1).view(np.int64)).to(DEV)
+        t_rm = torch.from_numpy(rmask.view(np.int16) if S > 8 else rmask).to(DEV, dtype=md)
+        t_ack = torch.from_numpy(acks.view(np.int16) if S > 8 else acks).to(DEV, dtype=md)
+        read_ok = torch.zeros(G, dtype=torch.uint8, device=DEV)
+        adv = torch.zeros(G, dtype=torch.uint8, device=DEV)
+        stats = eng.stats_buffer(DEV)
+        eng.replication_round(st, t_resp, t_rm, t_ack, read_ok, adv, stats)
+        folded = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+        o_ro, o_adv, o_stats = orc.replication_round(
+            G, 0, S, b.stride, h["match"], h["next"], h["committed"], h["term_start"],
+            h["last_index"], hm["inc"], hm["out"], resp_full.reshape(-1), rmask, acks)
+        np.testing.assert_array_equal(b.match.cpu().numpy().view(np.uint64), h["match"])
+        np.testing.assert_array_equal(st.next.cpu().numpy().view(np.uint64), h["next"])
+        np.testing.assert_array_equal(st.committed.cpu().numpy().view(np.uint64), h["committed"])
+        np.testing.assert_array_equal(read_ok.cpu().numpy(), o_ro)
+        np.testing.assert_array_equal(adv.cpu().numpy(), o_adv)
+        np.testing.assert_array_equal(folded, o_stats)
+        assert o_adv.sum() > 0
+
+
+def test_test_commit_table_on_gpu(eng):
+    """TestCommit (raft/raft_test.go:1127-1174) through qe_replication_round:
+    matches arrive as MsgAppResp on a fresh Progress, then maybeCommit."""
+    rows = raft_tables()["TestCommit"]["rows"]
+    by_n = {}
+    for r in rows:
+        by_n.setdefault(len(r["matches"]), []).append(r)
+    for n, rs in by_n.items():
+        G = len(rs)
+        b = eng.SlotBatch(G, n, DEV, masks=(), votes=False)
+        resp = np.zeros((n, b.stride), np.uint64)
+        ts = np.zeros(G, np.uint64)
+        li = np.zeros(G, np.uint64)
+        for i, r in enumerate(rs):
+            resp[:, i] = r["matches"]
+            ts[i], li[i] = Q.log_term_range(r["logs"], r["sm_term"])
+        st = eng.ReplicationState(
+            b, torch.zeros(G, dtype=torch.int64, device=DEV),
+            torch.from_numpy(ts.view(np.int64)).to(DEV), torch.from_numpy(li.view(np.int64)).to(DEV),
+            nxt=torch.ones(n * b.stride, dtype=torch.int64, device=DEV))
+        full = (1 << n) - 1
+        rm = torch.full((G,), full, dtype=torch.uint8, device=DEV)
+        eng.replication_round(st, torch.from_numpy(resp.reshape(-1).view(np.int64)).to(DEV), rm)
+        got = st.committed.cpu().numpy()
+        assert [int(x) for x in got] == [r["want"] for r in rs]
+
+
+# --------------------------------------------------------------------------
+# Election simulation (config 5)
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("S,joint", [(1, False), (3, False), (5, False), (7, False), (10, True),
+                                     (16, True)])
+def test_election_steps(eng, orc, S, joint):
+    G = 30011
+    masks = ("inc", "out", "learner")
+    b = eng.SlotBatch(G, S, DEV, masks=masks, votes=False, group_offset=999)
+    eng.gen_groups(b, 0xE1EC + S, n_inc=(S + 1) // 2 if joint else 0,
+                   n_out=(S // 2 if joint else 0))
+    self_slot = eng.first_voter_slot(b)
+    est = eng.ElectionState(b, self_slot)
+    h = b.host()
+    term = np.zeros(G, np.uint64)
+    state = np.zeros(G, np.uint8)
+    voted = np.zeros(G, eng.mask_np_dtype(S))
+    granted = np.zeros(G, eng.mask_np_dtype(S))
+    ss = self_slot.cpu().numpy()
+    step0 = 0
+    for launch, steps in enumerate((1, 7, 32)):
+        stats = eng.stats_buffer(DEV)
+        eng.election_steps(est, 77, step0, steps, p_drop=13107, p_grant=32768, stats=stats)
+        got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+        want = orc.election_steps(G, 999, S, term, state, voted, granted, ss, h["inc"], h["out"],
+                                  h["learner"], 77, step0, steps, 13107, 32768)
+        step0 += steps
+        np.testing.assert_array_equal(est.term.cpu().numpy().view(np.uint64), term)
+        np.testing.assert_array_equal(est.state.cpu().numpy(), state)
+        np.testing.assert_array_equal(est.voted.cpu().numpy().view(voted.dtype), voted)
+        np.testing.assert_array_equal(est.granted.cpu().numpy().view(granted.dtype), granted)
+        np.testing.assert_array_equal(got, want)
+        assert want[14] == 0  # invariant violations
+    assert int(want[12]) > 0  # some leaders elected
+
+
+def test_leader_election_table_on_gpu(eng):
+    """TestLeaderElectionInOneRoundRPC through the GPU primitives:
+    campaign self-vote (qe_record_votes) then one response round
+    (qe_record_votes) and TallyVotes (qe_commit_vote)."""
+    rows = raft_tables()["TestLeaderElectionInOneRoundRPC"]["rows"]
+    for r in rows:
+        n = r["size"]
+        b = eng.SlotBatch(1, n, DEV, masks=(), votes=True)
+        b.load_host(np.zeros((n, 1), np.uint64))
+        one = torch.ones(1, dtype=torch.uint8, device=DEV)
+        eng.record_votes(b, one, one)  # self (slot 0 = id 1) votes yes
+        out = eng.commit_vote(b)
+        state = "StateLeader" if int(out.vote[0]) == 3 else "StateCandidate"
+        for vid, v in r["votes"]:
+            if state != "StateCandidate":
+                break
+            bit = torch.tensor([1 << (vid - 1)], dtype=torch.uint8, device=DEV)
+            eng.record_votes(b, bit, bit if v else torch.zeros_like(bit))
+            res = int(eng.commit_vote(b).vote[0])
+            state = {3: "StateLeader", 2: "StateFollower"}.get(res, "StateCandidate")
+        assert state == r["state"], r
+
+
+def test_tuning_knobs_do_not_change_results(eng, orc):
+    b = gpu_batch(eng, 100003, 7, 31337, masks=())
+    try:
+        for bpc in (1, 2, 8):
+            for nt in (0, 1):
+                eng.tune("blocks_per_cu", bpc)
+                eng.tune("nontemporal", nt)
+                check_commit_vote(eng, orc, b)
+    finally:
+        eng.tune("blocks_per_cu", 8)
+        eng.tune("nontemporal", 0)

@@ -1,0 +1,148 @@
+"""Pins the CPU oracle (oracle/quorum_ref.py and oracle/quorum_oracle.c)
+against the reference's own golden vectors -- the 127 datadriven cases of
+raft/quorum/testdata/*.txt and the TestCommit / TestLeaderElectionInOneRoundRPC
+/ TestProgressUpdate tables -- plus the self-consistency checks the
+reference's harness performs (raft/quorum/datadriven_test.go:175-241) and
+TestQuick's differential check (raft/quorum/quick_test.go:28-44)."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import quorum_ref as Q
+from etcd_amd.packing import pack
+from tests.golden_util import INF, case_acked, case_id, case_votes, datadriven_cases, raft_tables
+
+CASES = datadriven_cases()
+
+
+def test_fixture_counts():
+    by_file = {}
+    for c in CASES:
+        f = c["source"].split("/")[-1].split(":")[0]
+        by_file[f] = by_file.get(f, 0) + 1
+    assert by_file == {"majority_commit.txt": 16, "majority_vote.txt": 22,
+                       "joint_commit.txt": 50, "joint_vote.txt": 39}
+
+
+@pytest.mark.parametrize("case", CASES, ids=case_id)
+def test_python_oracle_matches_golden(case):
+    c0, c1 = case["cfg"], case["cfgj"]
+    if case["cmd"] == "committed":
+        l = case_acked(case)
+        if case["joint"]:
+            got = Q.joint_committed(c0, c1, l)
+            # datadriven_test.go:218-221 symmetry
+            assert Q.joint_committed(c1, c0, l) == got
+        else:
+            got = Q.majority_committed(c0, l)
+            # datadriven_test.go:175-185: alternative, zero-joint, self-joint
+            assert Q.alternative_committed(c0, l) == got
+            assert Q.joint_committed(c0, [], l) == got
+            assert Q.joint_committed(c0, c0, l) == got
+            # datadriven_test.go:186-213: lowering a non-deciding voter
+            for vid in c0:
+                iidx = l.get(vid, 0)
+                if got > iidx > 0:
+                    for low in (iidx - 1, 0):
+                        ll = dict(l)
+                        ll[vid] = low
+                        ll = {k: v for k, v in ll.items() if k in c0}
+                        assert Q.majority_committed(c0, ll) == got
+    else:
+        v = case_votes(case)
+        if case["joint"]:
+            got = Q.joint_vote(c0, c1, v)
+            assert Q.joint_vote(c1, c0, v) == got  # datadriven_test.go:238-241
+        else:
+            got = Q.majority_vote(c0, v)
+    assert got == case["expect"], case["expect_text"]
+
+
+def _packed_case_arrays(cases):
+    groups = [{"c0": c["cfg"], "c1": c["cfgj"], "acked": case_acked(c), "votes": case_votes(c)}
+              for c in cases]
+    return pack(groups, num_slots=16)
+
+
+def test_c_oracle_matches_golden(orc):
+    p = _packed_case_arrays(CASES)
+    b = orc.Batch(p.G, 16)
+    b.match[:] = p.match.reshape(-1)
+    b.inc[:] = p.inc
+    b.out[:] = p.out
+    b.learner[:] = 0
+    b.voted[:] = p.voted
+    b.granted[:] = p.granted
+    for alg in (0, 1):
+        commit, vote, gc, rc, stats = orc.commit_vote(b, alg=alg)
+        for i, c in enumerate(CASES):
+            if c["cmd"] == "committed":
+                assert int(commit[i]) == c["expect"], (c["source"], alg)
+            else:
+                assert int(vote[i]) == c["expect"], c["source"]
+
+
+def test_quick_differential(orc):
+    """TestQuick: CommittedIndex == alternative on small random maps
+    (quick_test.go:47-64 generator: n < 10 ids from perm(2n), idx < n)."""
+    rng = random.Random(0x5EED)
+    L = orc.lib()
+    for _ in range(50000):
+        n = rng.randrange(10)
+        ids = rng.sample(range(2 * n), n) if n else []
+        idxs = [rng.randrange(n) for _ in ids] if n else []
+        m = dict(zip(ids, idxs))
+        mem_n = rng.randrange(10)
+        mem = set(rng.sample(range(2 * mem_n), mem_n)) if mem_n else set()
+        want = Q.alternative_committed(mem, m)
+        got = Q.majority_committed(mem, m)
+        assert got == want
+        # and the C restatement on the packed slot form
+        p = pack([{"c0": mem, "acked": m}], num_slots=16) if len(mem) <= 16 else None
+        if p is not None:
+            vals = np.ascontiguousarray(p.match[:, 0])
+            assert L.orc_majority_committed(16, int(p.inc[0]), orc.P(vals)) == want
+
+
+def test_test_commit_table(orc):
+    """TestCommit (raft/raft_test.go:1127-1174) through the oracle's
+    Committed + maybeCommit with the synthetic log model."""
+    for row in raft_tables()["TestCommit"]["rows"]:
+        ids = list(range(1, len(row["matches"]) + 1))
+        acked = dict(zip(ids, row["matches"]))
+        mci = Q.majority_committed(ids, acked)
+        ts, li = Q.log_term_range(row["logs"], row["sm_term"])
+        _, committed = Q.maybe_commit(mci, 0, ts, li)
+        assert committed == row["want"], row
+
+
+def _one_round_election(size, votes):
+    """TestLeaderElectionInOneRoundRPC: MsgHup then one MsgVoteResp per entry
+    (raft_paper_test.go:218-224), via RecordVote + TallyVotes."""
+    cfg = list(range(1, size + 1))
+    v = {}
+    Q.record_vote(v, 1, True)  # campaign self-vote, raft.go:803
+    _, _, res = Q.tally_votes(cfg, [], set(), v)
+    state = "StateLeader" if res == Q.VOTE_WON else "StateCandidate"
+    for vid, granted in votes:
+        if state != "StateCandidate":
+            break
+        Q.record_vote(v, vid, granted)
+        _, _, res = Q.tally_votes(cfg, [], set(), v)
+        if res == Q.VOTE_WON:
+            state = "StateLeader"
+        elif res == Q.VOTE_LOST:
+            state = "StateFollower"
+    return state
+
+
+def test_leader_election_table():
+    for row in raft_tables()["TestLeaderElectionInOneRoundRPC"]["rows"]:
+        assert _one_round_election(row["size"], row["votes"]) == row["state"], row
+
+
+def test_progress_update_table():
+    for row in raft_tables()["TestProgressUpdate"]["rows"]:
+        ok, m, n = Q.maybe_update(row["prev_match"], row["prev_next"], row["update"])
+        assert (ok, m, n) == (row["want_ok"], row["want_match"], row["want_next"]), row
