@@ -7,6 +7,12 @@ library is the product: if it is missing this module raises at import time
 import ctypes as C
 import os
 
+# torch must be imported BEFORE the library is dlopen'ed: torch ships its own
+# libamdhip64.so.7 and device memory / streams come from torch, so the
+# library's DT_NEEDED libamdhip64.so.7 has to bind to that same runtime
+# instance (two HIP runtimes in one process do not see each other's devices).
+import torch  # noqa: F401
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
