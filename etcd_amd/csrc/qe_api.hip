@@ -7,8 +7,9 @@
 
 namespace qe {
 
-int g_blocks_per_cu = 8;
-int g_nontemporal = 0;
+int g_blocks_per_cu = 0;  // 0 = kernel occupancy
+int g_nontemporal = 3;  // nt loads + nt stores (measured best)
+int g_tiles_per_wave = 2;  // 0 = persistent grid
 
 static thread_local char g_errbuf[256];
 
@@ -96,17 +97,24 @@ size_t qe_mask_bytes(uint32_t num_slots) {
 }
 
 // Optional tuning knobs (not part of the reference semantics):
-//   "blocks_per_cu"  persistent-grid workgroups per CU (1..32, default 8)
-//   "nontemporal"    0/1: non-temporal match loads in qe_commit_vote
+//   "blocks_per_cu"  cap on persistent-grid workgroups per CU (0 = occupancy)
+//   "tiles_per_wave" 0 = persistent grid, T > 0 = each wave walks T tiles
+//   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
 int qe_tune(const char *key, int value) {
   if (!key) return QE_EINVAL;
   if (!strcmp(key, "blocks_per_cu")) {
-    if (value < 1 || value > 32) return QE_ERANGE;
+    if (value < 0 || value > 32) return QE_ERANGE;
     g_blocks_per_cu = value;
     return QE_OK;
   }
+  if (!strcmp(key, "tiles_per_wave")) {
+    if (value < 0 || value > 4096) return QE_ERANGE;
+    g_tiles_per_wave = value;
+    return QE_OK;
+  }
   if (!strcmp(key, "nontemporal")) {
-    g_nontemporal = value ? 1 : 0;
+    if (value < 0 || value > 3) return QE_ERANGE;
+    g_nontemporal = value;
     return QE_OK;
   }
   return QE_EINVAL;

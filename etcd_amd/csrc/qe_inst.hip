@@ -5,6 +5,9 @@
 #ifndef QE_S
 #error "compile with -DQE_S=<slots>"
 #endif
+#ifndef QE_PAIRS
+#define QE_PAIRS ((QE_S) <= 8 ? 2 : 1)  // adjacent-group pairs per lane per tile
+#endif
 
 namespace qe {
 
@@ -12,24 +15,26 @@ namespace {
 constexpr int S = QE_S;
 using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
 
-template <int MODE>
-int launch_cv(const CVArgs &a, bool vec, hipStream_t st) {
-  constexpr int kPairs = 2;
+template <int MODE, bool VEC, bool NTL, bool NTS>
+int launch_cv_k(const CVArgs &a, hipStream_t st) {
+  constexpr int kPairs = QE_PAIRS;
+  auto kern = k_commit_vote<S, MODE, MT, kPairs, VEC, NTL, NTS>;
+  static int occ = occupancy(kern);
   const uint64_t npairs = (a.G + 1) / 2;
   const uint64_t tiles = (npairs + 64 * kPairs - 1) / (64 * kPairs);
-  const unsigned grid = grid_for(tiles);
-  if (vec) {
-    if (g_nontemporal)
-      hipLaunchKernelGGL((k_commit_vote<S, MODE, MT, kPairs, true, true>), dim3(grid),
-                         dim3(kBlock), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_commit_vote<S, MODE, MT, kPairs, true, false>), dim3(grid),
-                         dim3(kBlock), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((k_commit_vote<S, MODE, MT, kPairs, false, false>), dim3(grid),
-                       dim3(kBlock), 0, st, a);
-  }
+  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
+}
+
+template <int MODE>
+int launch_cv(const CVArgs &a, bool vec, hipStream_t st) {
+  if (!vec) return launch_cv_k<MODE, false, false, false>(a, st);
+  switch (g_nontemporal & 3) {
+    case 1: return launch_cv_k<MODE, true, true, false>(a, st);
+    case 2: return launch_cv_k<MODE, true, false, true>(a, st);
+    case 3: return launch_cv_k<MODE, true, true, true>(a, st);
+    default: return launch_cv_k<MODE, true, false, false>(a, st);
+  }
 }
 }  // namespace
 
@@ -44,30 +49,39 @@ int QE_CAT(dispatch_cv_, QE_S)(const CVArgs &a, int mode, bool vec, hipStream_t 
   }
 }
 
-int QE_CAT(dispatch_repl_, QE_S)(const RArgs &a, bool masked, bool joint, bool vec,
-                                 hipStream_t st) {
+template <bool J, bool M, bool V, bool NT>
+static int launch_repl_k(const RArgs &a, hipStream_t st) {
+  auto kern = k_replication<S, J, M, MT, V, NT>;
+  static int occ = occupancy(kern);
   const uint64_t tiles = ((a.G + 1) / 2 + 63) / 64;
-  const unsigned grid = grid_for(tiles);
-#define QE_RL(J, M, V) \
-  hipLaunchKernelGGL((k_replication<S, J, M, MT, V>), dim3(grid), dim3(kBlock), 0, st, a)
-  if (vec) {
-    if (joint) QE_RL(true, true, true);
-    else if (masked) QE_RL(false, true, true);
-    else QE_RL(false, false, true);
-  } else {
-    if (joint) QE_RL(true, true, false);
-    else if (masked) QE_RL(false, true, false);
-    else QE_RL(false, false, false);
-  }
-#undef QE_RL
+  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
+// non-temporal state traffic whenever qe_tune("nontemporal") has both bits
+template <bool J, bool M, bool V>
+static int launch_repl(const RArgs &a, hipStream_t st) {
+  if (V && (g_nontemporal & 3) == 3) return launch_repl_k<J, M, V, true>(a, st);
+  return launch_repl_k<J, M, V, false>(a, st);
+}
+
+int QE_CAT(dispatch_repl_, QE_S)(const RArgs &a, bool masked, bool joint, bool vec,
+                                 hipStream_t st) {
+  if (vec) {
+    if (joint) return launch_repl<true, true, true>(a, st);
+    if (masked) return launch_repl<false, true, true>(a, st);
+    return launch_repl<false, false, true>(a, st);
+  }
+  if (joint) return launch_repl<true, true, false>(a, st);
+  if (masked) return launch_repl<false, true, false>(a, st);
+  return launch_repl<false, false, false>(a, st);
+}
+
 int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
-  const uint64_t cap = static_cast<uint64_t>(num_cus()) * g_blocks_per_cu;
-  const uint64_t need = (a.G + kBlock - 1) / kBlock;
-  const unsigned grid = static_cast<unsigned>(need < cap ? (need ? need : 1) : cap);
-  hipLaunchKernelGGL((k_election<S, MT>), dim3(grid), dim3(kBlock), 0, st, a);
+  auto kern = k_election<S, MT>;
+  static int occ = occupancy(kern);
+  const uint64_t waves = (a.G + 63) / 64;
+  hipLaunchKernelGGL(kern, dim3(grid_for(waves, occ)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 

@@ -26,7 +26,7 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // Tuning knobs (qe_tune): occupancy of the persistent grid.
 // ---------------------------------------------------------------------------
 extern int g_blocks_per_cu;
-extern int g_nontemporal;
+extern int g_nontemporal;  // bit 0: loads, bit 1: stores
 
 inline int num_cus() {
   static int cached[64] = {0};
@@ -42,11 +42,31 @@ inline int num_cus() {
   return cached[dev];
 }
 
-inline unsigned grid_for(uint64_t work_waves) {
-  const uint64_t cap = static_cast<uint64_t>(num_cus()) * g_blocks_per_cu;
+// Grid: with g_tiles_per_wave == 0 a persistent grid of min(work, CUs x
+// resident blocks per CU) (`occ` = hipOccupancyMaxActiveBlocksPerMultiprocessor,
+// capped by g_blocks_per_cu); with g_tiles_per_wave = T > 0 each wave walks
+// T tiles and the hardware dispatcher keeps refilling CUs as blocks retire.
+extern int g_tiles_per_wave;
+inline unsigned grid_for(uint64_t work_waves, int occ) {
   const uint64_t need = (work_waves + (kBlock / 64) - 1) / (kBlock / 64);
-  uint64_t g = need < cap ? need : cap;
+  uint64_t g;
+  if (g_tiles_per_wave > 0) {
+    g = (need + g_tiles_per_wave - 1) / g_tiles_per_wave;
+  } else {
+    int per_cu = occ > 0 ? occ : 4;
+    if (g_blocks_per_cu > 0 && g_blocks_per_cu < per_cu) per_cu = g_blocks_per_cu;
+    const uint64_t cap = static_cast<uint64_t>(num_cus()) * per_cu;
+    g = need < cap ? need : cap;
+  }
+  if (g > 0x7FFFFFFFull) g = 0x7FFFFFFFull;
   return static_cast<unsigned>(g ? g : 1);
+}
+
+template <typename K>
+inline int occupancy(K kernel) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kBlock, 0) != hipSuccess) n = 0;
+  return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -66,14 +86,15 @@ __device__ __forceinline__ void ld_u64_pair(const uint64_t *p, uint64_t g0, uint
   }
 }
 
-template <bool VEC>
+template <bool VEC, bool NT = false>
 __device__ __forceinline__ void st_u64_pair(uint64_t *p, uint64_t g0, uint64_t G, uint64_t lo,
                                             uint64_t hi) {
   if (VEC && g0 + 1 < G) {
     u64x2 x;
     x.x = lo;
     x.y = hi;
-    *reinterpret_cast<u64x2 *>(p + g0) = x;
+    if (NT) __builtin_nontemporal_store(x, reinterpret_cast<u64x2 *>(p + g0));
+    else *reinterpret_cast<u64x2 *>(p + g0) = x;
   } else {
     if (g0 < G) p[g0] = lo;
     if (g0 + 1 < G) p[g0 + 1] = hi;
@@ -118,11 +139,13 @@ __device__ __forceinline__ void st_mask_pair(void *p, uint64_t g0, uint64_t G, u
 }
 
 // uint8 outputs: a pair is one uint16 store.
-template <bool VEC>
+template <bool VEC, bool NT = false>
 __device__ __forceinline__ void st_u8_pair(uint8_t *p, uint64_t g0, uint64_t G, uint32_t lo,
                                            uint32_t hi) {
   if (VEC && g0 + 1 < G) {
-    *reinterpret_cast<uint16_t *>(p + g0) = static_cast<uint16_t>(lo | (hi << 8));
+    const uint16_t x = static_cast<uint16_t>(lo | (hi << 8));
+    if (NT) __builtin_nontemporal_store(x, reinterpret_cast<uint16_t *>(p + g0));
+    else *reinterpret_cast<uint16_t *>(p + g0) = x;
   } else {
     if (g0 < G) p[g0] = static_cast<uint8_t>(lo);
     if (g0 + 1 < G) p[g0 + 1] = static_cast<uint8_t>(hi);
@@ -168,7 +191,7 @@ __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint3
   rc = popc(voted & ~granted & voters);
 }
 
-template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NT>
+template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   const int lane = threadIdx.x & 63;
@@ -193,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
       const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
 #pragma unroll
       for (int s = 0; s < S; s++)
-        ld_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, v[j][0][s], v[j][1][s]);
+        ld_u64_pair<VEC, NTL>(a.match + s * a.stride, g0, G, v[j][0][s], v[j][1][s]);
       if constexpr (MODE >= 1) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[j][0], mi[j][1]);
       else mi[j][0] = mi[j][1] = kFull;
       if constexpr (MODE == 2) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[j][0], mo[j][1]);
@@ -234,10 +257,10 @@ __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
           cnt[C_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
         }
       }
-      if (a.commit) st_u64_pair<VEC>(a.commit, g0, G, c[0], c[1]);
-      if (a.vote) st_u8_pair<VEC>(a.vote, g0, G, vt[0], vt[1]);
-      if (a.gcount) st_u8_pair<VEC>(a.gcount, g0, G, gc[0], gc[1]);
-      if (a.rcount) st_u8_pair<VEC>(a.rcount, g0, G, rc[0], rc[1]);
+      if (a.commit) st_u64_pair<VEC, NTS>(a.commit, g0, G, c[0], c[1]);
+      if (a.vote) st_u8_pair<VEC, NTS>(a.vote, g0, G, vt[0], vt[1]);
+      if (a.gcount) st_u8_pair<VEC, NTS>(a.gcount, g0, G, gc[0], gc[1]);
+      if (a.rcount) st_u8_pair<VEC, NTS>(a.rcount, g0, G, rc[0], rc[1]);
     }
   }
   if (want_stats) {
@@ -263,7 +286,7 @@ struct RArgs {
 
 enum { R_GROUPS, R_SUM, R_ADV, R_READ, R_VIOL, R_CSUM, R_N };
 
-template <int S, bool JOINT, bool MASKED, typename MT, bool VEC>
+template <int S, bool JOINT, bool MASKED, typename MT, bool VEC, bool NT>
 __global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   const int lane = threadIdx.x & 63;
@@ -279,14 +302,7 @@ __global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
 
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = 2 * (t * 64 + lane);
-    uint64_t m[2][S], n[2][S], r[2][S];
     uint32_t mi[2], mo[2], rm[2], ack[2];
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      ld_u64_pair<VEC, false>(a.match + s * a.stride, g0, G, m[0][s], m[1][s]);
-      ld_u64_pair<VEC, false>(a.next + s * a.stride, g0, G, n[0][s], n[1][s]);
-      ld_u64_pair<VEC, false>(a.resp + s * a.stride, g0, G, r[0][s], r[1][s]);
-    }
     if (MASKED) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[0], mi[1]);
     else mi[0] = mi[1] = kFull;
     if (JOINT) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[0], mo[1]);
@@ -296,23 +312,33 @@ __global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
     if (a.read_acks) ld_mask_pair<MT, VEC>(a.read_acks, g0, G, ack[0], ack[1]);
     else ack[0] = ack[1] = 0;
     uint64_t ts[2], li[2], cm[2];
-    ld_u64_pair<VEC, false>(a.term_start, g0, G, ts[0], ts[1]);
-    ld_u64_pair<VEC, false>(a.last_index, g0, G, li[0], li[1]);
-    ld_u64_pair<VEC, false>(a.committed, g0, G, cm[0], cm[1]);
+    ld_u64_pair<VEC, NT>(a.term_start, g0, G, ts[0], ts[1]);
+    ld_u64_pair<VEC, NT>(a.last_index, g0, G, li[0], li[1]);
+    ld_u64_pair<VEC, NT>(a.committed, g0, G, cm[0], cm[1]);
 
-    uint32_t ro[2], adv[2];
+    // Progress.MaybeUpdate on every responding slot (progress.go:144-153),
+    // streamed slot by slot: read match/next/resp, update, write back.
     uint64_t sel[2][S];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      // Progress.MaybeUpdate on every responding slot (progress.go:144-153)
+    for (int s = 0; s < S; s++) {
+      uint64_t m[2], n[2], r[2];
+      ld_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, m[0], m[1]);
+      ld_u64_pair<VEC, NT>(a.next + s * a.stride, g0, G, n[0], n[1]);
+      ld_u64_pair<VEC, NT>(a.resp + s * a.stride, g0, G, r[0], r[1]);
 #pragma unroll
-      for (int s = 0; s < S; s++) {
+      for (int h = 0; h < 2; h++) {
         const bool resp = (rm[h] >> s) & 1u;
-        const uint64_t x = r[h][s];
-        m[h][s] = (resp && m[h][s] < x) ? x : m[h][s];
-        n[h][s] = (resp && n[h][s] < x + 1) ? x + 1 : n[h][s];
-        sel[h][s] = m[h][s];
+        m[h] = (resp && m[h] < r[h]) ? r[h] : m[h];
+        n[h] = (resp && n[h] < r[h] + 1) ? r[h] + 1 : n[h];
+        sel[h][s] = m[h];
       }
+      st_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, m[0], m[1]);
+      st_u64_pair<VEC, NT>(a.next + s * a.stride, g0, G, n[0], n[1]);
+    }
+
+    uint32_t ro[2], adv[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
       const uint32_t inc = mi[h] & kFull, out = mo[h] & kFull;
       const uint64_t mci = (!JOINT && !MASKED) ? select_fixed<S>(sel[h])
                                                : joint_committed<S>(sel[h], inc, out);
@@ -331,14 +357,9 @@ __global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
         cnt[R_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ cm[h] ^ tag);
       }
     }
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      st_u64_pair<VEC>(a.match + s * a.stride, g0, G, m[0][s], m[1][s]);
-      st_u64_pair<VEC>(a.next + s * a.stride, g0, G, n[0][s], n[1][s]);
-    }
-    st_u64_pair<VEC>(a.committed, g0, G, cm[0], cm[1]);
-    if (a.read_ok) st_u8_pair<VEC>(a.read_ok, g0, G, ro[0], ro[1]);
-    if (a.adv) st_u8_pair<VEC>(a.adv, g0, G, adv[0], adv[1]);
+    st_u64_pair<VEC, NT>(a.committed, g0, G, cm[0], cm[1]);
+    if (a.read_ok) st_u8_pair<VEC, NT>(a.read_ok, g0, G, ro[0], ro[1]);
+    if (a.adv) st_u8_pair<VEC, NT>(a.adv, g0, G, adv[0], adv[1]);
   }
   if (want_stats) {
     const int idx[R_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,

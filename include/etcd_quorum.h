@@ -132,8 +132,11 @@ const char *qe_strerror(int status);
 size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
 
 /* Optional launch tuning (no reference counterpart; never changes results):
- *   "blocks_per_cu"  persistent-grid workgroups per CU, 1..32 (default 8)
- *   "nontemporal"    0/1 non-temporal match loads in qe_commit_vote        */
+ *   "blocks_per_cu"  cap on persistent-grid workgroups per CU, 0..32
+ *                    (default 0 = the kernel's occupancy)
+ *   "tiles_per_wave" 0 = persistent grid; T > 0: each wave walks T tiles
+ *   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
+ *                    of qe_commit_vote                                     */
 int qe_tune(const char *key, int value);
 
 /* ---- quorum decisions -------------------------------------------------- */

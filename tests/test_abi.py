@@ -111,7 +111,8 @@ def test_argument_errors_without_gpu():
     assert L.qe_record_votes(4, 0, None, None, None, None, None) == _lib.QE_EINVAL
     assert L.qe_replication_round(None, None, None, None) == _lib.QE_EINVAL
     assert L.qe_election_steps(None, None, None, None) == _lib.QE_EINVAL
-    assert L.qe_tune(b"blocks_per_cu", 0) == _lib.QE_ERANGE
+    assert L.qe_tune(b"blocks_per_cu", -1) == _lib.QE_ERANGE
+    assert L.qe_tune(b"blocks_per_cu", 33) == _lib.QE_ERANGE
     assert L.qe_tune(b"nope", 1) == _lib.QE_EINVAL
     p = _lib.QeElectionParams(p_drop_q16=70000)
     st = _lib.QeElectionState(num_groups=1, num_slots=3, term=C.c_void_p(64),

@@ -427,11 +427,14 @@ def test_leader_election_table_on_gpu(eng):
 def test_tuning_knobs_do_not_change_results(eng, orc):
     b = gpu_batch(eng, 100003, 7, 31337, masks=())
     try:
-        for bpc in (1, 2, 8):
-            for nt in (0, 1):
-                eng.tune("blocks_per_cu", bpc)
-                eng.tune("nontemporal", nt)
-                check_commit_vote(eng, orc, b)
+        for bpc in (1, 2, 0):
+            for nt in (0, 1, 2, 3):
+                for tpw in (0, 1, 3):
+                    eng.tune("blocks_per_cu", bpc)
+                    eng.tune("nontemporal", nt)
+                    eng.tune("tiles_per_wave", tpw)
+                    check_commit_vote(eng, orc, b)
     finally:
-        eng.tune("blocks_per_cu", 8)
+        eng.tune("blocks_per_cu", 0)
         eng.tune("nontemporal", 0)
+        eng.tune("tiles_per_wave", 0)
