@@ -37,8 +37,12 @@ WORKLOADS = {
                    1 << 26, 5, "majority"),
     "config2_n7": ("64M groups x 7-voter MajorityConfig CommittedIndex+VoteResult+TallyVotes",
                    1 << 26, 7, "majority"),
-    "config3_joint": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked) "
-                      "CommittedIndex+VoteResult+TallyVotes", 1 << 27, 10, "joint"),
+    "config3_joint": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked, "
+                      "shape-bucketed layout) CommittedIndex+VoteResult+TallyVotes",
+                      1 << 27, 10, "joint"),
+    "config3_joint_rot": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked, "
+                          "per-group rotated slots) CommittedIndex+VoteResult+TallyVotes",
+                          1 << 27, 10, "joint_rot"),
     "config4_repl": ("32M groups x 5 voters lockstep replication round (MaybeUpdate, "
                      "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
     "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
@@ -49,8 +53,8 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="config2_n5", choices=sorted(WORKLOADS))
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -61,32 +65,52 @@ def parse():
 
 
 class Dist:
+    """One process per GPU (torch.distributed.run env).  Collectives go over
+    RCCL (backend "nccl") by default.  QE_DIST_BACKEND=gloo with
+    QE_DEVICE_MOD=1 rehearses the multi-rank logic on a 1-GPU box (all ranks
+    on cuda:0, counters reduced on the host)."""
+
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(self.local)
-        self.dev = torch.device("cuda", self.local)
+        self.backend = os.environ.get("QE_DIST_BACKEND", "nccl")
+        mod = int(os.environ.get("QE_DEVICE_MOD", "0"))
+        dev_idx = self.local % mod if mod > 0 else self.local
+        torch.cuda.set_device(dev_idx)
+        self.dev = torch.device("cuda", dev_idx)
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=self.dev)
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
+
+    def _coll(self, t):
+        return t if self.backend == "nccl" else t.cpu()
 
     def barrier(self):
         if self.world > 1:
-            dist.barrier(device_ids=[self.local])
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.dev.index])
+            else:
+                dist.barrier()
 
     def max(self, x):
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        t = self._coll(torch.tensor([x], dtype=torch.float64, device=self.dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_stats(self, folded):
-        """RCCL all-reduce of the uint64 statistics vector (sum; the int64
-        wraparound equals uint64 modular addition)."""
+        """All-reduce (sum) of the uint64 statistics vector; the int64
+        wraparound equals uint64 modular addition.  RCCL over xGMI: 128 B,
+        once per run, latency-bound and off the data path."""
         if self.world > 1:
-            dist.all_reduce(folded, op=dist.ReduceOp.SUM)
+            t = self._coll(folded)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            folded = t.to(self.dev)
         return folded
 
 
@@ -95,11 +119,13 @@ class Dist:
 # ---------------------------------------------------------------------------
 def setup(name, G, S, kind, d, stats):
     goff = d.rank * G
-    if kind in ("majority", "joint"):
+    if kind in ("majority", "joint", "joint_rot"):
         masks = () if kind == "majority" else ("inc", "out", "learner")
         b = engine.SlotBatch(G, S, d.dev, masks=masks, group_offset=goff)
         if kind == "joint":
-            engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5)
+            engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5, mask_mode=2)
+        elif kind == "joint_rot":
+            engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5, mask_mode=0)
         else:
             engine.gen_groups(b, 0x5EED)
         out = engine.Outputs(G, d.dev)
@@ -115,7 +141,7 @@ def setup(name, G, S, kind, d, stats):
         # algorithmic bytes per group: every input read once, every output
         # written once; +2 B TallyVotes counts we also write
         bpg = b.bytes_per_group(with_outputs=True) + 2
-        if kind == "joint":
+        if kind != "majority":
             # config 3 counts only the union slots' Match: 19 + 8u + 2 (tally)
             inc = b.inc.to(torch.int32)
             uni = (inc | b.out.to(torch.int32))
@@ -304,7 +330,7 @@ def main():
         line = {
             "metric": METRIC,
             "value": main_res["value"],
-            "unit": "group-evals/s" if kind in ("majority", "joint") else main_res["unit"],
+            "unit": "group-evals/s" if kind in ("majority", "joint", "joint_rot") else main_res["unit"],
             "n_gpus": d.world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -329,7 +355,7 @@ def main():
                 "unit": "GB/s",
                 "frac": main_res["hbm_frac"],
                 "traffic": traffic,
-                "kernel": "qe::k_commit_vote" if kind in ("majority", "joint") else kind,
+                "kernel": "qe::k_commit_vote" if kind in ("majority", "joint", "joint_rot") else kind,
                 "kernel_ms": main_res["kernel_ms"],
                 "bytes_per_unit": main_res["bytes_per_unit"],
             },

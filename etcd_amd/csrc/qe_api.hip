@@ -9,7 +9,7 @@ namespace qe {
 
 int g_blocks_per_cu = 0;  // 0 = kernel occupancy
 int g_nontemporal = 3;  // nt loads + nt stores (measured best)
-int g_tiles_per_wave = 2;  // 0 = persistent grid
+int g_tiles_per_wave = -1;  // -1 = per-kernel default, 0 = persistent grid
 
 static thread_local char g_errbuf[256];
 
@@ -98,7 +98,8 @@ size_t qe_mask_bytes(uint32_t num_slots) {
 
 // Optional tuning knobs (not part of the reference semantics):
 //   "blocks_per_cu"  cap on persistent-grid workgroups per CU (0 = occupancy)
-//   "tiles_per_wave" 0 = persistent grid, T > 0 = each wave walks T tiles
+//   "tiles_per_wave" -1 = per-kernel default, 0 = persistent grid,
+//                    T > 0 = each wave walks T tiles
 //   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
 int qe_tune(const char *key, int value) {
   if (!key) return QE_EINVAL;
@@ -108,7 +109,7 @@ int qe_tune(const char *key, int value) {
     return QE_OK;
   }
   if (!strcmp(key, "tiles_per_wave")) {
-    if (value < 0 || value > 4096) return QE_ERANGE;
+    if (value < -1 || value > 4096) return QE_ERANGE;
     g_tiles_per_wave = value;
     return QE_OK;
   }

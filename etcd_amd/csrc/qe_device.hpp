@@ -144,7 +144,17 @@ __device__ __forceinline__ uint32_t joint_vote(uint32_t inc, uint32_t out, uint3
 }
 
 // ---------------------------------------------------------------------------
-// Wave / block reductions for the statistics counters.
+// Wave / block reductions.
+// ---------------------------------------------------------------------------
+// OR of a 32-bit value over the 64 lanes, returned wave-uniform (SGPR).
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x |= __shfl_xor(x, off, 64);
+  return __builtin_amdgcn_readfirstlane(x);
+}
+
+// ---------------------------------------------------------------------------
+// Statistics counters.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
 #pragma unroll

@@ -22,7 +22,7 @@ int launch_cv_k(const CVArgs &a, hipStream_t st) {
   static int occ = occupancy(kern);
   const uint64_t npairs = (a.G + 1) / 2;
   const uint64_t tiles = (npairs + 64 * kPairs - 1) / (64 * kPairs);
-  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ)), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ, MODE == 2 ? 8 : 1)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -54,7 +54,7 @@ static int launch_repl_k(const RArgs &a, hipStream_t st) {
   auto kern = k_replication<S, J, M, MT, V, NT>;
   static int occ = occupancy(kern);
   const uint64_t tiles = ((a.G + 1) / 2 + 63) / 64;
-  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ)), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ, 2)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 

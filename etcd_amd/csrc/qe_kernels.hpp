@@ -46,12 +46,15 @@ inline int num_cus() {
 // resident blocks per CU) (`occ` = hipOccupancyMaxActiveBlocksPerMultiprocessor,
 // capped by g_blocks_per_cu); with g_tiles_per_wave = T > 0 each wave walks
 // T tiles and the hardware dispatcher keeps refilling CUs as blocks retire.
+// g_tiles_per_wave < 0 (default) picks the per-kernel `auto_tpw` measured best
+// (DESIGN.md §6).
 extern int g_tiles_per_wave;
-inline unsigned grid_for(uint64_t work_waves, int occ) {
+inline unsigned grid_for(uint64_t work_waves, int occ, int auto_tpw = 0) {
   const uint64_t need = (work_waves + (kBlock / 64) - 1) / (kBlock / 64);
+  const int tpw = g_tiles_per_wave >= 0 ? g_tiles_per_wave : auto_tpw;
   uint64_t g;
-  if (g_tiles_per_wave > 0) {
-    g = (need + g_tiles_per_wave - 1) / g_tiles_per_wave;
+  if (tpw > 0) {
+    g = (need + tpw - 1) / tpw;
   } else {
     int per_cu = occ > 0 ? occ : 4;
     if (g_blocks_per_cu > 0 && g_blocks_per_cu < per_cu) per_cu = g_blocks_per_cu;
@@ -72,10 +75,12 @@ inline int occupancy(K kernel) {
 // ---------------------------------------------------------------------------
 // Loads/stores of a pair of adjacent groups.
 // ---------------------------------------------------------------------------
-template <bool VEC, bool NT>
+// GUARD = false: the caller knows the whole tile is in range (wave-uniform
+// fast path, no per-element branches between the loads).
+template <bool VEC, bool NT, bool GUARD = true>
 __device__ __forceinline__ void ld_u64_pair(const uint64_t *p, uint64_t g0, uint64_t G,
                                             uint64_t &lo, uint64_t &hi) {
-  if (VEC && g0 + 1 < G) {
+  if (VEC && (!GUARD || g0 + 1 < G)) {
     const u64x2 *q = reinterpret_cast<const u64x2 *>(p + g0);
     u64x2 x = NT ? __builtin_nontemporal_load(q) : *q;
     lo = x.x;
@@ -86,10 +91,10 @@ __device__ __forceinline__ void ld_u64_pair(const uint64_t *p, uint64_t g0, uint
   }
 }
 
-template <bool VEC, bool NT = false>
+template <bool VEC, bool NT = false, bool GUARD = true>
 __device__ __forceinline__ void st_u64_pair(uint64_t *p, uint64_t g0, uint64_t G, uint64_t lo,
                                             uint64_t hi) {
-  if (VEC && g0 + 1 < G) {
+  if (VEC && (!GUARD || g0 + 1 < G)) {
     u64x2 x;
     x.x = lo;
     x.y = hi;
@@ -102,11 +107,11 @@ __device__ __forceinline__ void st_u64_pair(uint64_t *p, uint64_t g0, uint64_t G
 }
 
 // Mask pairs: uint8 masks load as one uint16, uint16 masks as one uint32.
-template <typename MT, bool VEC>
+template <typename MT, bool VEC, bool GUARD = true>
 __device__ __forceinline__ void ld_mask_pair(const void *p, uint64_t g0, uint64_t G,
                                              uint32_t &lo, uint32_t &hi) {
   const MT *m = static_cast<const MT *>(p);
-  if (VEC && g0 + 1 < G) {
+  if (VEC && (!GUARD || g0 + 1 < G)) {
     if constexpr (sizeof(MT) == 1) {
       const uint32_t x = *reinterpret_cast<const uint16_t *>(m + g0);
       lo = x & 0xFFu;
@@ -122,11 +127,11 @@ __device__ __forceinline__ void ld_mask_pair(const void *p, uint64_t g0, uint64_
   }
 }
 
-template <typename MT, bool VEC>
+template <typename MT, bool VEC, bool GUARD = true>
 __device__ __forceinline__ void st_mask_pair(void *p, uint64_t g0, uint64_t G, uint32_t lo,
                                              uint32_t hi) {
   MT *m = static_cast<MT *>(p);
-  if (VEC && g0 + 1 < G) {
+  if (VEC && (!GUARD || g0 + 1 < G)) {
     if constexpr (sizeof(MT) == 1) {
       *reinterpret_cast<uint16_t *>(m + g0) = static_cast<uint16_t>(lo | (hi << 8));
     } else {
@@ -139,10 +144,10 @@ __device__ __forceinline__ void st_mask_pair(void *p, uint64_t g0, uint64_t G, u
 }
 
 // uint8 outputs: a pair is one uint16 store.
-template <bool VEC, bool NT = false>
+template <bool VEC, bool NT = false, bool GUARD = true>
 __device__ __forceinline__ void st_u8_pair(uint8_t *p, uint64_t g0, uint64_t G, uint32_t lo,
                                            uint32_t hi) {
-  if (VEC && g0 + 1 < G) {
+  if (VEC && (!GUARD || g0 + 1 < G)) {
     const uint16_t x = static_cast<uint16_t>(lo | (hi << 8));
     if (NT) __builtin_nontemporal_store(x, reinterpret_cast<uint16_t *>(p + g0));
     else *reinterpret_cast<uint16_t *>(p + g0) = x;
@@ -191,16 +196,101 @@ __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint3
   rc = popc(voted & ~granted & voters);
 }
 
+// One tile (64 lanes x PAIRS pairs) of qe_commit_vote.  GUARD = false on
+// every tile that lies wholly inside [0, G): then no load or store carries
+// a bounds branch and all the tile's loads issue back to back.
+template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NTL, bool NTS, bool GUARD>
+__device__ __forceinline__ void cv_tile(const CVArgs &a, uint64_t t, int lane, bool want_stats,
+                                        uint64_t (&cnt)[C_N]) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr uint64_t kTile = 64ull * PAIRS;
+  const uint64_t G = a.G;
+  uint64_t v[PAIRS][2][S];
+  uint32_t mi[PAIRS][2], mo[PAIRS][2], ml[PAIRS][2], vd[PAIRS][2], gr[PAIRS][2];
+  // ---- masked configs: voter masks first, so that slot rows no group of
+  // this wave uses (learner / empty slots) are not fetched at all ----
+  uint32_t used = kFull;
+  if constexpr (MODE >= 1) {
+    uint32_t u = 0;
+#pragma unroll
+    for (int j = 0; j < PAIRS; j++) {
+      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+      ld_mask_pair<MT, VEC, GUARD>(a.inc, g0, G, mi[j][0], mi[j][1]);
+      if constexpr (MODE == 2) ld_mask_pair<MT, VEC, GUARD>(a.out, g0, G, mo[j][0], mo[j][1]);
+      else mo[j][0] = mo[j][1] = 0;
+      u |= mi[j][0] | mi[j][1] | mo[j][0] | mo[j][1];
+    }
+    used = wave_or(u) & kFull;
+  } else {
+#pragma unroll
+    for (int j = 0; j < PAIRS; j++) {
+      mi[j][0] = mi[j][1] = kFull;
+      mo[j][0] = mo[j][1] = 0;
+    }
+  }
+  // ---- issue every remaining load of the tile (bytes in flight) ----
+#pragma unroll
+  for (int j = 0; j < PAIRS; j++) {
+    const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      if (MODE == 0 || ((used >> s) & 1u))
+        ld_u64_pair<VEC, NTL, GUARD>(a.match + s * a.stride, g0, G, v[j][0][s], v[j][1][s]);
+      else
+        v[j][0][s] = v[j][1][s] = 0;  // no group of the wave has a voter here
+    }
+    if (a.learner) ld_mask_pair<MT, VEC, GUARD>(a.learner, g0, G, ml[j][0], ml[j][1]);
+    else ml[j][0] = ml[j][1] = 0;
+    if (a.voted) {
+      ld_mask_pair<MT, VEC, GUARD>(a.voted, g0, G, vd[j][0], vd[j][1]);
+      if (a.granted) ld_mask_pair<MT, VEC, GUARD>(a.granted, g0, G, gr[j][0], gr[j][1]);
+      else gr[j][0] = gr[j][1] = 0;
+    } else {
+      vd[j][0] = vd[j][1] = gr[j][0] = gr[j][1] = 0;
+    }
+  }
+  // ---- compute + store ----
+#pragma unroll
+  for (int j = 0; j < PAIRS; j++) {
+    const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+    uint64_t c[2];
+    uint32_t vt[2], gc[2], rc[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t inc = mi[j][h] & kFull, out = mo[j][h] & kFull, lrn = ml[j][h] & kFull;
+      const uint32_t vv = vd[j][h] & kFull, gg = gr[j][h] & kFull;
+      eval_group<S, MODE>(v[j][h], inc, out, lrn, vv, gg, c[h], vt[h], gc[h], rc[h]);
+      if (want_stats && (!GUARD || g0 + h < G)) {
+        cnt[C_GROUPS] += 1;
+        cnt[C_INF] += (c[h] == kInf);
+        cnt[C_SUM] += (c[h] == kInf) ? 0 : c[h];
+        cnt[C_ZERO] += (c[h] == 0);
+        cnt[C_WON] += (vt[h] == kVoteWon);
+        cnt[C_LOST] += (vt[h] == kVoteLost);
+        cnt[C_PEND] += (vt[h] == kVotePending);
+        cnt[C_GR] += gc[h];
+        cnt[C_RJ] += rc[h];
+        cnt[C_VIOL] += ((lrn & (inc | out)) != 0);
+        const uint64_t tag = static_cast<uint64_t>(vt[h] | (gc[h] << 2) | (rc[h] << 7)) << 52;
+        cnt[C_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
+      }
+    }
+    if (a.commit) st_u64_pair<VEC, NTS, GUARD>(a.commit, g0, G, c[0], c[1]);
+    if (a.vote) st_u8_pair<VEC, NTS, GUARD>(a.vote, g0, G, vt[0], vt[1]);
+    if (a.gcount) st_u8_pair<VEC, NTS, GUARD>(a.gcount, g0, G, gc[0], gc[1]);
+    if (a.rcount) st_u8_pair<VEC, NTS, GUARD>(a.rcount, g0, G, rc[0], rc[1]);
+  }
+}
+
 template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
-  constexpr uint32_t kFull = (1u << S) - 1u;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * kBlock) >> 6;
-  const uint64_t G = a.G;
-  const uint64_t npairs = (G + 1) >> 1;
+  const uint64_t npairs = (a.G + 1) >> 1;
   constexpr uint64_t kTile = 64ull * PAIRS;
   const uint64_t ntiles = (npairs + kTile - 1) / kTile;
+  const uint64_t nfull = a.G / (2 * kTile);  // tiles wholly inside [0, G)
   const bool want_stats = a.stats != nullptr;
 
   uint64_t cnt[C_N];
@@ -208,60 +298,10 @@ __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
   for (int i = 0; i < C_N; i++) cnt[i] = 0;
 
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    uint64_t v[PAIRS][2][S];
-    uint32_t mi[PAIRS][2], mo[PAIRS][2], ml[PAIRS][2], vd[PAIRS][2], gr[PAIRS][2];
-    // ---- issue every load of the tile first (bytes in flight) ----
-#pragma unroll
-    for (int j = 0; j < PAIRS; j++) {
-      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
-#pragma unroll
-      for (int s = 0; s < S; s++)
-        ld_u64_pair<VEC, NTL>(a.match + s * a.stride, g0, G, v[j][0][s], v[j][1][s]);
-      if constexpr (MODE >= 1) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[j][0], mi[j][1]);
-      else mi[j][0] = mi[j][1] = kFull;
-      if constexpr (MODE == 2) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[j][0], mo[j][1]);
-      else mo[j][0] = mo[j][1] = 0;
-      if (a.learner) ld_mask_pair<MT, VEC>(a.learner, g0, G, ml[j][0], ml[j][1]);
-      else ml[j][0] = ml[j][1] = 0;
-      if (a.voted) {
-        ld_mask_pair<MT, VEC>(a.voted, g0, G, vd[j][0], vd[j][1]);
-        if (a.granted) ld_mask_pair<MT, VEC>(a.granted, g0, G, gr[j][0], gr[j][1]);
-        else gr[j][0] = gr[j][1] = 0;
-      } else {
-        vd[j][0] = vd[j][1] = gr[j][0] = gr[j][1] = 0;
-      }
-    }
-    // ---- compute + store ----
-#pragma unroll
-    for (int j = 0; j < PAIRS; j++) {
-      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
-      uint64_t c[2];
-      uint32_t vt[2], gc[2], rc[2];
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const uint32_t inc = mi[j][h] & kFull, out = mo[j][h] & kFull, lrn = ml[j][h] & kFull;
-        const uint32_t vv = vd[j][h] & kFull, gg = gr[j][h] & kFull;
-        eval_group<S, MODE>(v[j][h], inc, out, lrn, vv, gg, c[h], vt[h], gc[h], rc[h]);
-        if (want_stats && g0 + h < G) {
-          cnt[C_GROUPS] += 1;
-          cnt[C_INF] += (c[h] == kInf);
-          cnt[C_SUM] += (c[h] == kInf) ? 0 : c[h];
-          cnt[C_ZERO] += (c[h] == 0);
-          cnt[C_WON] += (vt[h] == kVoteWon);
-          cnt[C_LOST] += (vt[h] == kVoteLost);
-          cnt[C_PEND] += (vt[h] == kVotePending);
-          cnt[C_GR] += gc[h];
-          cnt[C_RJ] += rc[h];
-          cnt[C_VIOL] += ((lrn & (inc | out)) != 0);
-          const uint64_t tag = static_cast<uint64_t>(vt[h] | (gc[h] << 2) | (rc[h] << 7)) << 52;
-          cnt[C_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
-        }
-      }
-      if (a.commit) st_u64_pair<VEC, NTS>(a.commit, g0, G, c[0], c[1]);
-      if (a.vote) st_u8_pair<VEC, NTS>(a.vote, g0, G, vt[0], vt[1]);
-      if (a.gcount) st_u8_pair<VEC, NTS>(a.gcount, g0, G, gc[0], gc[1]);
-      if (a.rcount) st_u8_pair<VEC, NTS>(a.rcount, g0, G, rc[0], rc[1]);
-    }
+    if (VEC && t < nfull)
+      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, false>(a, t, lane, want_stats, cnt);
+    else
+      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, true>(a, t, lane, want_stats, cnt);
   }
   if (want_stats) {
     const int idx[C_N] = {QE_STAT_GROUPS,     QE_STAT_COMMIT_INF,   QE_STAT_COMMIT_SUM,
@@ -286,80 +326,89 @@ struct RArgs {
 
 enum { R_GROUPS, R_SUM, R_ADV, R_READ, R_VIOL, R_CSUM, R_N };
 
+template <int S, bool JOINT, bool MASKED, typename MT, bool VEC, bool NT, bool GUARD>
+__device__ __forceinline__ void repl_tile(const RArgs &a, uint64_t t, int lane, bool want_stats,
+                                          uint64_t (&cnt)[R_N]) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const uint64_t G = a.G;
+  const uint64_t g0 = 2 * (t * 64 + lane);
+  uint32_t mi[2], mo[2], rm[2], ack[2];
+  if (MASKED) ld_mask_pair<MT, VEC, GUARD>(a.inc, g0, G, mi[0], mi[1]);
+  else mi[0] = mi[1] = kFull;
+  if (JOINT) ld_mask_pair<MT, VEC, GUARD>(a.out, g0, G, mo[0], mo[1]);
+  else mo[0] = mo[1] = 0;
+  if (a.resp_mask) ld_mask_pair<MT, VEC, GUARD>(a.resp_mask, g0, G, rm[0], rm[1]);
+  else rm[0] = rm[1] = 0;
+  if (a.read_acks) ld_mask_pair<MT, VEC, GUARD>(a.read_acks, g0, G, ack[0], ack[1]);
+  else ack[0] = ack[1] = 0;
+  uint64_t ts[2], li[2], cm[2];
+  ld_u64_pair<VEC, NT, GUARD>(a.term_start, g0, G, ts[0], ts[1]);
+  ld_u64_pair<VEC, NT, GUARD>(a.last_index, g0, G, li[0], li[1]);
+  ld_u64_pair<VEC, NT, GUARD>(a.committed, g0, G, cm[0], cm[1]);
+
+  // Progress.MaybeUpdate on every responding slot (progress.go:144-153),
+  // streamed slot by slot: read match/next/resp, update, write back.
+  uint64_t sel[2][S];
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    uint64_t m[2], n[2], r[2];
+    ld_u64_pair<VEC, NT, GUARD>(a.match + s * a.stride, g0, G, m[0], m[1]);
+    ld_u64_pair<VEC, NT, GUARD>(a.next + s * a.stride, g0, G, n[0], n[1]);
+    ld_u64_pair<VEC, NT, GUARD>(a.resp + s * a.stride, g0, G, r[0], r[1]);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const bool resp = (rm[h] >> s) & 1u;
+      m[h] = (resp && m[h] < r[h]) ? r[h] : m[h];
+      n[h] = (resp && n[h] < r[h] + 1) ? r[h] + 1 : n[h];
+      sel[h][s] = m[h];
+    }
+    st_u64_pair<VEC, NT, GUARD>(a.match + s * a.stride, g0, G, m[0], m[1]);
+    st_u64_pair<VEC, NT, GUARD>(a.next + s * a.stride, g0, G, n[0], n[1]);
+  }
+
+  uint32_t ro[2], adv[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t inc = mi[h] & kFull, out = mo[h] & kFull;
+    const uint64_t mci = (!JOINT && !MASKED) ? select_fixed<S>(sel[h])
+                                             : joint_committed<S>(sel[h], inc, out);
+    // raftLog.maybeCommit with term(i)==Term <=> term_start<=i<=last_index
+    adv[h] = (mci > cm[h] && mci >= ts[h] && mci <= li[h]) ? 1u : 0u;
+    cm[h] = adv[h] ? mci : cm[h];
+    const uint32_t acks = ack[h] & kFull;
+    ro[h] = a.read_acks ? (joint_vote(inc, out, acks, acks) == kVoteWon) : 0u;
+    if (want_stats && (!GUARD || g0 + h < G)) {
+      cnt[R_GROUPS] += 1;
+      cnt[R_SUM] += cm[h];
+      cnt[R_ADV] += adv[h];
+      cnt[R_READ] += ro[h];
+      cnt[R_VIOL] += (mci > li[h]);
+      const uint64_t tag = (static_cast<uint64_t>(ro[h]) << 62) | (static_cast<uint64_t>(adv[h]) << 61);
+      cnt[R_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ cm[h] ^ tag);
+    }
+  }
+  st_u64_pair<VEC, NT, GUARD>(a.committed, g0, G, cm[0], cm[1]);
+  if (a.read_ok) st_u8_pair<VEC, NT, GUARD>(a.read_ok, g0, G, ro[0], ro[1]);
+  if (a.adv) st_u8_pair<VEC, NT, GUARD>(a.adv, g0, G, adv[0], adv[1]);
+}
+
 template <int S, bool JOINT, bool MASKED, typename MT, bool VEC, bool NT>
 __global__ __launch_bounds__(kBlock) void k_replication(RArgs a) {
-  constexpr uint32_t kFull = (1u << S) - 1u;
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * kBlock) >> 6;
-  const uint64_t G = a.G;
-  const uint64_t npairs = (G + 1) >> 1;
+  const uint64_t npairs = (a.G + 1) >> 1;
   const uint64_t ntiles = (npairs + 63) / 64;
+  const uint64_t nfull = a.G / 128;
   const bool want_stats = a.stats != nullptr;
   uint64_t cnt[R_N];
 #pragma unroll
   for (int i = 0; i < R_N; i++) cnt[i] = 0;
-
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    const uint64_t g0 = 2 * (t * 64 + lane);
-    uint32_t mi[2], mo[2], rm[2], ack[2];
-    if (MASKED) ld_mask_pair<MT, VEC>(a.inc, g0, G, mi[0], mi[1]);
-    else mi[0] = mi[1] = kFull;
-    if (JOINT) ld_mask_pair<MT, VEC>(a.out, g0, G, mo[0], mo[1]);
-    else mo[0] = mo[1] = 0;
-    if (a.resp_mask) ld_mask_pair<MT, VEC>(a.resp_mask, g0, G, rm[0], rm[1]);
-    else rm[0] = rm[1] = 0;
-    if (a.read_acks) ld_mask_pair<MT, VEC>(a.read_acks, g0, G, ack[0], ack[1]);
-    else ack[0] = ack[1] = 0;
-    uint64_t ts[2], li[2], cm[2];
-    ld_u64_pair<VEC, NT>(a.term_start, g0, G, ts[0], ts[1]);
-    ld_u64_pair<VEC, NT>(a.last_index, g0, G, li[0], li[1]);
-    ld_u64_pair<VEC, NT>(a.committed, g0, G, cm[0], cm[1]);
-
-    // Progress.MaybeUpdate on every responding slot (progress.go:144-153),
-    // streamed slot by slot: read match/next/resp, update, write back.
-    uint64_t sel[2][S];
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      uint64_t m[2], n[2], r[2];
-      ld_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, m[0], m[1]);
-      ld_u64_pair<VEC, NT>(a.next + s * a.stride, g0, G, n[0], n[1]);
-      ld_u64_pair<VEC, NT>(a.resp + s * a.stride, g0, G, r[0], r[1]);
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const bool resp = (rm[h] >> s) & 1u;
-        m[h] = (resp && m[h] < r[h]) ? r[h] : m[h];
-        n[h] = (resp && n[h] < r[h] + 1) ? r[h] + 1 : n[h];
-        sel[h][s] = m[h];
-      }
-      st_u64_pair<VEC, NT>(a.match + s * a.stride, g0, G, m[0], m[1]);
-      st_u64_pair<VEC, NT>(a.next + s * a.stride, g0, G, n[0], n[1]);
-    }
-
-    uint32_t ro[2], adv[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint32_t inc = mi[h] & kFull, out = mo[h] & kFull;
-      const uint64_t mci = (!JOINT && !MASKED) ? select_fixed<S>(sel[h])
-                                               : joint_committed<S>(sel[h], inc, out);
-      // raftLog.maybeCommit with term(i)==Term <=> term_start<=i<=last_index
-      adv[h] = (mci > cm[h] && mci >= ts[h] && mci <= li[h]) ? 1u : 0u;
-      cm[h] = adv[h] ? mci : cm[h];
-      const uint32_t acks = ack[h] & kFull;
-      ro[h] = a.read_acks ? (joint_vote(inc, out, acks, acks) == kVoteWon) : 0u;
-      if (want_stats && g0 + h < G) {
-        cnt[R_GROUPS] += 1;
-        cnt[R_SUM] += cm[h];
-        cnt[R_ADV] += adv[h];
-        cnt[R_READ] += ro[h];
-        cnt[R_VIOL] += (mci > li[h]);
-        const uint64_t tag = (static_cast<uint64_t>(ro[h]) << 62) | (static_cast<uint64_t>(adv[h]) << 61);
-        cnt[R_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ cm[h] ^ tag);
-      }
-    }
-    st_u64_pair<VEC, NT>(a.committed, g0, G, cm[0], cm[1]);
-    if (a.read_ok) st_u8_pair<VEC, NT>(a.read_ok, g0, G, ro[0], ro[1]);
-    if (a.adv) st_u8_pair<VEC, NT>(a.adv, g0, G, adv[0], adv[1]);
+    if (VEC && t < nfull)
+      repl_tile<S, JOINT, MASKED, MT, VEC, NT, false>(a, t, lane, want_stats, cnt);
+    else
+      repl_tile<S, JOINT, MASKED, MT, VEC, NT, true>(a, t, lane, want_stats, cnt);
   }
   if (want_stats) {
     const int idx[R_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
@@ -560,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_gen(GArgs a) {
     const uint64_t gid = a.goff + g;
     const uint64_t hb = hash4(a.p.seed, gid, 0xFFFFu, 0);
     uint32_t mi, mo, ml;
-    if (a.p.mask_mode == 0) {
+    if (a.p.mask_mode == 0 || a.p.mask_mode == 2) {
       uint32_t ni = a.p.n_inc ? a.p.n_inc : S;
       if (ni > S) ni = S;
       uint32_t no = a.p.n_out > S ? S : a.p.n_out;
@@ -571,13 +620,14 @@ __global__ __launch_bounds__(kBlock) void k_gen(GArgs a) {
       } else {
         const uint32_t omin = (ni + no > S) ? ni + no - S : 0;
         const uint32_t omax = ni < no ? ni : no;
-        const uint32_t o = omin + static_cast<uint32_t>((hb >> 8) % (omax - omin + 1));
+        const uint64_t okey = a.p.mask_mode == 2 ? (gid >> 20) : (hb >> 8);
+        const uint32_t o = omin + static_cast<uint32_t>(okey % (omax - omin + 1));
         const uint32_t uni = ni + no - o;
         mi = (1u << ni) - 1u;
         mo = ((1u << no) - 1u) << (ni - o);
         ml = full & ~((1u << uni) - 1u);
       }
-      const uint32_t r = static_cast<uint32_t>((hb >> 16) % S);
+      const uint32_t r = a.p.mask_mode == 2 ? 0u : static_cast<uint32_t>((hb >> 16) % S);
       mi = rotl_s(mi, r, S);
       mo = rotl_s(mo, r, S);
       ml = rotl_s(ml, r, S);

@@ -134,7 +134,8 @@ size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
 /* Optional launch tuning (no reference counterpart; never changes results):
  *   "blocks_per_cu"  cap on persistent-grid workgroups per CU, 0..32
  *                    (default 0 = the kernel's occupancy)
- *   "tiles_per_wave" 0 = persistent grid; T > 0: each wave walks T tiles
+ *   "tiles_per_wave" -1 = per-kernel default (measured best), 0 =
+ *                    persistent grid, T > 0: each wave walks T tiles
  *   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
  *                    of qe_commit_vote                                     */
 int qe_tune(const char *key, int value);
@@ -263,7 +264,9 @@ typedef struct qe_gen_params {
   uint32_t p_granted_q16;    /* P(granted | voted) * 65536                   */
   uint32_t n_inc;            /* joint: incoming voters (0 = all S slots)     */
   uint32_t n_out;            /* joint: outgoing voters (0 = non-joint)       */
-  uint32_t mask_mode;        /* 0 structured (config 3), 1 arbitrary random  */
+  uint32_t mask_mode;        /* 0 structured + rotated, 1 arbitrary random,
+                                2 shape-bucketed (voters in low slots, overlap
+                                constant per 2^20 consecutive groups)        */
   uint32_t reserved;
 } qe_gen_params;
 

@@ -73,7 +73,11 @@ void orc_gen_group(uint64_t seed, uint64_t gid, uint32_t S, uint32_t dist,
   uint64_t hb = orc_hash(seed, gid, 0xFFFFu, 0);
   /* masks */
   uint32_t mi, mo, ml;
-  if (mask_mode == 0) {
+  if (mask_mode == 0 || mask_mode == 2) {
+    /* 0: structured, rotated per group; 2: shape-bucketed -- voters packed
+     * into the low slots (no rotation) and the overlap constant over runs of
+     * 2^20 consecutive group ids, the layout a host packer produces when it
+     * buckets groups by configuration shape. */
     uint32_t ni = n_inc ? n_inc : S;
     if (ni > S) ni = S;
     uint32_t no = n_out;
@@ -85,13 +89,14 @@ void orc_gen_group(uint64_t seed, uint64_t gid, uint32_t S, uint32_t dist,
     } else {
       uint32_t omin = (ni + no > S) ? ni + no - S : 0;
       uint32_t omax = ni < no ? ni : no;
-      uint32_t o = omin + (uint32_t)((hb >> 8) % (uint64_t)(omax - omin + 1));
+      uint64_t okey = mask_mode == 2 ? (gid >> 20) : (hb >> 8);
+      uint32_t o = omin + (uint32_t)(okey % (uint64_t)(omax - omin + 1));
       uint32_t uni = ni + no - o;
       mi = (1u << ni) - 1u;
       mo = ((1u << no) - 1u) << (ni - o);
       ml = full & ~((1u << uni) - 1u);
     }
-    uint32_t r = (uint32_t)((hb >> 16) % S);
+    uint32_t r = mask_mode == 2 ? 0u : (uint32_t)((hb >> 16) % S);
     mi = rotl_s(mi, r, S);
     mo = rotl_s(mo, r, S);
     ml = rotl_s(ml, r, S);

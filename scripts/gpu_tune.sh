@@ -8,8 +8,9 @@ for p in ${PAIRS:-}; do
 done
 rm -f gpurun_out/tune.log
 for lib in $LIBS; do
-  for s in ${SLOTS:-5 7}; do
-    QE_LIB=$R/etcd_amd/lib/$lib TUNE_S=$s timeout -k 10 240 python scripts/tune_cv.py >> gpurun_out/tune.log 2>&1 || { echo tune failed; tail gpurun_out/tune.log; exit 3; }
+  for cfg in ${CFGS:-majority:5:0 majority:7:0 joint:10:0 joint:10:2}; do
+    IFS=: read mode s mm <<< "$cfg"
+    QE_LIB=$R/etcd_amd/lib/$lib TUNE_MODE=$mode TUNE_S=$s TUNE_MASK_MODE=$mm TUNE_G=$([ $mode = joint ] && echo 134217728 || echo 67108864) timeout -k 10 240 python scripts/tune_cv.py >> gpurun_out/tune.log 2>&1 || { echo tune failed; tail gpurun_out/tune.log; exit 3; }
   done
 done
 grep '^{' gpurun_out/tune.log

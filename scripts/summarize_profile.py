@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {
     "config2_n5": "void qe::k_commit_vote<5, 0,",
     "config2_n7": "void qe::k_commit_vote<7, 0,",
-    "config3_joint": "void qe::k_commit_vote<10, 2,",
+    "config3_joint": "void qe::k_commit_vote<10, 2,",  # bucketed + rotated runs share it
     "config4_repl": "void qe::k_replication<5,",
     "config5_elec": "void qe::k_election<5,",
 }

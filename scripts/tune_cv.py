@@ -18,16 +18,19 @@ G = int(os.environ.get("TUNE_G", 1 << 26))
 S = int(os.environ.get("TUNE_S", 5))
 ROUNDS, LAUNCHES = 5, 20
 VARIANTS = []
-for tpw in (0, 1, 2, 4, 8):
-    for nt in (0, 1, 3):
-        VARIANTS.append({"tiles_per_wave": tpw, "blocks_per_cu": 0, "nontemporal": nt, "stats": 1})
-VARIANTS.append({"tiles_per_wave": 1, "blocks_per_cu": 0, "nontemporal": 1, "stats": 0})
-VARIANTS.append({"tiles_per_wave": 2, "blocks_per_cu": 0, "nontemporal": 1, "stats": 0})
+for tpw in (-1, 0, 1, 2, 4, 8):
+    VARIANTS.append({"tiles_per_wave": tpw, "blocks_per_cu": 0, "nontemporal": 3, "stats": 1})
 if os.environ.get("TUNE_ONLY_DEFAULT"):
     VARIANTS = VARIANTS[:1]
+MODE = os.environ.get("TUNE_MODE", "majority")
 dev = torch.device("cuda:0")
-b = engine.SlotBatch(G, S, dev, masks=())
-engine.gen_groups(b, 0x5EED)
+if MODE == "joint":
+    b = engine.SlotBatch(G, S, dev, masks=("inc", "out", "learner"))
+    engine.gen_groups(b, 0x5EED, n_inc=S // 2, n_out=S - S // 2,
+                      mask_mode=int(os.environ.get("TUNE_MASK_MODE", "0")))
+else:
+    b = engine.SlotBatch(G, S, dev, masks=())
+    engine.gen_groups(b, 0x5EED)
 out = engine.Outputs(G, dev)
 stats = engine.stats_buffer(dev)
 gs, os_, os_nostats = b.struct(), out.struct(stats), out.struct(None)
@@ -53,6 +56,6 @@ for r in range(ROUNDS):
         res[i] += [a.elapsed_time(e) for a, e in ev]
 for i, v in enumerate(VARIANTS):
     ms = np.array(res[i])
-    print(json.dumps({"lib": os.path.basename(engine._lib.LIB_PATH), **v, "S": S,
+    print(json.dumps({"lib": os.path.basename(engine._lib.LIB_PATH), **v, "S": S, "mode": MODE, "mask_mode": os.environ.get("TUNE_MASK_MODE", "0"),
                       "median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
                       "GBs_median": bpg * G / np.median(ms) / 1e6}))

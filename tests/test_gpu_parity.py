@@ -139,7 +139,7 @@ def test_tracker_mirror(eng):
 # --------------------------------------------------------------------------
 @pytest.mark.parametrize("S,n_inc,n_out,mask_mode,dist", [
     (3, 0, 0, 0, 0), (5, 0, 0, 0, 1), (7, 0, 0, 0, 2), (10, 5, 5, 0, 0), (16, 7, 9, 0, 2),
-    (8, 0, 0, 1, 0), (13, 0, 0, 1, 1)])
+    (8, 0, 0, 1, 0), (13, 0, 0, 1, 1), (10, 5, 5, 2, 0), (7, 4, 0, 2, 2)])
 def test_generator_bit_identical(eng, orc, S, n_inc, n_out, mask_mode, dist):
     G = 4099
     b = gpu_batch(eng, G, S, 0xABCD + S, goff=77, dist=dist, n_inc=n_inc, n_out=n_out,
@@ -165,7 +165,7 @@ def test_commit_vote_fixed_majority_all_slots(eng, orc, S):
 
 @pytest.mark.parametrize("S", list(range(1, 17)))
 def test_commit_vote_masked_and_joint(eng, orc, S):
-    for mask_mode in (0, 1):
+    for mask_mode in (0, 1, 2):
         for dist in (0, 2):
             n_inc = max(1, S // 2)
             n_out = max(1, S - n_inc) if S > 1 else 1
@@ -227,6 +227,15 @@ def test_full_size_config2_bit_exact(eng, orc):
     G, S = 1 << 26, 5
     b = gpu_batch(eng, G, S, 0x5EED, masks=())
     check_commit_vote(eng, orc, b)
+
+
+def test_commit_vote_bucketed_across_buckets(eng, orc):
+    """Shape-bucketed layout (mask_mode 2) over several 2^20-group buckets:
+    whole waves skip learner slot rows; results stay bit-exact."""
+    G, S = (1 << 22) + 12345, 10
+    for goff in (0, (1 << 20) - 777):
+        b = gpu_batch(eng, G, S, 0xB0C, goff=goff, n_inc=5, n_out=5, mask_mode=2)
+        check_commit_vote(eng, orc, b, goff=goff)
 
 
 def test_full_size_config3_properties(eng, orc):
@@ -436,5 +445,5 @@ def test_tuning_knobs_do_not_change_results(eng, orc):
                     check_commit_vote(eng, orc, b)
     finally:
         eng.tune("blocks_per_cu", 0)
-        eng.tune("nontemporal", 0)
-        eng.tune("tiles_per_wave", 0)
+        eng.tune("nontemporal", 3)
+        eng.tune("tiles_per_wave", -1)
