@@ -84,6 +84,18 @@ class QeGenParams(C.Structure):
     ]
 
 
+class QeConfStateCSR(C.Structure):
+    _fields_ = [("num_groups", u64), ("voters", vp), ("voters_off", vp),
+                ("voters_outgoing", vp), ("outgoing_off", vp), ("learners", vp),
+                ("learners_off", vp), ("learners_next", vp), ("learners_next_off", vp)]
+
+
+QE_PACK_TOO_MANY_PEERS = 1
+QE_PACK_LEARNER_IS_VOTER = 2
+QE_PACK_LEARNER_NEXT_NOT_OUTGOING = 4
+QE_PACK_ZERO_ID = 8
+
+
 # Every symbol include/etcd_quorum.h declares, with its prototype.
 PROTOTYPES = {
     "qe_abi_version": (C.c_int, []),
@@ -100,6 +112,12 @@ PROTOTYPES = {
                                     vp, vp]),
     "qe_stats_reduce": (C.c_int, [vp, vp, vp]),
     "qe_gen_groups": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeGenParams), vp]),
+    "qe_apply_append_resps": (C.c_int, [u64, u32, u64, vp, vp, u64, vp, vp, vp, vp, vp]),
+    "qe_pack_confstate": (C.c_int, [C.POINTER(QeConfStateCSR), u32, vp, vp, vp, vp, vp, vp]),
+    "qe_pack_match": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, u64, vp]),
+    "qe_pack_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp]),
+    "qe_slot_lookup": (C.c_int, [u64, u32, vp, u64, vp, vp, vp]),
+    "qe_pack_threads": (C.c_int, [C.c_int]),
 }
 
 

@@ -30,6 +30,29 @@ static unsigned simple_grid(uint64_t G) {
   return static_cast<unsigned>(need < cap ? (need ? need : 1) : cap);
 }
 
+// Sparse MsgAppResp acks: Progress.MaybeUpdate with 64-bit atomic max.
+__global__ __launch_bounds__(kBlock) void k_apply_acks(uint64_t G, uint32_t S, uint64_t stride,
+                                                       uint64_t *match, uint64_t *next,
+                                                       uint64_t n, const uint64_t *group,
+                                                       const int8_t *slot,
+                                                       const uint64_t *index,
+                                                       uint8_t *touched) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint64_t g = group[i];
+    const int s = slot[i];
+    if (g >= G || s < 0 || s >= static_cast<int>(S)) continue;
+    const uint64_t x = index[i];
+    const uint64_t off = static_cast<uint64_t>(s) * stride + g;
+    atomicMax(reinterpret_cast<unsigned long long *>(match + off),
+              static_cast<unsigned long long>(x));
+    if (x != ~0ull)  // next = max(next, x+1); x+1 wraps only for x = max
+      atomicMax(reinterpret_cast<unsigned long long *>(next + off),
+                static_cast<unsigned long long>(x + 1));
+    if (touched) touched[g] = 1;
+  }
+}
+
 __global__ void k_stats_reduce(const uint64_t *stats, uint64_t *out) {
   const int c = threadIdx.x;
   if (c < QE_STATS_COUNTERS) {
@@ -291,6 +314,19 @@ int qe_election_steps(const qe_election_state *s, const qe_election_params *p, u
   a.p_grant = p->p_grant_q16;
   a.stats = stats;
   return dispatch_elec(s->num_slots, a, static_cast<hipStream_t>(stream));
+}
+
+int qe_apply_append_resps(uint64_t num_groups, uint32_t num_slots, uint64_t stride,
+                          uint64_t *match, uint64_t *next, uint64_t n, const uint64_t *group,
+                          const int8_t *slot, const uint64_t *index, uint8_t *touched,
+                          void *stream) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (n == 0 || num_groups == 0) return QE_OK;
+  if (stride < num_groups || !match || !next || !group || !slot || !index) return QE_EINVAL;
+  hipLaunchKernelGGL(k_apply_acks, dim3(simple_grid(n)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), num_groups, num_slots, stride, match,
+                     next, n, group, slot, index, touched);
+  return hip_status(hipGetLastError());
 }
 
 int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream) {

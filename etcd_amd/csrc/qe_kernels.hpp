@@ -196,30 +196,57 @@ __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint3
   rc = popc(voted & ~granted & voters);
 }
 
+// Per-thread statistics of qe_commit_vote: counts in 32 bits (a thread sees
+// far fewer than 2^32 groups), sums in 64 bits -- fewer live VGPRs.
+struct CVStats {
+  uint32_t groups = 0, inf = 0, zero = 0, won = 0, lost = 0, pend = 0, gr = 0, rj = 0, viol = 0;
+  uint64_t sum = 0, csum = 0;
+};
+
+// Voter masks (JointConfig halves) of one tile.
+template <typename MT, int MODE, int PAIRS, bool VEC, bool GUARD>
+__device__ __forceinline__ void cv_masks(const CVArgs &a, uint64_t t, int lane,
+                                         uint32_t (&mi)[PAIRS][2], uint32_t (&mo)[PAIRS][2]) {
+  constexpr uint64_t kTile = 64ull * PAIRS;
+#pragma unroll
+  for (int j = 0; j < PAIRS; j++) {
+    const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
+    ld_mask_pair<MT, VEC, GUARD>(a.inc, g0, a.G, mi[j][0], mi[j][1]);
+    if constexpr (MODE == 2) ld_mask_pair<MT, VEC, GUARD>(a.out, g0, a.G, mo[j][0], mo[j][1]);
+    else mo[j][0] = mo[j][1] = 0;
+  }
+}
+
 // One tile (64 lanes x PAIRS pairs) of qe_commit_vote.  GUARD = false on
-// every tile that lies wholly inside [0, G): then no load or store carries
-// a bounds branch and all the tile's loads issue back to back.
+// every tile that lies wholly inside [0, G): then no load or store carries a
+// bounds branch and all the tile's loads issue back to back.  Masked modes
+// receive this tile's voter masks (mi/mo, loaded one tile ahead) and prefetch
+// the next tile's into mi_n/mo_n after issuing this tile's loads, so the
+// dependent mask -> row-skip decision costs no extra memory round trip.
 template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NTL, bool NTS, bool GUARD>
 __device__ __forceinline__ void cv_tile(const CVArgs &a, uint64_t t, int lane, bool want_stats,
-                                        uint64_t (&cnt)[C_N]) {
+                                        CVStats &st, const uint32_t (&mi_in)[PAIRS][2],
+                                        const uint32_t (&mo_in)[PAIRS][2], uint64_t tn,
+                                        uint64_t ntiles, uint64_t nfull,
+                                        uint32_t (&mi_n)[PAIRS][2], uint32_t (&mo_n)[PAIRS][2]) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint64_t kTile = 64ull * PAIRS;
   const uint64_t G = a.G;
   uint64_t v[PAIRS][2][S];
   uint32_t mi[PAIRS][2], mo[PAIRS][2], ml[PAIRS][2], vd[PAIRS][2], gr[PAIRS][2];
-  // ---- masked configs: voter masks first, so that slot rows no group of
-  // this wave uses (learner / empty slots) are not fetched at all ----
+  // ---- slot rows no group of this wave uses (learner / empty slots) are
+  // not fetched at all ----
   uint32_t used = kFull;
   if constexpr (MODE >= 1) {
     uint32_t u = 0;
 #pragma unroll
-    for (int j = 0; j < PAIRS; j++) {
-      const uint64_t g0 = 2 * (t * kTile + j * 64 + lane);
-      ld_mask_pair<MT, VEC, GUARD>(a.inc, g0, G, mi[j][0], mi[j][1]);
-      if constexpr (MODE == 2) ld_mask_pair<MT, VEC, GUARD>(a.out, g0, G, mo[j][0], mo[j][1]);
-      else mo[j][0] = mo[j][1] = 0;
-      u |= mi[j][0] | mi[j][1] | mo[j][0] | mo[j][1];
-    }
+    for (int j = 0; j < PAIRS; j++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        mi[j][h] = mi_in[j][h];
+        mo[j][h] = mo_in[j][h];
+        u |= mi[j][h] | mo[j][h];
+      }
     used = wave_or(u) & kFull;
   } else {
 #pragma unroll
@@ -249,6 +276,13 @@ __device__ __forceinline__ void cv_tile(const CVArgs &a, uint64_t t, int lane, b
       vd[j][0] = vd[j][1] = gr[j][0] = gr[j][1] = 0;
     }
   }
+  // ---- prefetch the next tile's voter masks ----
+  if constexpr (MODE >= 1) {
+    if (tn < ntiles) {
+      if (VEC && tn < nfull) cv_masks<MT, MODE, PAIRS, VEC, false>(a, tn, lane, mi_n, mo_n);
+      else cv_masks<MT, MODE, PAIRS, VEC, true>(a, tn, lane, mi_n, mo_n);
+    }
+  }
   // ---- compute + store ----
 #pragma unroll
   for (int j = 0; j < PAIRS; j++) {
@@ -261,18 +295,18 @@ __device__ __forceinline__ void cv_tile(const CVArgs &a, uint64_t t, int lane, b
       const uint32_t vv = vd[j][h] & kFull, gg = gr[j][h] & kFull;
       eval_group<S, MODE>(v[j][h], inc, out, lrn, vv, gg, c[h], vt[h], gc[h], rc[h]);
       if (want_stats && (!GUARD || g0 + h < G)) {
-        cnt[C_GROUPS] += 1;
-        cnt[C_INF] += (c[h] == kInf);
-        cnt[C_SUM] += (c[h] == kInf) ? 0 : c[h];
-        cnt[C_ZERO] += (c[h] == 0);
-        cnt[C_WON] += (vt[h] == kVoteWon);
-        cnt[C_LOST] += (vt[h] == kVoteLost);
-        cnt[C_PEND] += (vt[h] == kVotePending);
-        cnt[C_GR] += gc[h];
-        cnt[C_RJ] += rc[h];
-        cnt[C_VIOL] += ((lrn & (inc | out)) != 0);
+        st.groups += 1;
+        st.inf += (c[h] == kInf);
+        st.sum += (c[h] == kInf) ? 0 : c[h];
+        st.zero += (c[h] == 0);
+        st.won += (vt[h] == kVoteWon);
+        st.lost += (vt[h] == kVoteLost);
+        st.pend += (vt[h] == kVotePending);
+        st.gr += gc[h];
+        st.rj += rc[h];
+        st.viol += ((lrn & (inc | out)) != 0);
         const uint64_t tag = static_cast<uint64_t>(vt[h] | (gc[h] << 2) | (rc[h] << 7)) << 52;
-        cnt[C_CSUM] += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
+        st.csum += mix64(((a.goff + g0 + h) * kPhi) ^ c[h] ^ tag);
       }
     }
     if (a.commit) st_u64_pair<VEC, NTS, GUARD>(a.commit, g0, G, c[0], c[1]);
@@ -282,8 +316,13 @@ __device__ __forceinline__ void cv_tile(const CVArgs &a, uint64_t t, int lane, b
   }
 }
 
+#ifndef QE_JOINT_MIN_WAVES
+#define QE_JOINT_MIN_WAVES 1  // min waves per SIMD requested for the joint kernel
+#endif
 template <int S, int MODE, typename MT, int PAIRS, bool VEC, bool NTL, bool NTS>
-__global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
+                          amdgpu_waves_per_eu(MODE == 2 ? QE_JOINT_MIN_WAVES : 1)))
+void k_commit_vote(CVArgs a) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * kBlock) >> 6;
@@ -293,17 +332,35 @@ __global__ __launch_bounds__(kBlock) void k_commit_vote(CVArgs a) {
   const uint64_t nfull = a.G / (2 * kTile);  // tiles wholly inside [0, G)
   const bool want_stats = a.stats != nullptr;
 
-  uint64_t cnt[C_N];
-#pragma unroll
-  for (int i = 0; i < C_N; i++) cnt[i] = 0;
-
+  CVStats st;
+  uint32_t mi[PAIRS][2] = {}, mo[PAIRS][2] = {};
+  if constexpr (MODE >= 1) {
+    if (wave < ntiles) {
+      if (VEC && wave < nfull) cv_masks<MT, MODE, PAIRS, VEC, false>(a, wave, lane, mi, mo);
+      else cv_masks<MT, MODE, PAIRS, VEC, true>(a, wave, lane, mi, mo);
+    }
+  }
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    uint32_t mi_n[PAIRS][2], mo_n[PAIRS][2];
     if (VEC && t < nfull)
-      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, false>(a, t, lane, want_stats, cnt);
+      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, false>(a, t, lane, want_stats, st, mi, mo,
+                                                        t + nwaves, ntiles, nfull, mi_n, mo_n);
     else
-      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, true>(a, t, lane, want_stats, cnt);
+      cv_tile<S, MODE, MT, PAIRS, VEC, NTL, NTS, true>(a, t, lane, want_stats, st, mi, mo,
+                                                       t + nwaves, ntiles, nfull, mi_n, mo_n);
+    if constexpr (MODE >= 1) {
+#pragma unroll
+      for (int j = 0; j < PAIRS; j++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          mi[j][h] = mi_n[j][h];
+          mo[j][h] = mo_n[j][h];
+        }
+    }
   }
   if (want_stats) {
+    uint64_t cnt[C_N] = {st.groups, st.inf, st.sum, st.zero, st.won, st.lost,
+                         st.pend,   st.gr,  st.rj,  st.viol, st.csum};
     const int idx[C_N] = {QE_STAT_GROUPS,     QE_STAT_COMMIT_INF,   QE_STAT_COMMIT_SUM,
                           QE_STAT_COMMIT_ZERO, QE_STAT_VOTE_WON,    QE_STAT_VOTE_LOST,
                           QE_STAT_VOTE_PENDING, QE_STAT_GRANTED,    QE_STAT_REJECTED,

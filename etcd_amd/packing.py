@@ -8,6 +8,8 @@ so any injective ID -> slot assignment is legal.  We assign the union of
 JointConfig.IDs() (raft/quorum/joint.go:30-38) in ascending ID order, then
 learners, so a group's slots are [voters..., learners...].
 """
+import ctypes
+
 import numpy as np
 
 MAX_SLOTS = 16
@@ -85,3 +87,93 @@ def pack(groups, num_slots=None):
         p.inc[gi], p.out[gi], p.learner[gi] = mi, mo, ml
         p.voted[gi], p.granted[gi], p.recent[gi] = vd, gr, ra
     return p
+
+
+# ---------------------------------------------------------------------------
+# Native (C++) packer: the wire-format path used at scale.
+# ---------------------------------------------------------------------------
+def _csr(lists):
+    """list of id-iterables -> (ids uint64, off uint64[G+1])."""
+    lens = np.fromiter((len(x) for x in lists), dtype=np.uint64, count=len(lists))
+    off = np.zeros(len(lists) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    ids = np.fromiter((i for x in lists for i in x), dtype=np.uint64, count=int(off[-1]))
+    return ids, off
+
+
+class ConfStates:
+    """G raftpb.ConfState messages (raft/raftpb/raft.proto:115-130) in CSR
+    form: each field is (ids uint64, off uint64[G+1]) or None."""
+
+    def __init__(self, voters, voters_outgoing=None, learners=None, learners_next=None):
+        self.G = len(voters)
+        self.voters = _csr(voters)
+        self.voters_outgoing = _csr(voters_outgoing) if voters_outgoing is not None else None
+        self.learners = _csr(learners) if learners is not None else None
+        self.learners_next = _csr(learners_next) if learners_next is not None else None
+
+    def struct(self):
+        from ._lib import QeConfStateCSR
+
+        def p(x, i):
+            return None if x is None else x[i].ctypes.data_as(ctypes.c_void_p)
+        return QeConfStateCSR(self.G, p(self.voters, 0), p(self.voters, 1),
+                              p(self.voters_outgoing, 0), p(self.voters_outgoing, 1),
+                              p(self.learners, 0), p(self.learners, 1),
+                              p(self.learners_next, 0), p(self.learners_next, 1))
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def pack_confstates(cs, num_slots):
+    """Native qe_pack_confstate -> PackedGroups (masks, slot_ids) + flags."""
+    from . import _lib
+    p = PackedGroups(cs.G, num_slots)
+    flags = np.zeros(cs.G, dtype=np.uint32)
+    nflag = ctypes.c_uint64(0)
+    st = cs.struct()
+    _lib.check("qe_pack_confstate", _lib.lib().qe_pack_confstate(
+        ctypes.byref(st), num_slots, _np_ptr(p.inc), _np_ptr(p.out), _np_ptr(p.learner),
+        _np_ptr(p.slot_ids), _np_ptr(flags), ctypes.byref(nflag)))
+    p.flags = flags
+    p.num_flagged = int(nflag.value)
+    p.joint = cs.voters_outgoing is not None
+    return p
+
+
+def pack_progress(p, progress, stride=None):
+    """progress: list (per group) of {id: Match} -> p.match via qe_pack_match."""
+    from . import _lib
+    ids, off = _csr([list(d.keys()) for d in progress])
+    vals = np.fromiter((v for d in progress for v in d.values()), dtype=np.uint64,
+                       count=int(off[-1]))
+    stride = stride or p.G
+    match = np.zeros(p.S * stride, dtype=np.uint64)
+    unknown = ctypes.c_uint64(0)
+    _lib.check("qe_pack_match", _lib.lib().qe_pack_match(
+        p.G, p.S, _np_ptr(p.slot_ids), _np_ptr(off), _np_ptr(ids), _np_ptr(vals),
+        _np_ptr(match), stride, ctypes.byref(unknown)))
+    p.match = match.reshape(p.S, stride)[:, : p.G]
+    return int(unknown.value)
+
+
+def pack_votes(p, votes):
+    """votes: list (per group) of [(id, bool), ...] in arrival order."""
+    from . import _lib
+    ids, off = _csr([[i for i, _ in v] for v in votes])
+    vals = np.fromiter((int(b) for v in votes for _, b in v), dtype=np.uint8, count=int(off[-1]))
+    _lib.check("qe_pack_votes", _lib.lib().qe_pack_votes(
+        p.G, p.S, _np_ptr(p.slot_ids), _np_ptr(off), _np_ptr(ids), _np_ptr(vals),
+        _np_ptr(p.voted), _np_ptr(p.granted)))
+
+
+def slot_lookup(p, group, ids):
+    from . import _lib
+    group = np.ascontiguousarray(group, dtype=np.uint64)
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    out = np.zeros(len(ids), dtype=np.int8)
+    _lib.check("qe_slot_lookup", _lib.lib().qe_slot_lookup(
+        p.G, p.S, _np_ptr(p.slot_ids), len(ids), _np_ptr(group), _np_ptr(ids), _np_ptr(out)))
+    return out

@@ -248,6 +248,67 @@ int qe_election_steps(const qe_election_state *st,
                       const qe_election_params *p, uint64_t *stats,
                       void *stream);
 
+/* ---- sparse MsgAppResp deltas ------------------------------------------ */
+
+/* Apply n MsgAppResp acks in COO form -- ack i: group[i], slot[i] (-1 =
+ * skip), index[i] -- with Progress.MaybeUpdate semantics
+ * (raft/tracker/progress.go:144-153): match = max(match, index),
+ * next = max(next, index + 1), via 64-bit atomic max.  Max is commutative,
+ * so duplicated or reordered acks give the same state as applying them one
+ * by one in any order.  touched[g] (optional) is set to 1 for every group
+ * that received an ack.  All pointers are device pointers. */
+int qe_apply_append_resps(uint64_t num_groups, uint32_t num_slots, uint64_t stride,
+                          uint64_t *match, uint64_t *next, uint64_t n, const uint64_t *group,
+                          const int8_t *slot, const uint64_t *index, uint8_t *touched,
+                          void *stream);
+
+/* ---- host-side ConfState packing (wire format -> slot SoA) -------------- */
+
+/* G ConfStates (raft/raftpb/raft.proto:115-130) in CSR form: list k of
+ * group g is ids_k[off_k[g] .. off_k[g+1]).  NULL lists are empty.  HOST
+ * pointers.  Produced by ProgressTracker.ConfState (tracker.go:146-154). */
+typedef struct qe_confstate_csr {
+  uint64_t num_groups;
+  const uint64_t *voters, *voters_off;
+  const uint64_t *voters_outgoing, *outgoing_off;
+  const uint64_t *learners, *learners_off;
+  const uint64_t *learners_next, *learners_next_off;
+} qe_confstate_csr;
+
+/* group_flags bits reported by qe_pack_confstate */
+#define QE_PACK_TOO_MANY_PEERS 1u          /* > num_slots peers: group left empty */
+#define QE_PACK_LEARNER_IS_VOTER 2u        /* confchange.go:308-318 violated      */
+#define QE_PACK_LEARNER_NEXT_NOT_OUTGOING 4u /* confchange.go:299-306 violated   */
+#define QE_PACK_ZERO_ID 8u                 /* ID 0 is raft.None                   */
+
+/* Slot assignment: voters of both halves ascending, then learners ascending.
+ * Writes the three masks (mask-typed, may be NULL), slot_ids[G][S] (0 =
+ * unused slot) and optional per-group flags; *num_flagged counts flagged
+ * groups.  Multi-threaded (qe_pack_threads). */
+int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_mask,
+                      void *out_mask, void *learner_mask, uint64_t *slot_ids,
+                      uint32_t *group_flags, uint64_t *num_flagged);
+
+/* Progress.Match of each peer (CSR prog_ids/prog_match) into match[S][stride]
+ * (host); peers without a slot are counted in *num_unknown. */
+int qe_pack_match(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
+                  const uint64_t *prog_off, const uint64_t *prog_ids,
+                  const uint64_t *prog_match, uint64_t *match, uint64_t stride,
+                  uint64_t *num_unknown);
+
+/* ProgressTracker.Votes (CSR vote_ids / vote_vals 0|1) into voted/granted
+ * bitmaps; the first vote per peer sticks (tracker.go:258-263). */
+int qe_pack_votes(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
+                  const uint64_t *vote_off, const uint64_t *vote_ids, const uint8_t *vote_vals,
+                  void *voted, void *granted);
+
+/* (group, id) -> slot (-1 if the id has no slot) for routing deltas. */
+int qe_slot_lookup(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
+                   uint64_t n, const uint64_t *group, const uint64_t *id, int8_t *slot);
+
+/* Host packing threads (0 = min(16, hardware threads)). */
+int qe_pack_threads(int n);
+
 /* ---- statistics -------------------------------------------------------- */
 
 /* out[QE_STATS_COUNTERS] (device) = sum over shards of stats (device). */

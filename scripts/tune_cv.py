@@ -18,7 +18,7 @@ G = int(os.environ.get("TUNE_G", 1 << 26))
 S = int(os.environ.get("TUNE_S", 5))
 ROUNDS, LAUNCHES = 5, 20
 VARIANTS = []
-for tpw in (-1, 0, 1, 2, 4, 8):
+for tpw in [int(x) for x in os.environ.get("TUNE_TPW", "-1,0,1,2,4,8").split(",")]:
     VARIANTS.append({"tiles_per_wave": tpw, "blocks_per_cu": 0, "nontemporal": 3, "stats": 1})
 if os.environ.get("TUNE_ONLY_DEFAULT"):
     VARIANTS = VARIANTS[:1]

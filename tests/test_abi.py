@@ -54,6 +54,7 @@ int main(void) {
   Z(qe_election_state) F(qe_election_state, term) F(qe_election_state, learner_mask)
   Z(qe_election_params) F(qe_election_params, steps) F(qe_election_params, p_grant_q16)
   Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
+  Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
   return 0;
 }
 """
@@ -61,7 +62,8 @@ int main(void) {
 CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
           "qe_repl_state": _lib.QeReplState, "qe_repl_msgs": _lib.QeReplMsgs,
           "qe_election_state": _lib.QeElectionState,
-          "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams}
+          "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams,
+          "qe_confstate_csr": _lib.QeConfStateCSR}
 
 
 def test_struct_layout_matches_header(tmp_path):

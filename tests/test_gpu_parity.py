@@ -447,3 +447,75 @@ def test_tuning_knobs_do_not_change_results(eng, orc):
         eng.tune("blocks_per_cu", 0)
         eng.tune("nontemporal", 3)
         eng.tune("tiles_per_wave", -1)
+
+
+# --------------------------------------------------------------------------
+# Sparse MsgAppResp deltas + wire-format packing end to end
+# --------------------------------------------------------------------------
+def test_apply_append_resps_matches_sequential_maybe_update(eng):
+    """qe_apply_append_resps (atomic max) == Progress.MaybeUpdate applied
+    one ack at a time in arrival order (progress.go:144-153), incl.
+    duplicates, stale acks, skipped (-1) slots and out-of-range groups."""
+    import ctypes as C
+    rng = np.random.default_rng(11)
+    G, S, n = 10007, 7, 200000
+    b = eng.SlotBatch(G, S, DEV, masks=(), votes=False)
+    eng.gen_groups(b, 5, dist=2)
+    match0 = b.match.cpu().numpy().view(np.uint64).reshape(S, b.stride).copy()
+    nxt = b.match.clone() + 1
+    next0 = nxt.cpu().numpy().view(np.uint64).reshape(S, b.stride).copy()
+    group = rng.integers(0, G + 3, n).astype(np.uint64)
+    slot = rng.integers(-1, S, n).astype(np.int8)
+    index = rng.integers(0, 8, n).astype(np.uint64)
+    touched = torch.zeros(G, dtype=torch.uint8, device=DEV)
+    dg = torch.from_numpy(group.view(np.int64)).to(DEV)
+    ds = torch.from_numpy(slot).to(DEV)
+    di = torch.from_numpy(index.view(np.int64)).to(DEV)
+    eng.check("qe_apply_append_resps", eng._lib.lib().qe_apply_append_resps(
+        G, S, b.stride, eng._ptr(b.match), eng._ptr(nxt), n, eng._ptr(dg), eng._ptr(ds),
+        eng._ptr(di), eng._ptr(touched), eng._stream(b.device)))
+    m, nx = match0.copy(), next0.copy()
+    want_touched = np.zeros(G, np.uint8)
+    for g, s, x in zip(group.tolist(), slot.tolist(), index.tolist()):
+        if g >= G or s < 0:
+            continue
+        _, m[s, g], nx[s, g] = Q.maybe_update(int(m[s, g]), int(nx[s, g]), x)
+        want_touched[g] = 1
+    np.testing.assert_array_equal(b.match.cpu().numpy().view(np.uint64).reshape(S, -1), m)
+    np.testing.assert_array_equal(nxt.cpu().numpy().view(np.uint64).reshape(S, -1), nx)
+    np.testing.assert_array_equal(touched.cpu().numpy(), want_touched)
+
+
+def test_wire_format_to_gpu_decisions(eng):
+    """ConfState CSR -> native packer -> device -> qe_commit_vote equals the
+    map-based restatement on the same ConfStates / Progress / Votes."""
+    import random
+    from etcd_amd.packing import ConfStates, pack_confstates, pack_progress, pack_votes
+    rng = random.Random(99)
+    confs, progress, votes = [], [], []
+    for _ in range(5000):
+        pool = rng.sample(range(1, 1 << 30), 10)
+        c0 = pool[:rng.randint(0, 5)]
+        c1 = (rng.sample(c0, rng.randint(0, len(c0))) + pool[5:5 + rng.randint(0, 3)]
+              if rng.random() < 0.5 else [])
+        lrn = pool[8:8 + rng.randint(0, 2)]
+        confs.append((c0, c1, lrn))
+        peers = list(dict.fromkeys(c0 + c1 + lrn))
+        progress.append({i: rng.randrange(100) for i in peers if rng.random() < 0.9})
+        votes.append([(i, rng.random() < 0.5) for i in peers if rng.random() < 0.8])
+    cs = ConfStates([c[0] for c in confs], [c[1] for c in confs], [c[2] for c in confs])
+    p = pack_confstates(cs, 12)
+    pack_progress(p, progress)
+    pack_votes(p, votes)
+    b = eng.SlotBatch(p.G, p.S, DEV)
+    b.load_host(p.match, inc=p.inc, out=p.out, learner=p.learner, voted=p.voted,
+                granted=p.granted)
+    out = eng.commit_vote(b)
+    commit = out.commit.cpu().numpy().view(np.uint64)
+    vote, gc, rc = (x.cpu().numpy() for x in (out.vote, out.granted, out.rejected))
+    for g, (c0, c1, lrn) in enumerate(confs):
+        vmap = {}
+        for i, v in votes[g]:
+            Q.record_vote(vmap, i, v)
+        assert int(commit[g]) == Q.joint_committed(c0, c1, progress[g])
+        assert (int(gc[g]), int(rc[g]), int(vote[g])) == Q.tally_votes(c0, c1, set(lrn), vmap)

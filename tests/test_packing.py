@@ -1,0 +1,108 @@
+"""Host-side packing (the wire-format side of the boundary): the native C++
+ConfState packer agrees with the Python packer, enforces the confchange
+invariants as flags, and -- chained with the C oracle -- reproduces the
+reference decisions computed on ID-keyed maps (oracle/quorum_ref.py)."""
+import random
+
+import numpy as np
+import pytest
+
+from etcd_amd import _lib
+from etcd_amd.packing import (ConfStates, pack, pack_confstates, pack_progress, pack_votes,
+                              slot_lookup)
+from oracle import quorum_ref as Q
+
+
+def random_confstate(rng, max_voters=5, joint_p=0.5, learner_p=0.5):
+    pool = rng.sample(range(1, 1 << 40), 12)
+    nv = rng.randint(0, max_voters)
+    voters = pool[:nv]
+    outgoing = []
+    if rng.random() < joint_p:
+        k = rng.randint(1, max_voters)
+        keep = rng.sample(voters, rng.randint(0, min(nv, k)))
+        outgoing = keep + pool[nv:nv + k - len(keep)]
+    used = set(voters) | set(outgoing)
+    rest = [x for x in pool if x not in used]
+    learners = rest[: rng.randint(0, 3)] if rng.random() < learner_p else []
+    lnext = [x for x in outgoing if x not in voters][:1]
+    return voters, outgoing, learners, lnext
+
+
+def test_native_packer_matches_python_and_oracle(orc):
+    rng = random.Random(7)
+    G, S = 3000, 16
+    confs = [random_confstate(rng) for _ in range(G)]
+    cs = ConfStates([c[0] for c in confs], [c[1] for c in confs], [c[2] for c in confs],
+                    [c[3] for c in confs])
+    p = pack_confstates(cs, S)
+    assert p.num_flagged == 0
+    pyp = pack([{"c0": c[0], "c1": c[1], "learners": c[2]} for c in confs], num_slots=S)
+    np.testing.assert_array_equal(p.slot_ids, pyp.slot_ids)
+    np.testing.assert_array_equal(p.inc, pyp.inc)
+    np.testing.assert_array_equal(p.out, pyp.out)
+    np.testing.assert_array_equal(p.learner, pyp.learner)
+    # Progress.Match for every peer (some absent), votes in arrival order
+    progress, votes = [], []
+    for c in confs:
+        peers = list(dict.fromkeys(c[0] + c[1] + c[2]))
+        progress.append({i: rng.choice([0, 5, 7, 9, rng.randrange(1 << 62)]) for i in peers
+                         if rng.random() < 0.9})
+        votes.append([(i, rng.random() < 0.6) for i in peers if rng.random() < 0.7])
+        if votes[-1]:
+            votes[-1].append((votes[-1][0][0], not votes[-1][0][1]))  # later vote ignored
+    assert pack_progress(p, progress) == 0
+    pack_votes(p, votes)
+    b = orc.Batch(G, S)
+    b.match[:] = np.ascontiguousarray(p.match).reshape(-1)
+    b.inc[:], b.out[:], b.learner[:] = p.inc, p.out, p.learner
+    b.voted[:], b.granted[:] = p.voted, p.granted
+    commit, vote, gc, rc, _ = orc.commit_vote(b)
+    for g, c in enumerate(confs):
+        vmap = {}
+        for i, v in votes[g]:
+            Q.record_vote(vmap, i, v)
+        assert int(commit[g]) == Q.joint_committed(c[0], c[1], progress[g])
+        want_g, want_r, want_v = Q.tally_votes(c[0], c[1], set(c[2]), vmap)
+        assert (int(gc[g]), int(rc[g]), int(vote[g])) == (want_g, want_r, want_v)
+
+
+def test_packer_flags_invariant_violations():
+    cs = ConfStates(
+        voters=[[1, 2, 3], [1, 2], list(range(1, 20)), [0, 1]],
+        voters_outgoing=[[], [2, 3], [], []],
+        learners=[[3], [], [], []],
+        learners_next=[[], [9], [], []])
+    p = pack_confstates(cs, 16)
+    assert p.flags[0] & _lib.QE_PACK_LEARNER_IS_VOTER
+    assert p.flags[1] & _lib.QE_PACK_LEARNER_NEXT_NOT_OUTGOING
+    assert p.flags[2] & _lib.QE_PACK_TOO_MANY_PEERS
+    assert p.flags[3] & _lib.QE_PACK_ZERO_ID
+    assert p.num_flagged == 4
+    assert int(p.inc[2]) == 0 and not p.slot_ids[2].any()  # oversize group left empty
+
+
+def test_slot_lookup_routes_deltas():
+    cs = ConfStates(voters=[[10, 20, 30], [5]], voters_outgoing=[[30, 40], []],
+                    learners=[[50], []])
+    p = pack_confstates(cs, 8)
+    assert p.slot_ids[0].tolist()[:5] == [10, 20, 30, 40, 50]
+    got = slot_lookup(p, [0, 0, 0, 1, 1, 7], [40, 50, 99, 5, 0, 5])
+    assert got.tolist() == [3, 4, -1, 0, -1, -1]
+
+
+def test_pack_threads_knob_keeps_results():
+    rng = random.Random(3)
+    confs = [random_confstate(rng) for _ in range(20000)]
+    cs = ConfStates([c[0] for c in confs], [c[1] for c in confs], [c[2] for c in confs])
+    L = _lib.lib()
+    try:
+        L.qe_pack_threads(1)
+        a = pack_confstates(cs, 16)
+        L.qe_pack_threads(8)
+        b = pack_confstates(cs, 16)
+    finally:
+        L.qe_pack_threads(0)
+    np.testing.assert_array_equal(a.slot_ids, b.slot_ids)
+    np.testing.assert_array_equal(a.inc, b.inc)
+    assert L.qe_pack_threads(-1) == _lib.QE_ERANGE
