@@ -93,6 +93,13 @@ static int dispatch_elec(uint32_t S, const EArgs &a, hipStream_t st) {
 #undef QE_C
 }
 
+static int dispatch_progress(uint32_t S, const PArgs &a, int kind, bool masked, bool joint,
+                             hipStream_t st) {
+#define QE_C(n) dispatch_progress_##n(a, kind, masked, joint, st)
+  QE_SWITCH(S, QE_C)
+#undef QE_C
+}
+
 }  // namespace qe
 
 // ===========================================================================
@@ -327,6 +334,83 @@ int qe_apply_append_resps(uint64_t num_groups, uint32_t num_slots, uint64_t stri
                      static_cast<hipStream_t>(stream), num_groups, num_slots, stride, match,
                      next, n, group, slot, index, touched);
   return hip_status(hipGetLastError());
+}
+
+static int progress_args(const qe_progress *p, PArgs &a) {
+  if (!p) return QE_EINVAL;
+  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved) return QE_EINVAL;
+  if (p->inflight_cap == 0 || p->inflight_cap > QE_MAX_INFLIGHT) return QE_ERANGE;
+  if (p->log_runs > QE_MAX_LOG_RUNS) return QE_ERANGE;
+  if (p->num_groups && p->stride < p->num_groups) return QE_EINVAL;
+  if (p->out_mask && !p->inc_mask) return QE_EINVAL;
+  if (p->num_groups &&
+      (!p->match || !p->next || !p->pending_snapshot || !p->flags || !p->infl_start ||
+       !p->infl_count || !p->infl_buf || !p->committed || !p->term_start || !p->first_index ||
+       !p->last_index))
+    return QE_EINVAL;
+  if (p->num_groups && p->log_runs && (!p->run_first || !p->run_term || !p->run_count))
+    return QE_EINVAL;
+  a = PArgs{};
+  a.G = p->num_groups;
+  a.goff = p->group_offset;
+  a.stride = p->stride;
+  a.F = p->inflight_cap;
+  a.R = p->log_runs;
+  a.match = p->match;
+  a.next = p->next;
+  a.pending = p->pending_snapshot;
+  a.flags = p->flags;
+  a.istart = p->infl_start;
+  a.icount = p->infl_count;
+  a.ibuf = p->infl_buf;
+  a.committed = p->committed;
+  a.term_start = p->term_start;
+  a.first_index = p->first_index;
+  a.last_index = p->last_index;
+  a.run_first = p->run_first;
+  a.run_term = p->run_term;
+  a.run_count = p->run_count;
+  a.inc = p->inc_mask;
+  a.out = p->out_mask;
+  return QE_OK;
+}
+
+static const uint8_t kZeroRuns[1] = {0};
+
+int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
+                     void *stream) {
+  PArgs a;
+  int rc = progress_args(p, a);
+  if (rc) return rc;
+  if (!m) return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (!m->type || !m->index || !m->reject_hint || !m->log_term) return QE_EINVAL;
+  if (p->log_runs == 0) return QE_EINVAL;  // findConflictByTerm needs the log model
+  a.mtype = m->type;
+  a.mindex = m->index;
+  a.mhint = m->reject_hint;
+  a.mlogterm = m->log_term;
+  a.send_mask = m->send_mask;
+  a.bcast = m->bcast;
+  a.stats = stats;
+  (void)kZeroRuns;
+  return dispatch_progress(p->num_slots, a, 0, p->inc_mask != nullptr, p->out_mask != nullptr,
+                           static_cast<hipStream_t>(stream));
+}
+
+int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
+                     uint32_t max_ents, void *sent, void *snap, void *stream) {
+  PArgs a;
+  int rc = progress_args(p, a);
+  if (rc) return rc;
+  if (p->num_groups == 0) return QE_OK;
+  if (!want) return QE_EINVAL;
+  a.want = want;
+  a.send_if_empty = send_if_empty;
+  a.max_ents = max_ents;
+  a.sent = sent;
+  a.snap = snap;
+  return dispatch_progress(p->num_slots, a, 1, false, false, static_cast<hipStream_t>(stream));
 }
 
 int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream) {

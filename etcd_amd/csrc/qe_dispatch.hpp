@@ -11,7 +11,9 @@ int hip_status(hipError_t e);
   int dispatch_cv_##n(const CVArgs &a, int mode, bool vec, hipStream_t st);           \
   int dispatch_repl_##n(const RArgs &a, bool masked, bool joint, bool vec,            \
                         hipStream_t st);                                               \
-  int dispatch_elec_##n(const EArgs &a, hipStream_t st);
+  int dispatch_elec_##n(const EArgs &a, hipStream_t st);                            \
+  int dispatch_progress_##n(const PArgs &a, int kind, bool masked, bool joint,        \
+                            hipStream_t st);
 QE_DECL_S(1) QE_DECL_S(2) QE_DECL_S(3) QE_DECL_S(4) QE_DECL_S(5) QE_DECL_S(6) QE_DECL_S(7)
 QE_DECL_S(8) QE_DECL_S(9) QE_DECL_S(10) QE_DECL_S(11) QE_DECL_S(12) QE_DECL_S(13)
 QE_DECL_S(14) QE_DECL_S(15) QE_DECL_S(16)

@@ -85,4 +85,22 @@ int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
+int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
+                                     hipStream_t st) {
+  if (kind == 1) {
+    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
+                       dim3(kBlock), 0, st, a);
+  } else if (joint) {
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
+                       dim3(kBlock), 0, st, a);
+  } else if (masked) {
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false>),
+                       dim3(grid_for((a.G + 63) / 64, 0, 1)), dim3(kBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false>),
+                       dim3(grid_for((a.G + 63) / 64, 0, 1)), dim3(kBlock), 0, st, a);
+  }
+  return hip_status(hipGetLastError());
+}
+
 }  // namespace qe

@@ -590,6 +590,286 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Progress state machine (qe_progress_step / qe_progress_send).  One group
+// per thread; per-peer state lives in slot-SoA rows, the Inflights ring in
+// [S][F][stride] rows (F = MaxInflightMsgs).
+// ---------------------------------------------------------------------------
+struct PArgs {
+  uint64_t G, goff, stride;
+  uint32_t F, R;
+  uint64_t *match, *next, *pending;
+  uint8_t *flags, *istart, *icount;
+  uint64_t *ibuf;
+  uint64_t *committed;
+  const uint64_t *term_start, *first_index, *last_index;
+  const uint64_t *run_first, *run_term;
+  const uint8_t *run_count;
+  const void *inc, *out;
+  // step messages
+  const uint8_t *mtype;
+  const uint64_t *mindex, *mhint, *mlogterm;
+  void *send_mask;
+  uint8_t *bcast;
+  uint64_t *stats;
+  // send
+  const void *want;
+  uint32_t send_if_empty, max_ents;
+  void *sent, *snap;
+};
+
+struct PR {
+  uint64_t match, next, pending;
+  uint32_t state, probe_sent, recent_active, start, count;
+};
+
+__device__ __forceinline__ PR pr_load(const PArgs &a, uint64_t off) {
+  PR p;
+  p.match = a.match[off];
+  p.next = a.next[off];
+  p.pending = a.pending[off];
+  const uint32_t f = a.flags[off];
+  p.state = f & QE_PF_STATE;
+  p.probe_sent = (f & QE_PF_PROBE_SENT) != 0;
+  p.recent_active = (f & QE_PF_RECENT_ACTIVE) != 0;
+  p.start = a.istart[off];
+  p.count = a.icount[off];
+  return p;
+}
+
+__device__ __forceinline__ void pr_store(const PArgs &a, uint64_t off, const PR &p) {
+  a.match[off] = p.match;
+  a.next[off] = p.next;
+  a.pending[off] = p.pending;
+  a.flags[off] = static_cast<uint8_t>(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
+                                      (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u));
+  a.istart[off] = static_cast<uint8_t>(p.start);
+  a.icount[off] = static_cast<uint8_t>(p.count);
+}
+
+// Inflights slot k of peer (s, g): ibuf[(s*F + k)*stride + g]
+__device__ __forceinline__ uint64_t *infl(const PArgs &a, uint32_t s, uint64_t g, uint32_t k) {
+  return a.ibuf + (static_cast<uint64_t>(s) * a.F + k) * a.stride + g;
+}
+
+// inflights.go:87-113 FreeLE
+__device__ __forceinline__ void infl_free_le(const PArgs &a, uint32_t s, uint64_t g, PR &p,
+                                             uint64_t to) {
+  if (p.count == 0 || to < *infl(a, s, g, p.start)) return;
+  uint32_t idx = p.start, i;
+  for (i = 0; i < p.count; i++) {
+    if (to < *infl(a, s, g, idx)) break;
+    if (++idx >= a.F) idx -= a.F;
+  }
+  p.count -= i;
+  p.start = p.count == 0 ? 0 : idx;
+}
+
+__device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:84-90
+  p.probe_sent = 0;
+  p.pending = 0;
+  p.state = st;
+  p.count = 0;
+  p.start = 0;
+}
+__device__ __forceinline__ void pr_become_probe(PR &p) {  // progress.go:112-125
+  if (p.state == QE_PR_SNAPSHOT) {
+    const uint64_t ps = p.pending;
+    pr_reset(p, QE_PR_PROBE);
+    const uint64_t x = p.match + 1, y = ps + 1;
+    p.next = x > y ? x : y;
+  } else {
+    pr_reset(p, QE_PR_PROBE);
+    p.next = p.match + 1;
+  }
+}
+__device__ __forceinline__ void pr_become_replicate(PR &p) {  // progress.go:127-131
+  pr_reset(p, QE_PR_REPLICATE);
+  p.next = p.match + 1;
+}
+__device__ __forceinline__ bool pr_paused(const PR &p, uint32_t F) {  // progress.go:201-212
+  if (p.state == QE_PR_PROBE) return p.probe_sent;
+  if (p.state == QE_PR_REPLICATE) return p.count == F;
+  return true;
+}
+
+// raftLog.findConflictByTerm (raft/log.go:147-168) on the term-run model:
+// walking down index by index until term(index) <= t is the same as jumping
+// run by run to the end of the highest run whose term is <= t.
+__device__ __forceinline__ uint64_t find_conflict_by_term(const PArgs &a, uint64_t g, uint32_t nr,
+                                                          uint64_t li, uint64_t index,
+                                                          uint64_t t) {
+  if (index > li || nr == 0) return index;
+  if (index < a.run_first[g]) return index;  // term(index) = 0 <= t
+  int r = static_cast<int>(nr) - 1;
+  while (r > 0 && a.run_first[static_cast<uint64_t>(r) * a.stride + g] > index) r--;
+  // index lies in run r
+  while (r >= 0) {
+    if (a.run_term[static_cast<uint64_t>(r) * a.stride + g] <= t) return index;
+    index = a.run_first[static_cast<uint64_t>(r) * a.stride + g] - 1;  // end of run r-1
+    r--;
+  }
+  return index;  // below the dummy index: term 0 <= t
+}
+
+template <int S, bool MASKED, bool JOINT>
+__device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t inc, uint32_t out) {
+  uint64_t v[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) v[s] = vals[s];
+  if constexpr (!MASKED && !JOINT) return select_fixed<S>(v);
+  else return joint_committed<S>(v, inc, out);
+}
+
+enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
+
+template <int S, typename MT, bool MASKED, bool JOINT>
+__global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
+  const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t mi = MASKED ? (incp[g] & kFull) : kFull;
+    const uint32_t mo = JOINT ? (outp[g] & kFull) : 0u;
+    const uint64_t li = a.last_index[g], ts = a.term_start[g], c0 = a.committed[g];
+    const uint32_t nr = a.run_count[g] < a.R ? a.run_count[g] : a.R;
+    uint64_t c = c0;
+    uint64_t vals[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) vals[s] = a.match[static_cast<uint64_t>(s) * a.stride + g];
+    uint32_t send = 0, bc = 0;
+    // Runtime loop over slots (one copy of the selection network); the
+    // register-resident match row is updated with a static select-assign.
+#pragma unroll 1
+    for (int s = 0; s < S; s++) {
+      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+      const uint32_t ty = a.mtype[off];
+      if (ty == QE_MSG_NONE || ty > QE_MSG_HEARTBEAT_RESP) continue;
+      PR p = pr_load(a, off);
+      p.recent_active = 1;
+      if (ty == QE_MSG_APP_RESP_REJECT) {
+        const uint64_t idx = a.mindex[off], lt = a.mlogterm[off];
+        uint64_t probe = a.mhint[off];
+        if (lt > 0) probe = find_conflict_by_term(a, g, nr, li, probe, lt);
+        bool decr;  // MaybeDecrTo(m.Index, probe)
+        if (p.state == QE_PR_REPLICATE) {
+          decr = idx > p.match;
+          if (decr) p.next = p.match + 1;
+        } else {
+          decr = (p.next - 1 == idx);
+          if (decr) {
+            const uint64_t m = idx < probe + 1 ? idx : probe + 1;
+            p.next = m > 1 ? m : 1;
+            p.probe_sent = 0;
+          }
+        }
+        if (decr) {
+          if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
+          send |= 1u << s;
+        }
+      } else if (ty == QE_MSG_APP_RESP) {
+        const uint64_t idx = a.mindex[off];
+        if (idx > li) {
+          cnt[P_VIOL] += 1;
+        } else {
+          const bool old_paused = pr_paused(p, a.F);
+          bool updated = false;  // MaybeUpdate
+          if (p.match < idx) {
+            p.match = idx;
+            updated = true;
+            p.probe_sent = 0;
+          }
+          if (p.next < idx + 1) p.next = idx + 1;
+          if (updated) {
+            if (p.state == QE_PR_PROBE) {
+              pr_become_replicate(p);
+            } else if (p.state == QE_PR_SNAPSHOT && p.match >= p.pending) {
+              pr_become_probe(p);
+              pr_become_replicate(p);
+            } else if (p.state == QE_PR_REPLICATE) {
+              infl_free_le(a, s, g, p, idx);
+            }
+#pragma unroll
+            for (int k = 0; k < S; k++) vals[k] = (k == s) ? p.match : vals[k];
+            const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
+            if (mci > c && mci >= ts && mci <= li) {
+              c = mci;
+              bc = 1;
+            } else if (old_paused) {
+              send |= 1u << s;
+            }
+          }
+        }
+      } else {  // QE_MSG_HEARTBEAT_RESP
+        p.probe_sent = 0;
+        if (p.state == QE_PR_REPLICATE && p.count == a.F)
+          infl_free_le(a, s, g, p, *infl(a, s, g, p.start));
+        if (p.match < li) send |= 1u << s;
+      }
+      pr_store(a, off, p);
+    }
+    a.committed[g] = c;
+    if (a.send_mask) static_cast<MT *>(a.send_mask)[g] = static_cast<MT>(send);
+    if (a.bcast) a.bcast[g] = static_cast<uint8_t>(bc);
+    cnt[P_GROUPS] += 1;
+    cnt[P_SUM] += c;
+    cnt[P_ADV] += (c != c0);
+    const uint64_t tag = (static_cast<uint64_t>(send) << 40) | (static_cast<uint64_t>(bc) << 62);
+    cnt[P_CSUM] += mix64(((a.goff + g) * kPhi) ^ c ^ tag);
+  }
+  if (a.stats) {
+    const int idx[P_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
+                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
+    block_stats_add<P_N, kBlock>(cnt, idx, a.stats);
+  }
+}
+
+template <int S, typename MT>
+__global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const MT *wantp = static_cast<const MT *>(a.want);
+  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
+       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t w = wantp[g] & kFull;
+    const uint64_t fi = a.first_index[g], li = a.last_index[g];
+    uint32_t sm = 0, sn = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      if (!((w >> s) & 1u)) continue;
+      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+      PR p = pr_load(a, off);
+      if (pr_paused(p, a.F)) continue;
+      if (p.next > li) {  // no entries to send
+        if (!a.send_if_empty) continue;
+        sm |= 1u << s;
+      } else if (p.next < fi) {  // entries compacted: send a snapshot
+        if (!p.recent_active) continue;
+        pr_reset(p, QE_PR_SNAPSHOT);  // BecomeSnapshot(firstIndex - 1)
+        p.pending = fi - 1;
+        sm |= 1u << s;
+        sn |= 1u << s;
+      } else {
+        uint64_t last = p.next + (a.max_ents ? a.max_ents : 1u) - 1;
+        if (last > li || last < p.next) last = li;
+        if (p.state == QE_PR_REPLICATE) {
+          p.next = last + 1;  // OptimisticUpdate
+          uint32_t nx = p.start + p.count;  // Inflights.Add
+          if (nx >= a.F) nx -= a.F;
+          *infl(a, s, g, nx) = last;
+          p.count++;
+        } else if (p.state == QE_PR_PROBE) {
+          p.probe_sent = 1;
+        }
+        sm |= 1u << s;
+      }
+      pr_store(a, off, p);
+    }
+    if (a.sent) static_cast<MT *>(a.sent)[g] = static_cast<MT>(sm);
+    if (a.snap) static_cast<MT *>(a.snap)[g] = static_cast<MT>(sn);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Small bitmap kernels: QuorumActive, RecordVote.
 // ---------------------------------------------------------------------------
 template <typename MT>

@@ -248,6 +248,87 @@ int qe_election_steps(const qe_election_state *st,
                       const qe_election_params *p, uint64_t *stats,
                       void *stream);
 
+/* ---- Progress state machine ------------------ */
+
+/* tracker.StateType (raft/tracker/state.go) and per-peer flag bits */
+#define QE_PR_PROBE 0
+#define QE_PR_REPLICATE 1
+#define QE_PR_SNAPSHOT 2
+#define QE_PF_STATE 3u          /* flags & QE_PF_STATE = StateType           */
+#define QE_PF_PROBE_SENT 4u     /* Progress.ProbeSent                        */
+#define QE_PF_RECENT_ACTIVE 8u  /* Progress.RecentActive                     */
+#define QE_MAX_INFLIGHT 255     /* Inflights capacity (MaxInflightMsgs)      */
+#define QE_MAX_LOG_RUNS 16      /* term runs of the leader-log model          */
+
+/* message kinds of qe_peer_msgs.type */
+#define QE_MSG_NONE 0
+#define QE_MSG_APP_RESP 1         /* MsgAppResp, Reject=false                */
+#define QE_MSG_APP_RESP_REJECT 2  /* MsgAppResp, Reject=true                 */
+#define QE_MSG_HEARTBEAT_RESP 3   /* MsgHeartbeatResp                        */
+
+/* Leader-side Progress of every peer of G groups (raft/tracker/progress.go:
+ * 30-80) plus the leader's log model: term runs r < run_count[g] covering
+ * [run_first[r], run_first[r+1]) with run_term[r] (run 0 starts at the
+ * snapshot/dummy index = first_index - 1), ending at last_index; the current
+ * term's entries are [term_start, last_index]. */
+typedef struct qe_progress {
+  uint64_t num_groups;
+  uint64_t group_offset;
+  uint32_t num_slots;
+  uint32_t inflight_cap;        /* F = MaxInflightMsgs, 1..QE_MAX_INFLIGHT  */
+  uint64_t stride;
+  uint64_t *match, *next;       /* [S][stride]                               */
+  uint64_t *pending_snapshot;   /* [S][stride]                               */
+  uint8_t *flags;               /* [S][stride] QE_PF_* bits                  */
+  uint8_t *infl_start;          /* [S][stride] Inflights.start               */
+  uint8_t *infl_count;          /* [S][stride] Inflights.count               */
+  uint64_t *infl_buf;           /* [S][F][stride] Inflights.buffer           */
+  uint64_t *committed;          /* [G] raftLog.committed (rw)                */
+  const uint64_t *term_start;   /* [G]                                       */
+  const uint64_t *first_index;  /* [G] raftLog.firstIndex()                  */
+  const uint64_t *last_index;   /* [G] raftLog.lastIndex()                   */
+  uint32_t log_runs;            /* R <= QE_MAX_LOG_RUNS                      */
+  uint32_t reserved;
+  const uint64_t *run_first;    /* [R][stride]                               */
+  const uint64_t *run_term;     /* [R][stride]                               */
+  const uint8_t *run_count;     /* [G] valid runs, 1..R                       */
+  const void *inc_mask;         /* [G] as in qe_groups (NULL = all slots)    */
+  const void *out_mask;         /* [G] or NULL                               */
+} qe_progress;
+
+/* One round of peer responses: message of slot s for group g at
+ * [s*stride + g]. */
+typedef struct qe_peer_msgs {
+  const uint8_t *type;          /* QE_MSG_*                                  */
+  const uint64_t *index;        /* m.Index                                   */
+  const uint64_t *reject_hint;  /* m.RejectHint                              */
+  const uint64_t *log_term;     /* m.LogTerm                                 */
+  void *send_mask;              /* [G] out: slots sendAppend(m.From) ran for */
+  uint8_t *bcast;               /* [G] out: maybeCommit advanced -> bcastAppend */
+} qe_peer_msgs;
+
+/* Leader-side handling of one message per peer, slots in ascending order
+ * (raft/raft.go:1106-1296): RecentActive; reject -> findConflictByTerm
+ * (raft/log.go:147-168) + MaybeDecrTo (progress.go:170-193), Replicate ->
+ * BecomeProbe, sendAppend; accept -> IsPaused, MaybeUpdate, Probe ->
+ * BecomeReplicate / Snapshot caught up -> BecomeProbe+BecomeReplicate /
+ * Replicate -> Inflights.FreeLE, maybeCommit (bcast) else sendAppend if it
+ * was paused; heartbeat response -> ProbeSent=false, FreeFirstOne when the
+ * inflights are full, sendAppend if Match < lastIndex.  An accept with
+ * index > lastIndex is invalid input: ignored and counted as an invariant
+ * violation. */
+int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
+                     void *stream);
+
+/* raft.maybeSendAppend (raft/raft.go:432-492) for the slots of want[g]:
+ * skip paused peers; Next > lastIndex sends an empty MsgApp only when
+ * send_if_empty; Next < firstIndex sends a snapshot to recently active peers
+ * (BecomeSnapshot(firstIndex-1)); otherwise up to max_ents entries:
+ * Replicate -> OptimisticUpdate + Inflights.Add, Probe -> ProbeSent.
+ * sent / snap (mask-typed [G], may be NULL) report the outcome. */
+int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
+                     uint32_t max_ents, void *sent, void *snap, void *stream);
+
 /* ---- sparse MsgAppResp deltas ------------------------------------------ */
 
 /* Apply n MsgAppResp acks in COO form -- ack i: group[i], slot[i] (-1 =

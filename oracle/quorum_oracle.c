@@ -751,3 +751,358 @@ int orc_max_threads(void) {
   return 1;
 #endif
 }
+
+/* ------------------------------------------------------------------------ */
+/* Progress state machine: MsgAppResp accept /   */
+/* reject, MsgHeartbeatResp, inflights, and the send side.                  */
+/* ------------------------------------------------------------------------ */
+enum { PR_PROBE = 0, PR_REPLICATE = 1, PR_SNAPSHOT = 2 };
+#define PF_STATE 3u
+#define PF_PROBE_SENT 4u
+#define PF_RECENT_ACTIVE 8u
+
+typedef struct orc_pr {
+  uint64_t match, next, pending;
+  uint32_t state, probe_sent, recent_active;
+  uint32_t start, count, size; /* Inflights (raft/tracker/inflights.go:22-36) */
+  uint64_t *buf;               /* strided view: buf[k * bstride] */
+  uint64_t bstride;
+} orc_pr;
+
+static inline uint64_t *ib(orc_pr *p, uint32_t k) { return &p->buf[(uint64_t)k * p->bstride]; }
+
+/* inflights.go:55-71 Add */
+static void infl_add(orc_pr *p, uint64_t x) {
+  uint32_t nx = p->start + p->count;
+  if (nx >= p->size) nx -= p->size;
+  *ib(p, nx) = x;
+  p->count++;
+}
+/* inflights.go:87-113 FreeLE */
+static void infl_free_le(orc_pr *p, uint64_t to) {
+  if (p->count == 0 || to < *ib(p, p->start)) return;
+  uint32_t idx = p->start, i;
+  for (i = 0; i < p->count; i++) {
+    if (to < *ib(p, idx)) break;
+    if (++idx >= p->size) idx -= p->size;
+  }
+  p->count -= i;
+  p->start = idx;
+  if (p->count == 0) p->start = 0;
+}
+static int infl_full(const orc_pr *p) { return p->count == p->size; }
+
+/* progress.go:84-90 ResetState */
+static void pr_reset_state(orc_pr *p, uint32_t st) {
+  p->probe_sent = 0;
+  p->pending = 0;
+  p->state = st;
+  p->count = 0; /* Inflights.reset */
+  p->start = 0;
+}
+/* progress.go:112-125 BecomeProbe */
+static void pr_become_probe(orc_pr *p) {
+  if (p->state == PR_SNAPSHOT) {
+    uint64_t ps = p->pending;
+    pr_reset_state(p, PR_PROBE);
+    uint64_t a = p->match + 1, b = ps + 1;
+    p->next = a > b ? a : b;
+  } else {
+    pr_reset_state(p, PR_PROBE);
+    p->next = p->match + 1;
+  }
+}
+/* progress.go:127-131 BecomeReplicate */
+static void pr_become_replicate(orc_pr *p) {
+  pr_reset_state(p, PR_REPLICATE);
+  p->next = p->match + 1;
+}
+/* progress.go:135-139 BecomeSnapshot */
+static void pr_become_snapshot(orc_pr *p, uint64_t snap) {
+  pr_reset_state(p, PR_SNAPSHOT);
+  p->pending = snap;
+}
+/* progress.go:144-153 MaybeUpdate */
+static int pr_maybe_update(orc_pr *p, uint64_t n) {
+  int updated = 0;
+  if (p->match < n) {
+    p->match = n;
+    updated = 1;
+    p->probe_sent = 0; /* ProbeAcked */
+  }
+  if (p->next < n + 1) p->next = n + 1;
+  return updated;
+}
+/* progress.go:170-193 MaybeDecrTo */
+static int pr_maybe_decr_to(orc_pr *p, uint64_t rejected, uint64_t hint) {
+  if (p->state == PR_REPLICATE) {
+    if (rejected <= p->match) return 0;
+    p->next = p->match + 1;
+    return 1;
+  }
+  if (p->next - 1 != rejected) return 0;
+  uint64_t m = rejected < hint + 1 ? rejected : hint + 1;
+  p->next = m > 1 ? m : 1;
+  p->probe_sent = 0;
+  return 1;
+}
+/* progress.go:201-212 IsPaused */
+static int pr_is_paused(const orc_pr *p) {
+  if (p->state == PR_PROBE) return p->probe_sent;
+  if (p->state == PR_REPLICATE) return infl_full(p);
+  return 1;
+}
+
+/* raftLog.term (raft/log.go:265-285) on the term-run log model: runs r <
+ * nruns cover [first[r], first[r+1]) with term[r]; the last run ends at
+ * last_index; first[0] is the dummy (snapshot) index.  Out-of-range -> 0. */
+uint64_t orc_log_term(uint32_t nruns, const uint64_t *first, const uint64_t *term,
+                      uint64_t last_index, uint64_t i) {
+  if (nruns == 0 || i < first[0] || i > last_index) return 0;
+  uint64_t t = term[0];
+  for (uint32_t r = 0; r < nruns; r++)
+    if (i >= first[r]) t = term[r];
+  return t;
+}
+/* raftLog.findConflictByTerm (raft/log.go:147-168), linear as written. */
+uint64_t orc_find_conflict_by_term(uint32_t nruns, const uint64_t *first, const uint64_t *term,
+                                   uint64_t last_index, uint64_t index, uint64_t t) {
+  if (index > last_index) return index;
+  for (;;) {
+    uint64_t lt = orc_log_term(nruns, first, term, last_index, index);
+    if (lt <= t) break;
+    index--;
+  }
+  return index;
+}
+
+static void pr_load(orc_pr *p, uint64_t off, uint64_t stride, uint32_t F, uint64_t *match,
+                    uint64_t *next, uint64_t *pending, uint8_t *pflags, uint8_t *istart,
+                    uint8_t *icount, uint64_t *ibuf, uint32_t s, uint64_t g) {
+  p->match = match[off];
+  p->next = next[off];
+  p->pending = pending[off];
+  p->state = pflags[off] & PF_STATE;
+  p->probe_sent = (pflags[off] & PF_PROBE_SENT) != 0;
+  p->recent_active = (pflags[off] & PF_RECENT_ACTIVE) != 0;
+  p->start = istart[off];
+  p->count = icount[off];
+  p->size = F;
+  p->buf = ibuf + ((uint64_t)s * F) * stride + g;
+  p->bstride = stride;
+}
+static void pr_store(const orc_pr *p, uint64_t off, uint64_t *match, uint64_t *next,
+                     uint64_t *pending, uint8_t *pflags, uint8_t *istart, uint8_t *icount) {
+  match[off] = p->match;
+  next[off] = p->next;
+  pending[off] = p->pending;
+  pflags[off] = (uint8_t)(p->state | (p->probe_sent ? PF_PROBE_SENT : 0) |
+                          (p->recent_active ? PF_RECENT_ACTIVE : 0));
+  istart[off] = (uint8_t)p->start;
+  icount[off] = (uint8_t)p->count;
+}
+
+uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast) {
+  uint64_t tag = ((uint64_t)send << 40) | ((uint64_t)bcast << 62);
+  return orc_mix64((gid * PHI) ^ committed ^ tag);
+}
+
+/* One round of leader-side message handling per group (raft/raft.go:
+ * 1106-1296), messages taken in slot order.  type: 0 none, 1 MsgAppResp,
+ * 2 MsgAppResp reject, 3 MsgHeartbeatResp.  Accepts with index > lastIndex
+ * are invalid input: counted as invariant violations and ignored. */
+void orc_progress_step_batch(uint64_t G, uint64_t goff, uint32_t S, uint32_t F, uint64_t stride,
+                             uint64_t *match, uint64_t *next, uint64_t *pending, uint8_t *pflags,
+                             uint8_t *istart, uint8_t *icount, uint64_t *ibuf, uint64_t *committed,
+                             const uint64_t *term_start, const uint64_t *last_index, uint32_t R,
+                             const uint64_t *run_first, const uint64_t *run_term,
+                             const uint8_t *run_count, const void *inc, const void *out,
+                             const uint8_t *mtype, const uint64_t *mindex, const uint64_t *mhint,
+                             const uint64_t *mlogterm, void *send_mask, uint8_t *bcast,
+                             uint64_t *stats, int threads) {
+  uint32_t mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  uint64_t st[NSTAT];
+  memset(st, 0, sizeof(st));
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    uint64_t ls[NSTAT];
+    memset(ls, 0, sizeof(ls));
+#pragma omp for schedule(static)
+    for (int64_t gi = 0; gi < (int64_t)G; gi++) {
+      uint64_t g = (uint64_t)gi;
+      uint32_t mi = inc ? ld_mask(inc, mb, g) & full : full;
+      uint32_t mo = out ? ld_mask(out, mb, g) & full : 0;
+      uint64_t li = last_index[g], ts = term_start[g], c = committed[g];
+      uint32_t nr = run_count[g] < R ? run_count[g] : R;
+      uint64_t rf[16], rt[16];
+      for (uint32_t r = 0; r < nr; r++) {
+        rf[r] = run_first[r * stride + g];
+        rt[r] = run_term[r * stride + g];
+      }
+      uint64_t vals[16];
+      for (uint32_t s = 0; s < S; s++) vals[s] = match[s * stride + g];
+      uint32_t send = 0, bc = 0;
+      for (uint32_t s = 0; s < S; s++) {
+        uint64_t off = s * stride + g;
+        uint32_t ty = mtype[off];
+        if (ty == 0) continue;
+        orc_pr p;
+        pr_load(&p, off, stride, F, match, next, pending, pflags, istart, icount, ibuf, s, g);
+        p.recent_active = 1;
+        if (ty == 2) { /* MsgAppResp reject, raft.go:1109-1236 */
+          uint64_t probe = mhint[off];
+          if (mlogterm[off] > 0)
+            probe = orc_find_conflict_by_term(nr, rf, rt, li, mhint[off], mlogterm[off]);
+          if (pr_maybe_decr_to(&p, mindex[off], probe)) {
+            if (p.state == PR_REPLICATE) pr_become_probe(&p);
+            send |= 1u << s; /* sendAppend(m.From) */
+          }
+        } else if (ty == 1) { /* MsgAppResp accept, raft.go:1237-1282 */
+          if (mindex[off] > li) {
+            ls[ST_VIOLATIONS] += 1;
+          } else {
+            int old_paused = pr_is_paused(&p);
+            if (pr_maybe_update(&p, mindex[off])) {
+              if (p.state == PR_PROBE) {
+                pr_become_replicate(&p);
+              } else if (p.state == PR_SNAPSHOT && p.match >= p.pending) {
+                pr_become_probe(&p);
+                pr_become_replicate(&p);
+              } else if (p.state == PR_REPLICATE) {
+                infl_free_le(&p, mindex[off]);
+              }
+              vals[s] = p.match;
+              uint64_t mci = orc_joint_committed(S, mi, mo, vals);
+              if (orc_maybe_commit(mci, &c, ts, li)) {
+                bc = 1; /* releasePendingReadIndexMessages + bcastAppend */
+              } else if (old_paused) {
+                send |= 1u << s;
+              }
+            }
+          }
+        } else if (ty == 3) { /* MsgHeartbeatResp, raft.go:1284-1296 */
+          p.probe_sent = 0;
+          if (p.state == PR_REPLICATE && infl_full(&p)) infl_free_le(&p, *ib(&p, p.start));
+          if (p.match < li) send |= 1u << s;
+        }
+        pr_store(&p, off, match, next, pending, pflags, istart, icount);
+      }
+      uint64_t c0 = committed[g];
+      committed[g] = c;
+      if (send_mask) st_mask(send_mask, mb, g, send);
+      if (bcast) bcast[g] = (uint8_t)bc;
+      ls[ST_GROUPS] += 1;
+      ls[ST_COMMIT_SUM] += c;
+      ls[ST_COMMIT_ADVANCED] += (c != c0);
+      ls[ST_CHECKSUM] += orc_checksum_step(goff + g, c, send, bc);
+    }
+#pragma omp critical
+    for (int k = 0; k < NSTAT; k++) st[k] += ls[k];
+  }
+  if (stats)
+    for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+}
+
+/* raft.maybeSendAppend (raft/raft.go:432-492) for the slots in want[g]:
+ * entries exist in [first_index, last_index] (first_index - 1 is the
+ * snapshot index); at most max_ents entries per MsgApp. */
+void orc_progress_send_batch(uint64_t G, uint32_t S, uint32_t F, uint64_t stride, uint64_t *match,
+                             uint64_t *next, uint64_t *pending, uint8_t *pflags, uint8_t *istart,
+                             uint8_t *icount, uint64_t *ibuf, const uint64_t *first_index,
+                             const uint64_t *last_index, const void *want, uint32_t send_if_empty,
+                             uint32_t max_ents, void *sent, void *snap) {
+  uint32_t mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  for (uint64_t g = 0; g < G; g++) {
+    uint32_t w = ld_mask(want, mb, g) & full, sm = 0, sn = 0;
+    uint64_t fi = first_index[g], li = last_index[g];
+    for (uint32_t s = 0; s < S; s++) {
+      if (!((w >> s) & 1u)) continue;
+      uint64_t off = s * stride + g;
+      orc_pr p;
+      pr_load(&p, off, stride, F, match, next, pending, pflags, istart, icount, ibuf, s, g);
+      if (pr_is_paused(&p)) continue;
+      if (p.next > li) { /* no entries */
+        if (!send_if_empty) continue;
+        sm |= 1u << s;
+      } else if (p.next < fi) { /* entries compacted -> snapshot */
+        if (!p.recent_active) continue;
+        pr_become_snapshot(&p, fi - 1);
+        sm |= 1u << s;
+        sn |= 1u << s;
+      } else {
+        uint64_t last = p.next + (max_ents ? max_ents : 1) - 1;
+        if (last > li || last < p.next) last = li;
+        if (p.state == PR_REPLICATE) {
+          p.next = last + 1; /* OptimisticUpdate */
+          infl_add(&p, last);
+        } else if (p.state == PR_PROBE) {
+          p.probe_sent = 1;
+        }
+        sm |= 1u << s;
+      }
+      pr_store(&p, off, match, next, pending, pflags, istart, icount);
+    }
+    if (sent) st_mask(sent, mb, g, sm);
+    if (snap) st_mask(snap, mb, g, sn);
+  }
+}
+
+/* Scalar helpers for the golden tables (tests only). */
+int orc_pr_maybe_decr_to(uint32_t state, uint64_t *match, uint64_t *next, uint64_t rejected,
+                         uint64_t hint) {
+  orc_pr p;
+  memset(&p, 0, sizeof(p));
+  p.state = state;
+  p.match = *match;
+  p.next = *next;
+  int r = pr_maybe_decr_to(&p, rejected, hint);
+  *match = p.match;
+  *next = p.next;
+  return r;
+}
+
+int orc_pr_is_paused(uint32_t state, uint32_t probe_sent, uint32_t count, uint32_t size) {
+  orc_pr p;
+  memset(&p, 0, sizeof(p));
+  p.state = state;
+  p.probe_sent = probe_sent;
+  p.count = count;
+  p.size = size;
+  return pr_is_paused(&p);
+}
+
+uint64_t orc_pr_become_probe(uint32_t state, uint64_t match, uint64_t next, uint64_t pending) {
+  orc_pr p;
+  memset(&p, 0, sizeof(p));
+  p.state = state;
+  p.match = match;
+  p.next = next;
+  p.pending = pending;
+  pr_become_probe(&p);
+  return p.next;
+}
+
+/* Inflights op sequence on a contiguous buffer: ops[i] >= 0 -> Add(ops[i]),
+ * ops[i] == -1 -> FreeFirstOne, ops[i] <= -2 -> FreeLE(-ops[i] - 2). */
+void orc_inflights_ops(uint32_t size, uint32_t *start, uint32_t *count, uint64_t *buf,
+                       const int64_t *ops, uint32_t nops) {
+  orc_pr p;
+  memset(&p, 0, sizeof(p));
+  p.size = size;
+  p.start = *start;
+  p.count = *count;
+  p.buf = buf;
+  p.bstride = 1;
+  for (uint32_t i = 0; i < nops; i++) {
+    if (ops[i] >= 0) infl_add(&p, (uint64_t)ops[i]);
+    else if (ops[i] == -1) infl_free_le(&p, *ib(&p, p.start));
+    else infl_free_le(&p, (uint64_t)(-ops[i] - 2));
+  }
+  *start = p.start;
+  *count = p.count;
+}
