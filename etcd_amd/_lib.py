@@ -90,6 +90,28 @@ class QeConfStateCSR(C.Structure):
                 ("learners_off", vp), ("learners_next", vp), ("learners_next_off", vp)]
 
 
+class QeProgress(C.Structure):
+    _fields_ = [
+        ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("inflight_cap", u32),
+        ("stride", u64), ("match", vp), ("next", vp), ("pending_snapshot", vp), ("flags", vp),
+        ("infl_start", vp), ("infl_count", vp), ("infl_buf", vp), ("committed", vp),
+        ("term_start", vp), ("first_index", vp), ("last_index", vp), ("log_runs", u32),
+        ("reserved", u32), ("run_first", vp), ("run_term", vp), ("run_count", vp),
+        ("inc_mask", vp), ("out_mask", vp),
+    ]
+
+
+class QePeerMsgs(C.Structure):
+    _fields_ = [("type", vp), ("index", vp), ("reject_hint", vp), ("log_term", vp),
+                ("send_mask", vp), ("bcast", vp)]
+
+
+QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
+QE_PF_STATE, QE_PF_PROBE_SENT, QE_PF_RECENT_ACTIVE = 3, 4, 8
+QE_MSG_NONE, QE_MSG_APP_RESP, QE_MSG_APP_RESP_REJECT, QE_MSG_HEARTBEAT_RESP = 0, 1, 2, 3
+QE_MAX_INFLIGHT = 255
+QE_MAX_LOG_RUNS = 16
+
 QE_PACK_TOO_MANY_PEERS = 1
 QE_PACK_LEARNER_IS_VOTER = 2
 QE_PACK_LEARNER_NEXT_NOT_OUTGOING = 4
@@ -118,6 +140,8 @@ PROTOTYPES = {
     "qe_pack_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp]),
     "qe_slot_lookup": (C.c_int, [u64, u32, vp, u64, vp, vp, vp]),
     "qe_pack_threads": (C.c_int, [C.c_int]),
+    "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
+    "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, u32, vp, vp, vp]),
 }
 
 

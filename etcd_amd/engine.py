@@ -253,3 +253,109 @@ def election_steps(est, seed, step0, steps, p_drop=13107, p_grant=32768, stats=N
 
 def tune(key, value):
     check("qe_tune", _lib.lib().qe_tune(key.encode(), int(value)))
+
+
+class ProgressState:
+    """Device-resident leader-side Progress of G groups (qe_progress):
+    match/next/pending [S][stride], flags, Inflights rings [S][F][stride],
+    committed, and the leader-log model (term runs)."""
+
+    def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None):
+        if not 1 <= S <= _lib.QE_MAX_SLOTS or not 1 <= F <= _lib.QE_MAX_INFLIGHT:
+            raise ValueError("bad num_slots / inflight_cap")
+        if not 1 <= R <= _lib.QE_MAX_LOG_RUNS:
+            raise ValueError("bad log_runs")
+        self.G, self.S, self.F, self.R = int(G), int(S), int(F), int(R)
+        self.device = torch.device(device)
+        self.group_offset = int(group_offset)
+        self.stride = int(stride) if stride else max(ROW_ALIGN, -(-self.G // ROW_ALIGN) * ROW_ALIGN)
+        dev, n = self.device, self.S * self.stride
+        i64, u8 = torch.int64, torch.uint8
+        self.match = torch.zeros(n, dtype=i64, device=dev)
+        self.next = torch.ones(n, dtype=i64, device=dev)
+        self.pending = torch.zeros(n, dtype=i64, device=dev)
+        self.flags = torch.zeros(n, dtype=u8, device=dev)
+        self.istart = torch.zeros(n, dtype=u8, device=dev)
+        self.icount = torch.zeros(n, dtype=u8, device=dev)
+        self.ibuf = torch.zeros(self.S * self.F * self.stride, dtype=i64, device=dev)
+        self.committed = torch.zeros(self.G, dtype=i64, device=dev)
+        self.term_start = torch.zeros(self.G, dtype=i64, device=dev)
+        self.first_index = torch.ones(self.G, dtype=i64, device=dev)
+        self.last_index = torch.zeros(self.G, dtype=i64, device=dev)
+        self.run_first = torch.zeros(self.R * self.stride, dtype=i64, device=dev)
+        self.run_term = torch.zeros(self.R * self.stride, dtype=i64, device=dev)
+        self.run_count = torch.zeros(self.G, dtype=u8, device=dev)
+        md = mask_torch_dtype(S)
+        self.inc = torch.zeros(self.G, dtype=md, device=dev) if "inc" in masks else None
+        self.out = torch.zeros(self.G, dtype=md, device=dev) if "out" in masks else None
+
+    def struct(self):
+        return _lib.QeProgress(
+            self.G, self.group_offset, self.S, self.F, self.stride, _ptr(self.match),
+            _ptr(self.next), _ptr(self.pending), _ptr(self.flags), _ptr(self.istart),
+            _ptr(self.icount), _ptr(self.ibuf), _ptr(self.committed), _ptr(self.term_start),
+            _ptr(self.first_index), _ptr(self.last_index), self.R, 0, _ptr(self.run_first),
+            _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out))
+
+    ARRAYS = ("match", "next", "pending", "flags", "istart", "icount", "ibuf", "committed",
+              "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
+              "inc", "out")
+
+    def load_host(self, **arrays):
+        """numpy arrays (uint64 as uint64, masks/flags as uint8/uint16)."""
+        for k, a in arrays.items():
+            dst = getattr(self, k)
+            if dst is None or a is None:
+                continue
+            a = np.ascontiguousarray(a)
+            if a.dtype == np.uint64:
+                a = a.view(np.int64)
+            elif a.dtype == np.uint16:
+                a = a.view(np.int16)
+            dst.copy_(torch.from_numpy(a.reshape(-1)[: dst.numel()].copy()).to(self.device))
+        return self
+
+    def host(self):
+        out = {}
+        for k in self.ARRAYS:
+            t = getattr(self, k)
+            if t is None:
+                out[k] = None
+                continue
+            a = t.cpu().numpy()
+            out[k] = a.view(np.uint64) if a.dtype == np.int64 else (
+                a.view(np.uint16) if a.dtype == np.int16 else a)
+        return out
+
+
+class PeerMsgs:
+    """One round of per-peer messages for qe_progress_step ([S][stride])."""
+
+    def __init__(self, ps):
+        dev, n = ps.device, ps.S * ps.stride
+        self.type = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.index = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.reject_hint = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.log_term = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.send_mask = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=dev)
+        self.bcast = torch.zeros(ps.G, dtype=torch.uint8, device=dev)
+
+    def struct(self):
+        return _lib.QePeerMsgs(_ptr(self.type), _ptr(self.index), _ptr(self.reject_hint),
+                               _ptr(self.log_term), _ptr(self.send_mask), _ptr(self.bcast))
+
+
+def progress_step(ps, msgs, stats=None):
+    p, m = ps.struct(), msgs.struct()
+    check("qe_progress_step", _lib.lib().qe_progress_step(C.byref(p), C.byref(m), _ptr(stats),
+                                                           _stream(ps.device)))
+
+
+def progress_send(ps, want, send_if_empty=False, max_ents=1):
+    sent = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
+    snap = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
+    p = ps.struct()
+    check("qe_progress_send", _lib.lib().qe_progress_send(
+        C.byref(p), _ptr(want), int(bool(send_if_empty)), int(max_ents), _ptr(sent), _ptr(snap),
+        _stream(ps.device)))
+    return sent, snap

@@ -57,6 +57,15 @@ def _declare(L):
         "orc_gf_run": (dbl, [vp, vp, vp, i32, i32]),
         "orc_soa_run": (dbl, [u64, u32, u64, vp, vp, vp, vp, vp, vp, vp, i32, i32]),
         "orc_max_threads": (i32, []),
+        "orc_progress_step_batch": (None, [u64, u64, u32, u32, u64] + [vp] * 10 + [u32]
+                                    + [vp] * 12 + [i32]),
+        "orc_progress_send_batch": (None, [u64, u32, u32, u64] + [vp] * 10 + [u32, u32, vp, vp]),
+        "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
+        "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
+        "orc_pr_maybe_decr_to": (i32, [u32, vp, vp, u64, u64]),
+        "orc_pr_is_paused": (i32, [u32, u32, u32, u32]),
+        "orc_pr_become_probe": (u64, [u32, u64, u64, u64]),
+        "orc_inflights_ops": (None, [u32, vp, vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -141,3 +150,57 @@ def election_steps(G, goff, S, term, state, voted, granted, self_slot, inc, out,
 
 def max_threads():
     return lib().orc_max_threads()
+
+
+class ProgressBatch:
+    """Host mirror of qe_progress (numpy arrays, same layout)."""
+
+    def __init__(self, G, S, F, R, stride=None):
+        self.G, self.S, self.F, self.R = G, S, F, R
+        self.stride = stride or G
+        n = S * self.stride
+        self.match = np.zeros(n, np.uint64)
+        self.next = np.ones(n, np.uint64)
+        self.pending = np.zeros(n, np.uint64)
+        self.flags = np.zeros(n, np.uint8)
+        self.istart = np.zeros(n, np.uint8)
+        self.icount = np.zeros(n, np.uint8)
+        self.ibuf = np.zeros(S * F * self.stride, np.uint64)
+        self.committed = np.zeros(G, np.uint64)
+        self.term_start = np.zeros(G, np.uint64)
+        self.first_index = np.ones(G, np.uint64)
+        self.last_index = np.zeros(G, np.uint64)
+        self.run_first = np.zeros(max(R, 1) * self.stride, np.uint64)
+        self.run_term = np.zeros(max(R, 1) * self.stride, np.uint64)
+        self.run_count = np.zeros(G, np.uint8)
+        self.inc = None
+        self.out = None
+
+    def copy(self):
+        c = ProgressBatch.__new__(ProgressBatch)
+        for k, v in self.__dict__.items():
+            setattr(c, k, v.copy() if isinstance(v, np.ndarray) else v)
+        return c
+
+
+def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0):
+    send = np.zeros(pb.G, mask_dtype(pb.S))
+    bcast = np.zeros(pb.G, np.uint8)
+    stats = np.zeros(NSTAT, np.uint64)
+    lib().orc_progress_step_batch(
+        pb.G, goff, pb.S, pb.F, pb.stride, P(pb.match), P(pb.next), P(pb.pending), P(pb.flags),
+        P(pb.istart), P(pb.icount), P(pb.ibuf), P(pb.committed), P(pb.term_start),
+        P(pb.last_index), pb.R, P(pb.run_first), P(pb.run_term),
+        P(pb.run_count), P(pb.inc), P(pb.out), P(mtype), P(mindex), P(mhint), P(mlogterm),
+        P(send), P(bcast), P(stats), threads)
+    return send, bcast, stats
+
+
+def progress_send(pb, want, send_if_empty, max_ents):
+    sent = np.zeros(pb.G, mask_dtype(pb.S))
+    snap = np.zeros(pb.G, mask_dtype(pb.S))
+    lib().orc_progress_send_batch(
+        pb.G, pb.S, pb.F, pb.stride, P(pb.match), P(pb.next), P(pb.pending), P(pb.flags),
+        P(pb.istart), P(pb.icount), P(pb.ibuf), P(pb.first_index), P(pb.last_index), P(want),
+        send_if_empty, max_ents, P(sent), P(snap))
+    return sent, snap

@@ -17,6 +17,11 @@ Sources (read as text; nothing from the reference is executed):
   * TestCommit table, raft/raft_test.go:1127-1152.
   * TestLeaderElectionInOneRoundRPC table, raft/raft_paper_test.go:192-216.
   * TestProgressUpdate table, raft/tracker/progress_test.go:149-161.
+  * TestProgressMaybeDecr / IsPaused / BecomeProbe / BecomeReplicate /
+    BecomeSnapshot / Resume, raft/tracker/progress_test.go:40-245.
+  * TestInflightsAdd / TestInflightFreeTo / TestInflightFreeFirstOne
+    (raft/tracker/inflights_test.go:22-190), transcribed as op sequences.
+  * TestFastLogRejection leader-side rows, raft/raft_test.go:4319-4540.
 
 Outputs (data only: inputs + expected outputs):
   tests/golden/quorum_testdata.jsonl   127 rows
@@ -176,6 +181,100 @@ def progress_update_table():
     return rows
 
 
+STATES = {"StateProbe": 0, "StateReplicate": 1, "StateSnapshot": 2}
+
+
+def _body(path, fn):
+    src = open(os.path.join(REF, path), encoding="utf-8").read()
+    start = src.index(f"func {fn}(t *testing.T)")
+    end = src.index("\n}\n", start)
+    return src[start:end]
+
+
+def progress_tables():
+    out = {}
+    b = _body("tracker/progress_test.go", "TestProgressMaybeDecr")
+    rows = []
+    for m in re.finditer(r"(State\w+), (\d+), (\d+), (\d+), (\d+), (true|false), (\d+),", b):
+        rows.append({"state": STATES[m.group(1)], "match": int(m.group(2)), "next": int(m.group(3)),
+                     "rejected": int(m.group(4)), "last": int(m.group(5)),
+                     "want": m.group(6) == "true", "want_next": int(m.group(7))})
+    assert len(rows) == 10, len(rows)
+    out["TestProgressMaybeDecr"] = {"source": "raft/tracker/progress_test.go:181-245", "rows": rows}
+    b = _body("tracker/progress_test.go", "TestProgressIsPaused")
+    rows = [{"state": STATES[a], "probe_sent": p == "true", "want": w == "true"}
+            for a, p, w in re.findall(r"\{(State\w+), (true|false), (true|false)\}", b)]
+    assert len(rows) == 6, len(rows)
+    out["TestProgressIsPaused"] = {"source": "raft/tracker/progress_test.go:40-66", "rows": rows}
+    b = _body("tracker/progress_test.go", "TestProgressBecomeProbe")
+    match = int(re.search(r"match := uint64\((\d+)\)", b).group(1))
+    rows = []
+    for m in re.finditer(r"&Progress\{State: (State\w+), Match: match, Next: (\d+),"
+                         r"(?: PendingSnapshot: (\d+),)? Inflights: NewInflights\(256\)\},\s*(\d+),", b):
+        rows.append({"state": STATES[m.group(1)], "match": match, "next": int(m.group(2)),
+                     "pending": int(m.group(3) or 0), "want_next": int(m.group(4))})
+    assert len(rows) == 3, len(rows)
+    out["TestProgressBecomeProbe"] = {"source": "raft/tracker/progress_test.go:84-117", "rows": rows}
+    # single-case tests, transcribed (progress_test.go:68-82, :119-147)
+    out["TestProgressBecomeReplicate"] = {"source": "raft/tracker/progress_test.go:119-132",
+                                          "rows": [{"state": 0, "match": 1, "next": 5,
+                                                    "want_state": 1, "want_next": 2}]}
+    out["TestProgressBecomeSnapshot"] = {"source": "raft/tracker/progress_test.go:134-147",
+                                         "rows": [{"state": 0, "match": 1, "next": 5, "snap": 10,
+                                                   "want_state": 2, "want_pending": 10}]}
+    out["TestProgressResume"] = {"source": "raft/tracker/progress_test.go:68-82",
+                                 "rows": [{"next": 2, "decr_rejected": 1, "decr_hint": 1,
+                                           "update": 2, "want_probe_sent": False}]}
+    return out
+
+
+def inflights_tables():
+    """inflights_test.go:22-190 as op sequences: op >= 0 Add(op), -1
+    FreeFirstOne, -(k+2) FreeLE(k); each check lists the expected
+    (start, count, buffer)."""
+    return {"source": "raft/tracker/inflights_test.go:22-190", "rows": [
+        {"name": "TestInflightsAdd/no-rotate", "size": 10, "start": 0,
+         "steps": [{"ops": [0, 1, 2, 3, 4], "start": 0, "count": 5,
+                    "buffer": [0, 1, 2, 3, 4, 0, 0, 0, 0, 0]},
+                   {"ops": [5, 6, 7, 8, 9], "start": 0, "count": 10,
+                    "buffer": [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]}]},
+        {"name": "TestInflightsAdd/rotate", "size": 10, "start": 5,
+         "steps": [{"ops": [0, 1, 2, 3, 4], "start": 5, "count": 5,
+                    "buffer": [0, 0, 0, 0, 0, 0, 1, 2, 3, 4]},
+                   {"ops": [5, 6, 7, 8, 9], "start": 5, "count": 10,
+                    "buffer": [5, 6, 7, 8, 9, 0, 1, 2, 3, 4]}]},
+        {"name": "TestInflightFreeTo", "size": 10, "start": 0,
+         "steps": [{"ops": list(range(10)) + [-(4 + 2)], "start": 5, "count": 5,
+                    "buffer": list(range(10))},
+                   {"ops": [-(8 + 2)], "start": 9, "count": 1, "buffer": list(range(10))},
+                   {"ops": [10, 11, 12, 13, 14, -(12 + 2)], "start": 3, "count": 2,
+                    "buffer": [10, 11, 12, 13, 14, 5, 6, 7, 8, 9]},
+                   {"ops": [-(14 + 2)], "start": 0, "count": 0,
+                    "buffer": [10, 11, 12, 13, 14, 5, 6, 7, 8, 9]}]},
+        {"name": "TestInflightFreeFirstOne", "size": 10, "start": 0,
+         "steps": [{"ops": list(range(10)) + [-1], "start": 1, "count": 9,
+                    "buffer": list(range(10))}]},
+    ]}
+
+
+def fast_log_rejection_table():
+    b = _body("raft_test.go", "TestFastLogRejection")
+    table = b[:b.index("for i, test := range tests")]
+    rows = []
+    for case in re.split(r"\n\t\t\{\n", table)[1:]:
+        lead = case[case.index("leaderLog:"):case.index("followerLog:")]
+        ents = [[int(i), int(t)] for t, i in re.findall(r"\{Term: (\d+), Index: (\d+)\}", lead)]
+        def val(k):
+            return int(re.search(k + r":\s+(\d+)", case).group(1))
+        rows.append({"leader_log": ents, "reject_hint_index": val("rejectHintIndex"),
+                     "reject_hint_term": val("rejectHintTerm"),
+                     "next_append_index": val("nextAppendIndex"),
+                     "next_append_term": val("nextAppendTerm")})
+    assert len(rows) == 8, len(rows)
+    return {"source": "raft/raft_test.go:4319-4600 (leader side: heartbeat resp -> probe MsgApp "
+                      "-> rejection -> next MsgApp)", "rows": rows}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are already committed")
@@ -188,6 +287,9 @@ def main():
         "TestCommit": {"source": "raft/raft_test.go:1127-1152", "rows": test_commit_table()},
         "TestLeaderElectionInOneRoundRPC": {"source": "raft/raft_paper_test.go:192-216", "rows": election_table()},
         "TestProgressUpdate": {"source": "raft/tracker/progress_test.go:149-161", "rows": progress_update_table()},
+        **progress_tables(),
+        "Inflights": inflights_tables(),
+        "TestFastLogRejection": fast_log_rejection_table(),
     }
     with open(os.path.join(HERE, "raft_tables.json"), "w", encoding="utf-8") as f:
         json.dump(tables, f, indent=1)

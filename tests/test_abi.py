@@ -55,6 +55,8 @@ int main(void) {
   Z(qe_election_params) F(qe_election_params, steps) F(qe_election_params, p_grant_q16)
   Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
   Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
+  Z(qe_progress) F(qe_progress, infl_buf) F(qe_progress, log_runs) F(qe_progress, out_mask)
+  Z(qe_peer_msgs) F(qe_peer_msgs, bcast)
   return 0;
 }
 """
@@ -63,7 +65,8 @@ CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
           "qe_repl_state": _lib.QeReplState, "qe_repl_msgs": _lib.QeReplMsgs,
           "qe_election_state": _lib.QeElectionState,
           "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams,
-          "qe_confstate_csr": _lib.QeConfStateCSR}
+          "qe_confstate_csr": _lib.QeConfStateCSR, "qe_progress": _lib.QeProgress,
+          "qe_peer_msgs": _lib.QePeerMsgs}
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -116,6 +119,10 @@ def test_argument_errors_without_gpu():
     assert L.qe_tune(b"blocks_per_cu", -1) == _lib.QE_ERANGE
     assert L.qe_tune(b"blocks_per_cu", 33) == _lib.QE_ERANGE
     assert L.qe_tune(b"nope", 1) == _lib.QE_EINVAL
+    pr = _lib.QeProgress(num_groups=1, num_slots=3, inflight_cap=0, stride=1)
+    assert L.qe_progress_step(C.byref(pr), C.byref(_lib.QePeerMsgs()), None, None) == _lib.QE_ERANGE
+    pr = _lib.QeProgress(num_groups=1, num_slots=3, inflight_cap=4, stride=1, log_runs=17)
+    assert L.qe_progress_send(C.byref(pr), None, 0, 1, None, None, None) == _lib.QE_ERANGE
     p = _lib.QeElectionParams(p_drop_q16=70000)
     st = _lib.QeElectionState(num_groups=1, num_slots=3, term=C.c_void_p(64),
                               state=C.c_void_p(64), voted=C.c_void_p(64),

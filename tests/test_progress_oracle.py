@@ -1,0 +1,128 @@
+"""The Progress state-machine oracle (oracle/quorum_oracle.c, SURVEY.md
+§8(f) rows 3-4) pinned to the reference's own tables: TestProgressMaybeDecr,
+IsPaused, BecomeProbe/Replicate/Snapshot, Resume, the Inflights tests and the
+leader side of TestFastLogRejection."""
+import numpy as np
+
+from oracle import orc
+from tests.golden_util import raft_tables
+
+T = raft_tables()
+PF_PROBE_SENT, PF_RECENT_ACTIVE = 4, 8
+
+
+def log_runs(entries, extra=None):
+    """[(index, term)] (+ an appended entry) -> run_first, run_term arrays with
+    run 0 at the dummy index 0 (term 0), as MemoryStorage starts."""
+    ents = sorted(entries + ([extra] if extra else []))
+    first, term = [0], [0]
+    for i, t in ents:
+        if t != term[-1]:
+            first.append(i)
+            term.append(t)
+    return np.array(first, np.uint64), np.array(term, np.uint64), ents[-1][0]
+
+
+def test_maybe_decr_table(orc):
+    L = orc.lib()
+    for r in T["TestProgressMaybeDecr"]["rows"]:
+        m = np.array([r["match"]], np.uint64)
+        n = np.array([r["next"]], np.uint64)
+        ok = L.orc_pr_maybe_decr_to(r["state"], orc.P(m), orc.P(n), r["rejected"], r["last"])
+        assert (bool(ok), int(m[0]), int(n[0])) == (r["want"], r["match"], r["want_next"]), r
+
+
+def test_is_paused_table(orc):
+    for r in T["TestProgressIsPaused"]["rows"]:
+        assert bool(orc.lib().orc_pr_is_paused(r["state"], r["probe_sent"], 0, 256)) == r["want"], r
+
+
+def test_become_probe_table(orc):
+    for r in T["TestProgressBecomeProbe"]["rows"]:
+        assert orc.lib().orc_pr_become_probe(r["state"], r["match"], r["next"], r["pending"]) == r["want_next"]
+
+
+def test_inflights_tables(orc):
+    for case in T["Inflights"]["rows"]:
+        size = case["size"]
+        start = np.array([case["start"]], np.uint32)
+        count = np.array([0], np.uint32)
+        buf = np.zeros(size, np.uint64)
+        for st in case["steps"]:
+            ops = np.array(st["ops"], np.int64)
+            orc.lib().orc_inflights_ops(size, orc.P(start), orc.P(count), orc.P(buf), orc.P(ops),
+                                        len(ops))
+            assert (int(start[0]), int(count[0])) == (st["start"], st["count"]), case["name"]
+            assert buf.tolist() == st["buffer"], case["name"]
+
+
+def _one_group(F=16):
+    pb = orc.ProgressBatch(1, 1, F, 16)
+    return pb
+
+
+def test_fast_log_rejection_leader_side(orc):
+    """raft_test.go TestFastLogRejection, leader side, through the batch
+    runners: becomeLeader appends an empty entry at term 1 (the test's fresh
+    raft is at term 0 -> campaign -> term 1); the follower's heartbeat
+    response triggers a probe MsgApp at lastIndex-1; its rejection (hint
+    index / log term) goes through findConflictByTerm + MaybeDecrTo; the
+    next MsgApp's (Index, LogTerm) must match the test."""
+    L = orc.lib()
+    for r in T["TestFastLogRejection"]["rows"]:
+        lead = [tuple(e) for e in r["leader_log"]]
+        l_last = max(i for i, _ in lead)
+        rf, rt, last = log_runs(lead, (l_last + 1, 1))
+        pb = _one_group()
+        pb.run_first[: len(rf)] = rf
+        pb.run_term[: len(rt)] = rt
+        pb.run_count[0] = len(rf)
+        pb.first_index[0], pb.last_index[0] = 1, last
+        pb.term_start[0] = l_last + 1
+        pb.next[0], pb.match[0] = l_last + 1, 0  # reset(): Next = lastIndex+1 before the append
+        z = lambda v: np.array([v], np.uint64)
+        # heartbeat response -> sendAppend
+        send, _, _ = orc.progress_step(pb, np.array([3], np.uint8), z(0), z(0), z(0))
+        assert send[0] == 1
+        sent, snap = orc.progress_send(pb, send, 0, 1 << 20)
+        assert sent[0] == 1 and pb.flags[0] & PF_PROBE_SENT
+        # rejection of the MsgApp at Index = Next-1 = l_last
+        send, _, _ = orc.progress_step(pb, np.array([2], np.uint8), z(l_last),
+                                       z(r["reject_hint_index"]), z(r["reject_hint_term"]))
+        assert send[0] == 1
+        nxt = int(pb.next[0])
+        idx = nxt - 1
+        term = L.orc_log_term(len(rf), orc.P(rf), orc.P(rt), last, idx)
+        assert (idx, term) == (r["next_append_index"], r["next_append_term"]), r
+
+
+def test_find_conflict_by_term_jump_equals_walk(orc):
+    """The device walks term runs instead of single indexes; restate that
+    jump form here and check it against the linear loop of log.go:147-168."""
+    rng = np.random.default_rng(1)
+    L = orc.lib()
+    for _ in range(2000):
+        R = int(rng.integers(1, 6))
+        first = np.sort(rng.choice(np.arange(0, 40), R, replace=False)).astype(np.uint64)
+        term = rng.integers(0, 8, R).astype(np.uint64)
+        last = int(first[-1] + rng.integers(0, 5))
+        index = int(rng.integers(0, last + 3))
+        t = int(rng.integers(1, 9))
+        walk = L.orc_find_conflict_by_term(R, orc.P(first), orc.P(term), last, index, t)
+        # jump form (qe_kernels.hpp find_conflict_by_term)
+        if index > last or index < first[0]:
+            jump = index
+        else:
+            r = R - 1
+            while r > 0 and first[r] > index:
+                r -= 1
+            jump = None
+            while r >= 0:
+                if term[r] <= t:
+                    jump = index
+                    break
+                index = int(first[r]) - 1 if first[r] > 0 else (1 << 64) - 1
+                r -= 1
+            if jump is None:
+                jump = index
+        assert walk == jump
