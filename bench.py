@@ -47,6 +47,9 @@ WORKLOADS = {
                      "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
     "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
                      1 << 21, 5, "elec"),
+    "progress_step": ("16M groups x 5 peers: one round of MsgAppResp accept/reject + "
+                      "MsgHeartbeatResp through the full Progress state machine "
+                      "(inflights F=8, leader-log model R=4)", 1 << 24, 5, "progress"),
 }
 
 
@@ -203,6 +206,50 @@ def setup(name, G, S, kind, d, stats):
         # HBM bytes per group-step: state in+out / steps (register-resident)
         bpg = (8 + 1 + 1 + 1 + 1 + 1 + 8 + 1 + 1 + 1) / steps_per_launch
         return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
+    if kind == "progress":
+        F, R = 8, 4
+        ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff)
+        n = S * ps.stride
+        gen = torch.Generator(device=d.dev).manual_seed(0x5EED + d.rank)
+        base = torch.randint(1 << 20, 1 << 40, (ps.stride,), device=d.dev, generator=gen)
+        ps.match.copy_((base.repeat(S) + torch.randint(0, 64, (n,), device=d.dev, generator=gen)))
+        ps.next.copy_(ps.match + 1 + torch.randint(0, 4, (n,), device=d.dev, generator=gen))
+        ps.flags.fill_(1 | 8)  # StateReplicate, RecentActive
+        ps.icount.copy_(torch.randint(0, F + 1, (n,), device=d.dev, generator=gen).to(torch.uint8))
+        for k in range(F):
+            ps.ibuf.view(S, F, ps.stride)[:, k, :] = ps.match.view(S, ps.stride) + 1 + 8 * k
+        ps.last_index.copy_(base[:G] + 128)
+        ps.term_start.copy_(base[:G])
+        ps.first_index.copy_(base[:G] - 64)
+        ps.committed.copy_(base[:G])
+        rf = ps.run_first.view(R, ps.stride)
+        for r in range(R):
+            rf[r].copy_(base - 65 + 40 * r)
+        ps.run_term.view(R, ps.stride).copy_(
+            torch.arange(1, R + 1, device=d.dev).repeat_interleave(ps.stride).view(R, ps.stride))
+        ps.run_count.fill_(R)
+        msgs = engine.PeerMsgs(ps)
+        u = torch.rand(n, device=d.dev, generator=gen)
+        msgs.type.copy_(torch.where(u < 0.7, 1, torch.where(u < 0.8, 2, torch.where(u < 0.9, 3, 0)))
+                        .to(torch.uint8))
+        msgs.index.copy_(ps.match + torch.randint(0, 96, (n,), device=d.dev, generator=gen))
+        msgs.reject_hint.copy_(ps.match)
+        msgs.log_term.copy_(torch.randint(0, 4, (n,), device=d.dev, generator=gen))
+        import ctypes as C
+        p_, m_ = ps.struct(), msgs.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            engine.check("qe_progress_step",
+                         lib.qe_progress_step(C.byref(p_), C.byref(m_), sp, stream))
+
+        # per peer: match/next/pending rw (48) + flags/start/count rw (6) +
+        # >= 1 inflight read (8) + message (25); per group: committed rw (16),
+        # term_start/last_index/run_count (17), send mask + bcast out (2)
+        bpg = S * (48 + 6 + 8 + 25) + 16 + 17 + 2
+        return step, bpg, G, "group-rounds", {"ps": ps, "msgs": msgs}
     raise ValueError(kind)
 
 

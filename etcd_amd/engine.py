@@ -312,7 +312,8 @@ class ProgressState:
                 a = a.view(np.int64)
             elif a.dtype == np.uint16:
                 a = a.view(np.int16)
-            dst.copy_(torch.from_numpy(a.reshape(-1)[: dst.numel()].copy()).to(self.device))
+            a = a.reshape(-1)[: dst.numel()]
+            dst[: a.size].copy_(torch.from_numpy(a.copy()).to(self.device))
         return self
 
     def host(self):

@@ -260,7 +260,7 @@ int qe_election_steps(const qe_election_state *st,
 #define QE_MAX_INFLIGHT 255     /* Inflights capacity (MaxInflightMsgs)      */
 #define QE_MAX_LOG_RUNS 16      /* term runs of the leader-log model          */
 
-/* message kinds of qe_peer_msgs.type */
+/* message kinds of qe_peer_msgs.type (any other value: no message) */
 #define QE_MSG_NONE 0
 #define QE_MSG_APP_RESP 1         /* MsgAppResp, Reject=false                */
 #define QE_MSG_APP_RESP_REJECT 2  /* MsgAppResp, Reject=true                 */

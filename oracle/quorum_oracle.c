@@ -949,7 +949,7 @@ void orc_progress_step_batch(uint64_t G, uint64_t goff, uint32_t S, uint32_t F, 
       for (uint32_t s = 0; s < S; s++) {
         uint64_t off = s * stride + g;
         uint32_t ty = mtype[off];
-        if (ty == 0) continue;
+        if (ty == 0 || ty > 3) continue; /* no message / unknown kind: ignored */
         orc_pr p;
         pr_load(&p, off, stride, F, match, next, pending, pflags, istart, icount, ibuf, s, g);
         p.recent_active = 1;

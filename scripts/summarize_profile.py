@@ -30,6 +30,7 @@ DOMINANT = {
     "config3_joint": "void qe::k_commit_vote<10, 2,",  # bucketed + rotated runs share it
     "config4_repl": "void qe::k_replication<5,",
     "config5_elec": "void qe::k_election<5,",
+    "progress_step": "void qe::k_progress_step<5,",
 }
 
 
