@@ -537,6 +537,8 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
     uint32_t sta = a.state[g];
     uint32_t vd = vdp[g] & kFull, gr = grp[g] & kFull;
     const uint32_t others = prog & ~self;
+    // counter-based RNG key (oracle/quorum_oracle.c elec_gkey), once per group
+    const uint64_t gkey = mix64(a.seed + gid * kPhi) ^ 0x6A09E667F3BCC909ull;
     for (uint32_t k = 0; promotable && k < a.steps; k++) {
       const uint64_t step = a.step0 + k;
       if (sta != QE_STATE_CANDIDATE) {
@@ -548,12 +550,11 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
         cnt[E_ELEC] += 1;
         elec_tally(mi, mo, ml, vd, gr, 0u, sta, cnt);
       } else {
-        const uint64_t h = hash4(a.seed, gid, static_cast<uint32_t>(step),
-                                 3u + static_cast<uint32_t>(step >> 32));
+        const uint64_t h = mix64(gkey + step * 0xD6E8FEB86659FD93ull);
         uint32_t resp = 0, val = 0;
 #pragma unroll
         for (int j = 0; j < (S + 1) / 2; j++) {
-          const uint64_t hs = mix64(h + static_cast<uint64_t>(j + 1) * kPhi);
+          const uint64_t hs = j == 0 ? h : mix64(h + static_cast<uint64_t>(j) * kPhi);
 #pragma unroll
           for (int e = 0; e < 2; e++) {
             const int s = 2 * j + e;

@@ -31,12 +31,12 @@ if MODE == "joint":
 else:
     b = engine.SlotBatch(G, S, dev, masks=())
     engine.gen_groups(b, 0x5EED)
-out = engine.Outputs(G, dev)
+out = engine.Outputs(G, dev, tally=False)
 stats = engine.stats_buffer(dev)
 gs, os_, os_nostats = b.struct(), out.struct(stats), out.struct(None)
 lib = engine._lib.lib()
 stream = engine._stream(dev)
-bpg = b.bytes_per_group() + 2
+bpg = b.bytes_per_group()
 res = {i: [] for i in range(len(VARIANTS))}
 for r in range(ROUNDS):
     for i, v in enumerate(VARIANTS):
