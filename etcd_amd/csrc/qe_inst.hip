@@ -54,7 +54,7 @@ static int launch_repl_k(const RArgs &a, hipStream_t st) {
   auto kern = k_replication<S, J, M, MT, V, NT>;
   static int occ = occupancy(kern);
   const uint64_t tiles = ((a.G + 1) / 2 + 63) / 64;
-  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ, 2)), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid_for(tiles, occ, 1)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -81,24 +81,24 @@ int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
   auto kern = k_election<S, MT>;
   static int occ = occupancy(kern);
   const uint64_t waves = (a.G + 63) / 64;
-  hipLaunchKernelGGL(kern, dim3(grid_for(waves, occ)), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid_for(waves, occ, 1)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
   if (kind == 1) {
-    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
+    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 4)),
                        dim3(kBlock), 0, st, a);
   } else if (joint) {
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true>), dim3(grid_for((a.G + 63) / 64, 0, 4)),
                        dim3(kBlock), 0, st, a);
   } else if (masked) {
     hipLaunchKernelGGL((k_progress_step<S, MT, true, false>),
-                       dim3(grid_for((a.G + 63) / 64, 0, 1)), dim3(kBlock), 0, st, a);
+                       dim3(grid_for((a.G + 63) / 64, 0, 4)), dim3(kBlock), 0, st, a);
   } else {
     hipLaunchKernelGGL((k_progress_step<S, MT, false, false>),
-                       dim3(grid_for((a.G + 63) / 64, 0, 1)), dim3(kBlock), 0, st, a);
+                       dim3(grid_for((a.G + 63) / 64, 0, 4)), dim3(kBlock), 0, st, a);
   }
   return hip_status(hipGetLastError());
 }
