@@ -283,6 +283,15 @@ def main():
     with open(os.path.join(HERE, "quorum_testdata.jsonl"), "w", encoding="utf-8") as f:
         for r in rows:
             f.write(json.dumps(r, ensure_ascii=False) + "\n")
+    # the same cases in a line format the C++ test reads without a JSON parser:
+    # <cmd> <joint> <expect> cfg=a,b cfgj=c acked=id:idx,.. votes=id:0|1,.. <source>
+    with open(os.path.join(HERE, "quorum_testdata.txt"), "w", encoding="utf-8") as f:
+        for r in rows:
+            acked = ",".join(f"{k}:{v}" for k, v in r.get("acked", []))
+            votes = ",".join(f"{k}:{int(v)}" for k, v in r.get("votes", []))
+            f.write(f"{r['cmd']} {int(r['joint'])} {r['expect']} "
+                    f"cfg={','.join(map(str, r['cfg']))} cfgj={','.join(map(str, r['cfgj']))} "
+                    f"acked={acked} votes={votes} {r['source']}\n")
     tables = {
         "TestCommit": {"source": "raft/raft_test.go:1127-1152", "rows": test_commit_table()},
         "TestLeaderElectionInOneRoundRPC": {"source": "raft/raft_paper_test.go:192-216", "rows": election_table()},
@@ -293,6 +302,11 @@ def main():
     }
     with open(os.path.join(HERE, "raft_tables.json"), "w", encoding="utf-8") as f:
         json.dump(tables, f, indent=1)
+    # election table in a line format for the C++ test: <size> <state> id:0|1,..
+    with open(os.path.join(HERE, "election_table.txt"), "w", encoding="utf-8") as f:
+        for r in tables["TestLeaderElectionInOneRoundRPC"]["rows"]:
+            votes = ",".join(f"{i}:{int(v)}" for i, v in r["votes"])
+            f.write(f"{r['size']} {r['state']} votes={votes}\n")
     counts = {}
     for r in rows:
         k = r["source"].split("/")[-1].split(":")[0]
