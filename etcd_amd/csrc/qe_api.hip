@@ -10,6 +10,7 @@ namespace qe {
 int g_blocks_per_cu = 0;  // 0 = kernel occupancy
 int g_nontemporal = 3;  // nt loads + nt stores (measured best)
 int g_tiles_per_wave = -1;  // -1 = per-kernel default, 0 = persistent grid
+int g_cv_kernel = -1;  // qe_commit_vote kernel: 0 pair, 1 stream, -1 per-mode default
 
 static thread_local char g_errbuf[256];
 
@@ -141,6 +142,11 @@ int qe_tune(const char *key, int value) {
   if (!strcmp(key, "tiles_per_wave")) {
     if (value < -1 || value > 4096) return QE_ERANGE;
     g_tiles_per_wave = value;
+    return QE_OK;
+  }
+  if (!strcmp(key, "cv_kernel")) {
+    if (value < -1 || value > 1) return QE_ERANGE;
+    g_cv_kernel = value;
     return QE_OK;
   }
   if (!strcmp(key, "nontemporal")) {

@@ -2,6 +2,7 @@
 // (qe_inst.hip) and the C ABI (qe_api.hip).
 #pragma once
 #include "qe_kernels.hpp"
+#include "qe_stream.hpp"
 
 namespace qe {
 

@@ -26,8 +26,31 @@ int launch_cv_k(const CVArgs &a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
+template <int MODE, bool NTL, bool NTS>
+int launch_cv_stream(const CVArgs &a, hipStream_t st) {
+  auto kern = k_cv_stream<S, MODE, MT, NTL, NTS>;
+  const uint64_t tiles = (a.G + 63) / 64;
+  const uint64_t per_block = (kBlock / 64) * QE_STREAM_TPW;
+  const uint64_t blocks = (tiles + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 template <int MODE>
 int launch_cv(const CVArgs &a, bool vec, hipStream_t st) {
+  // default: the stream kernel (measured faster in every mode);
+  // it addresses each 64-group tile through buffer descriptors and needs
+  // no row alignment
+  const int which = g_cv_kernel >= 0 ? g_cv_kernel : 1;
+  if (which == 1) {
+    switch (g_nontemporal & 3) {
+      case 1: return launch_cv_stream<MODE, true, false>(a, st);
+      case 2: return launch_cv_stream<MODE, false, true>(a, st);
+      case 3: return launch_cv_stream<MODE, true, true>(a, st);
+      default: return launch_cv_stream<MODE, false, false>(a, st);
+    }
+  }
   if (!vec) return launch_cv_k<MODE, false, false, false>(a, st);
   switch (g_nontemporal & 3) {
     case 1: return launch_cv_k<MODE, true, true, false>(a, st);

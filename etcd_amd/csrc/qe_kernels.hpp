@@ -27,6 +27,7 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // ---------------------------------------------------------------------------
 extern int g_blocks_per_cu;
 extern int g_nontemporal;  // bit 0: loads, bit 1: stores
+extern int g_cv_kernel;    // qe_commit_vote: 0 pair kernel, 1 stream kernel, -1 default
 
 inline int num_cus() {
   static int cached[64] = {0};
@@ -184,10 +185,8 @@ __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint3
     commit = select_fixed<S>(v);
     inc = kFull;
     out = 0;
-  } else if constexpr (MODE == 1) {
-    out = 0;
-    commit = joint_committed<S>(v, inc, 0u);
   } else {
+    if constexpr (MODE == 1) out = 0;
     commit = joint_committed<S>(v, inc, out);
   }
   vote = joint_vote(inc, out, voted, granted);

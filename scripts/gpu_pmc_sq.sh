@@ -15,7 +15,7 @@ import csv, glob, os
 for f in sorted(glob.glob("gpurun_out/pmc_sq/*/pmc_counter_collection.csv")):
     agg = {}
     for r in csv.DictReader(open(f)):
-        if "k_commit_vote" not in r["Kernel_Name"]:
+        if "k_commit_vote" not in r["Kernel_Name"] and "k_cv_stream" not in r["Kernel_Name"]:
             continue
         agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     print(f.split("/")[2], {k: round(sum(v) / len(v)) for k, v in agg.items()})

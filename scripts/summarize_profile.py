@@ -25,9 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # bench workload -> kernel-name prefix of its dominant kernel
 DOMINANT = {
-    "config2_n5": "void qe::k_commit_vote<5, 0,",
-    "config2_n7": "void qe::k_commit_vote<7, 0,",
-    "config3_joint": "void qe::k_commit_vote<10, 2,",  # bucketed + rotated runs share it
+    "config2_n5": "void qe::k_cv_stream<5, 0,",
+    "config2_n7": "void qe::k_cv_stream<7, 0,",
+    "config3_joint": "void qe::k_cv_stream<10, 2,",  # bucketed + rotated runs share it
     "config4_repl": "void qe::k_replication<5,",
     "config5_elec": "void qe::k_election<5,",
     "progress_step": "void qe::k_progress_step<5,",

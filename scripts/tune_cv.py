@@ -22,6 +22,9 @@ for tpw in [int(x) for x in os.environ.get("TUNE_TPW", "-1,0,1,2,4,8").split(","
     VARIANTS.append({"tiles_per_wave": tpw, "blocks_per_cu": 0, "nontemporal": 3, "stats": 1})
 if os.environ.get("TUNE_ONLY_DEFAULT"):
     VARIANTS = VARIANTS[:1]
+if os.environ.get("TUNE_VARIANTS"):  # JSON list of knob dicts, e.g. [{"cv_kernel": 1}]
+    VARIANTS = [{"stats": 1, **v} for v in json.loads(os.environ["TUNE_VARIANTS"])]
+DEFAULTS = {"tiles_per_wave": -1, "blocks_per_cu": 0, "nontemporal": 3, "cv_kernel": -1}
 MODE = os.environ.get("TUNE_MODE", "majority")
 dev = torch.device("cuda:0")
 if MODE == "joint":
@@ -40,7 +43,7 @@ bpg = b.bytes_per_group()
 res = {i: [] for i in range(len(VARIANTS))}
 for r in range(ROUNDS):
     for i, v in enumerate(VARIANTS):
-        for k, x in v.items():
+        for k, x in {**DEFAULTS, **v}.items():
             if k != "stats":
                 engine.tune(k, x)
         o = os_ if v["stats"] else os_nostats

@@ -38,19 +38,29 @@ def host_batch(orc, b):
     return hb
 
 
+CV_KERNELS = (0, 1)  # qe_tune("cv_kernel"): pair kernel, stream kernel
+
+
 def check_commit_vote(eng, orc, b, goff=0):
-    stats = eng.stats_buffer(DEV)
-    out = eng.commit_vote(b, stats=stats)
-    folded = eng.stats_reduce(stats)
-    torch.cuda.synchronize()
+    """Both qe_commit_vote kernels against the oracle, bit for bit."""
     hb = host_batch(orc, b)
     commit, vote, gc, rc, ostats = orc.commit_vote(hb, goff=goff)
-    np.testing.assert_array_equal(out.commit.cpu().numpy().view(np.uint64), commit)
-    np.testing.assert_array_equal(out.vote.cpu().numpy(), vote)
-    np.testing.assert_array_equal(out.granted.cpu().numpy(), gc)
-    np.testing.assert_array_equal(out.rejected.cpu().numpy(), rc)
-    got = folded.cpu().numpy().view(np.uint64)
-    np.testing.assert_array_equal(got, ostats)
+    try:
+        for k in CV_KERNELS:
+            eng.tune("cv_kernel", k)
+            stats = eng.stats_buffer(DEV)
+            out = eng.commit_vote(b, stats=stats)
+            folded = eng.stats_reduce(stats)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.commit.cpu().numpy().view(np.uint64), commit,
+                                          err_msg=f"cv_kernel {k}")
+            np.testing.assert_array_equal(out.vote.cpu().numpy(), vote, err_msg=f"cv_kernel {k}")
+            np.testing.assert_array_equal(out.granted.cpu().numpy(), gc, err_msg=f"cv_kernel {k}")
+            np.testing.assert_array_equal(out.rejected.cpu().numpy(), rc, err_msg=f"cv_kernel {k}")
+            got = folded.cpu().numpy().view(np.uint64)
+            np.testing.assert_array_equal(got, ostats, err_msg=f"cv_kernel {k}")
+    finally:
+        eng.tune("cv_kernel", -1)
     return commit, vote
 
 
@@ -244,21 +254,29 @@ def test_full_size_config3_properties(eng, orc):
     symmetric in the halves (swap inc/out)."""
     G, S = 1 << 27, 10
     b = gpu_batch(eng, G, S, 0xC0FFEE, n_inc=5, n_out=5)
-    stats = eng.stats_buffer(DEV)
     out = eng.Outputs(G, DEV, tally=False)
-    eng.commit_vote(b, out, stats=stats)
-    got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
-    c1 = out.commit.clone()
-    b.inc, b.out = b.out, b.inc
-    eng.commit_vote(b, out)
-    assert torch.equal(c1, out.commit)
-    b.inc, b.out = b.out, b.inc
-    del c1, out
+    got = {}
+    try:
+        for k in CV_KERNELS:
+            eng.tune("cv_kernel", k)
+            stats = eng.stats_buffer(DEV)
+            eng.commit_vote(b, out, stats=stats)
+            got[k] = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+            c1 = out.commit.clone()
+            b.inc, b.out = b.out, b.inc
+            eng.commit_vote(b, out)
+            assert torch.equal(c1, out.commit), f"cv_kernel {k}"
+            b.inc, b.out = b.out, b.inc
+            del c1
+    finally:
+        eng.tune("cv_kernel", -1)
+    del out
     hb = host_batch(orc, b)
     del b
     torch.cuda.empty_cache()
     _, _, _, _, ostats = orc.commit_vote(hb)
-    np.testing.assert_array_equal(got, ostats)
+    for k in CV_KERNELS:
+        np.testing.assert_array_equal(got[k], ostats, err_msg=f"cv_kernel {k}")
 
 
 # --------------------------------------------------------------------------
