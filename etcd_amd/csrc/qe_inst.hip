@@ -26,11 +26,25 @@ int launch_cv_k(const CVArgs &a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
+// Chunk (tiles per wave): QE_STREAM_TPW on large batches; a batch too small
+// to give every CU 32 waves at that chunk gets shorter chunks (>= 2, so the
+// two-set pipeline still overlaps), trading per-wave pipelining for waves in
+// flight.  g_tiles_per_wave > 0 overrides (clamped to QE_STREAM_TPW).
 template <int MODE, bool NTL, bool NTS>
-int launch_cv_stream(const CVArgs &a, hipStream_t st) {
+int launch_cv_stream(CVArgs a, hipStream_t st) {
   auto kern = k_cv_stream<S, MODE, MT, NTL, NTS>;
   const uint64_t tiles = (a.G + 63) / 64;
-  const uint64_t per_block = (kBlock / 64) * QE_STREAM_TPW;
+  uint64_t chunk;
+  if (g_tiles_per_wave > 0) {
+    chunk = static_cast<uint64_t>(g_tiles_per_wave);
+  } else {
+    const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
+    chunk = (tiles + waves - 1) / waves;
+    if (chunk < 2) chunk = 2;
+  }
+  if (chunk > QE_STREAM_TPW) chunk = QE_STREAM_TPW;
+  a.chunk = static_cast<uint32_t>(chunk);
+  const uint64_t per_block = (kBlock / 64) * chunk;
   const uint64_t blocks = (tiles + per_block - 1) / per_block;
   if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);

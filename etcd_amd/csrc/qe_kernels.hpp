@@ -171,6 +171,7 @@ struct CVArgs {
   uint64_t *commit;
   uint8_t *vote, *gcount, *rcount;
   uint64_t *stats;
+  uint32_t chunk;  // k_cv_stream: tiles per wave, 1..QE_STREAM_TPW (set by the launcher)
 };
 
 enum { C_GROUPS, C_INF, C_SUM, C_ZERO, C_WON, C_LOST, C_PEND, C_GR, C_RJ, C_VIOL, C_CSUM, C_N };

@@ -137,8 +137,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ntiles = (a.G + 63) / 64;
-  const uint64_t t0 = (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + w) * TPW;
-  const uint32_t nt = t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < TPW ? ntiles - t0 : TPW) : 0u;
+  const uint32_t chunk = a.chunk;  // <= TPW (host-checked)
+  const uint64_t t0 = (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + w) * chunk;
+  const uint32_t nt =
+      t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < chunk ? ntiles - t0 : chunk) : 0u;
   const bool want_stats = a.stats != nullptr;
   CVStats st;
   if (nt > 0) {
