@@ -647,22 +647,11 @@ __device__ __forceinline__ void pr_store(const PArgs &a, uint64_t off, const PR 
   a.icount[off] = static_cast<uint8_t>(p.count);
 }
 
-// Inflights slot k of peer (s, g): ibuf[(s*F + k)*stride + g]
+// Inflights entry k of peer (s, g): ibuf[(s*stride + g)*F + k].  A peer's
+// ring is one contiguous F*8-byte row, so FreeLE's scan touches one HBM
+// burst per 8 entries instead of one per entry.
 __device__ __forceinline__ uint64_t *infl(const PArgs &a, uint32_t s, uint64_t g, uint32_t k) {
-  return a.ibuf + (static_cast<uint64_t>(s) * a.F + k) * a.stride + g;
-}
-
-// inflights.go:87-113 FreeLE
-__device__ __forceinline__ void infl_free_le(const PArgs &a, uint32_t s, uint64_t g, PR &p,
-                                             uint64_t to) {
-  if (p.count == 0 || to < *infl(a, s, g, p.start)) return;
-  uint32_t idx = p.start, i;
-  for (i = 0; i < p.count; i++) {
-    if (to < *infl(a, s, g, idx)) break;
-    if (++idx >= a.F) idx -= a.F;
-  }
-  p.count -= i;
-  p.start = p.count == 0 ? 0 : idx;
+  return a.ibuf + (static_cast<uint64_t>(s) * a.stride + g) * a.F + k;
 }
 
 __device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:84-90
@@ -693,23 +682,27 @@ __device__ __forceinline__ bool pr_paused(const PR &p, uint32_t F) {  // progres
   return true;
 }
 
-// raftLog.findConflictByTerm (raft/log.go:147-168) on the term-run model:
-// walking down index by index until term(index) <= t is the same as jumping
-// run by run to the end of the highest run whose term is <= t.
-__device__ __forceinline__ uint64_t find_conflict_by_term(const PArgs &a, uint64_t g, uint32_t nr,
+// raftLog.findConflictByTerm (raft/log.go:147-168) on the term-run model,
+// over the group's run table held in registers: walking down index by index
+// while term(index) > t is the same as jumping to the end of the run below,
+// run by run (term(i) = term of the highest run r with run_first[r] <= i,
+// 0 below run 0 or above lastIndex, as oracle/quorum_oracle.c orc_log_term).
+template <int RM>
+__device__ __forceinline__ uint64_t find_conflict_by_term(const uint64_t (&rf)[RM],
+                                                          const uint64_t (&rt)[RM], uint32_t nr,
                                                           uint64_t li, uint64_t index,
                                                           uint64_t t) {
   if (index > li || nr == 0) return index;
-  if (index < a.run_first[g]) return index;  // term(index) = 0 <= t
-  int r = static_cast<int>(nr) - 1;
-  while (r > 0 && a.run_first[static_cast<uint64_t>(r) * a.stride + g] > index) r--;
-  // index lies in run r
-  while (r >= 0) {
-    if (a.run_term[static_cast<uint64_t>(r) * a.stride + g] <= t) return index;
-    index = a.run_first[static_cast<uint64_t>(r) * a.stride + g] - 1;  // end of run r-1
-    r--;
+  uint64_t cur = index;
+  bool done = false;
+#pragma unroll
+  for (int r = RM - 1; r >= 0; r--) {
+    if (!done && static_cast<uint32_t>(r) < nr && rf[r] <= cur) {
+      if (rt[r] <= t) done = true;
+      else cur = rf[r] - 1;
+    }
   }
-  return index;  // below the dummy index: term 0 <= t
+  return cur;
 }
 
 template <int S, bool MASKED, bool JOINT>
@@ -723,91 +716,232 @@ __device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t i
 
 enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
 
-template <int S, typename MT, bool MASKED, bool JOINT>
+// One round of leader-side message handling, one group per lane.  The
+// reference's per-message work is a chain of dependent memory accesses
+// (message -> Progress -> Inflights scan -> log terms); here every access a
+// batch of slots needs is issued up front, in three waves of independent
+// loads, and the state machine then runs in registers:
+//   A  per group: masks, committed, termStart, lastIndex, run count; per slot:
+//      message type and Match (all slots: maybeCommit reads every Match)
+//   B  per slot of the batch that has a message: Next, PendingSnapshot,
+//      flags, Inflights start/count, m.Index (+ RejectHint/LogTerm of rejects)
+//   C  the first 8 Inflights entries of every ring FreeLE will scan, and the
+//      run table when a reject needs findConflictByTerm
+// Slots are processed in ascending order, as messages arrive in the
+// reference; batches of BS slots bound the registers held by B and C
+// (BS = 1: one slot's B and C in flight, 127 VGPRs, 4 waves per SIMD).
+#ifndef QE_RING_CHUNK
+#define QE_RING_CHUNK 8
+#endif
+#ifndef QE_PSTEP_BATCH
+#define QE_PSTEP_BATCH 1  // slots per batch: 1 measured best (occupancy 4 vs 1 at 5)
+#endif
+constexpr int kRingChunk = QE_RING_CHUNK;
+
+template <int S, typename MT, bool MASKED, bool JOINT, int RM>
 __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
-  constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr int BS = S <= QE_PSTEP_BATCH ? S : QE_PSTEP_BATCH;
+  constexpr int CH = kRingChunk;
   uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
   const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
+  const uint32_t F = a.F;
   for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
        g += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    constexpr uint32_t kFull = (1u << S) - 1u;
+    // ---- A ----
     const uint32_t mi = MASKED ? (incp[g] & kFull) : kFull;
     const uint32_t mo = JOINT ? (outp[g] & kFull) : 0u;
     const uint64_t li = a.last_index[g], ts = a.term_start[g], c0 = a.committed[g];
     const uint32_t nr = a.run_count[g] < a.R ? a.run_count[g] : a.R;
-    uint64_t c = c0;
     uint64_t vals[S];
+    uint32_t ty[S];
 #pragma unroll
-    for (int s = 0; s < S; s++) vals[s] = a.match[static_cast<uint64_t>(s) * a.stride + g];
-    uint32_t send = 0, bc = 0;
-    // Runtime loop over slots (one copy of the selection network); the
-    // register-resident match row is updated with a static select-assign.
-#pragma unroll 1
     for (int s = 0; s < S; s++) {
       const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
-      const uint32_t ty = a.mtype[off];
-      if (ty == QE_MSG_NONE || ty > QE_MSG_HEARTBEAT_RESP) continue;
-      PR p = pr_load(a, off);
-      p.recent_active = 1;
-      if (ty == QE_MSG_APP_RESP_REJECT) {
-        const uint64_t idx = a.mindex[off], lt = a.mlogterm[off];
-        uint64_t probe = a.mhint[off];
-        if (lt > 0) probe = find_conflict_by_term(a, g, nr, li, probe, lt);
-        bool decr;  // MaybeDecrTo(m.Index, probe)
-        if (p.state == QE_PR_REPLICATE) {
-          decr = idx > p.match;
-          if (decr) p.next = p.match + 1;
-        } else {
-          decr = (p.next - 1 == idx);
-          if (decr) {
-            const uint64_t m = idx < probe + 1 ? idx : probe + 1;
-            p.next = m > 1 ? m : 1;
-            p.probe_sent = 0;
-          }
-        }
-        if (decr) {
-          if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
-          send |= 1u << s;
-        }
-      } else if (ty == QE_MSG_APP_RESP) {
-        const uint64_t idx = a.mindex[off];
-        if (idx > li) {
-          cnt[P_VIOL] += 1;
-        } else {
-          const bool old_paused = pr_paused(p, a.F);
-          bool updated = false;  // MaybeUpdate
-          if (p.match < idx) {
-            p.match = idx;
-            updated = true;
-            p.probe_sent = 0;
-          }
-          if (p.next < idx + 1) p.next = idx + 1;
-          if (updated) {
-            if (p.state == QE_PR_PROBE) {
-              pr_become_replicate(p);
-            } else if (p.state == QE_PR_SNAPSHOT && p.match >= p.pending) {
-              pr_become_probe(p);
-              pr_become_replicate(p);
-            } else if (p.state == QE_PR_REPLICATE) {
-              infl_free_le(a, s, g, p, idx);
-            }
+      vals[s] = a.match[off];
+      ty[s] = a.mtype[off];
+    }
+    uint64_t rf[RM], rt[RM];
+    bool have_runs = false;
+    uint64_t c = c0;
+    uint32_t send = 0, bc = 0;
 #pragma unroll
-            for (int k = 0; k < S; k++) vals[k] = (k == s) ? p.match : vals[k];
-            const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
-            if (mci > c && mci >= ts && mci <= li) {
-              c = mci;
-              bc = 1;
-            } else if (old_paused) {
-              send |= 1u << s;
-            }
+    for (int b0 = 0; b0 < S; b0 += BS) {
+      // ---- B ----
+      uint64_t nx[BS], pd[BS], ix[BS], hn[BS], lt[BS];
+      uint32_t fl[BS], sta[BS], ct[BS];
+#pragma unroll
+      for (int j = 0; j < BS; j++) {
+        const int s = b0 + j;
+        nx[j] = pd[j] = ix[j] = hn[j] = lt[j] = 0;
+        fl[j] = sta[j] = ct[j] = 0;
+        if (s >= S) continue;
+        const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+        const uint32_t t = ty[s];
+        if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
+          nx[j] = a.next[off];
+          pd[j] = a.pending[off];
+          fl[j] = a.flags[off];
+          sta[j] = a.istart[off];
+          ct[j] = a.icount[off];
+        }
+        if (t == QE_MSG_APP_RESP || t == QE_MSG_APP_RESP_REJECT) ix[j] = a.mindex[off];
+        if (t == QE_MSG_APP_RESP_REJECT) {
+          hn[j] = a.mhint[off];
+          lt[j] = a.mlogterm[off];
+        }
+      }
+      // ---- C ----
+      bool need_runs = false;
+#pragma unroll
+      for (int j = 0; j < BS; j++)
+        if (b0 + j < S) need_runs |= ty[b0 + j] == QE_MSG_APP_RESP_REJECT && lt[j] > 0;
+      if (need_runs && !have_runs) {
+#pragma unroll
+        for (int r = 0; r < RM; r++) {
+          rf[r] = static_cast<uint32_t>(r) < nr ? a.run_first[static_cast<uint64_t>(r) * a.stride + g] : 0;
+          rt[r] = static_cast<uint32_t>(r) < nr ? a.run_term[static_cast<uint64_t>(r) * a.stride + g] : 0;
+        }
+        have_runs = true;
+      }
+      // FreeLE scans (inflights.go:87-113): an accept that raises Match of a
+      // Replicate peer frees entries <= m.Index; a heartbeat response on a
+      // full ring frees entries <= the first one (FreeFirstOne).
+      uint64_t e[BS][CH];
+      uint32_t nscan[BS];
+#pragma unroll
+      for (int j = 0; j < BS; j++) {
+        const int s = b0 + j;
+        nscan[j] = 0;
+        if (s < S) {
+          const uint32_t t = ty[s];
+          const bool repl = (fl[j] & QE_PF_STATE) == QE_PR_REPLICATE;
+          const bool acc = t == QE_MSG_APP_RESP && repl && ix[j] <= li && vals[s] < ix[j];
+          const bool hb = t == QE_MSG_HEARTBEAT_RESP && repl && ct[j] == F;
+          if (acc || hb) nscan[j] = ct[j] < CH ? ct[j] : CH;
+        }
+        const uint64_t *ring = a.ibuf + (static_cast<uint64_t>(s < S ? s : 0) * a.stride + g) * F;
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+          uint32_t pos = sta[j] + k;
+          if (pos >= F) pos -= F;
+          if (pos >= F) pos = 0;  // corrupt Inflights.start: stay inside the row
+          e[j][k] = static_cast<uint32_t>(k) < nscan[j] ? ring[pos] : 0;
+        }
+      }
+      uint32_t fr[BS];
+#pragma unroll
+      for (int j = 0; j < BS; j++) {
+        const int s = b0 + j;
+        const uint64_t to = ty[s < S ? s : 0] == QE_MSG_HEARTBEAT_RESP ? e[j][0] : ix[j];
+        uint32_t f = 0;
+        bool go = true;
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+          go = go && static_cast<uint32_t>(k) < nscan[j] && e[j][k] <= to;
+          f += go ? 1u : 0u;
+        }
+        if (f == CH && ct[j] > CH) {  // MaxInflightMsgs > 8: scan on
+          const uint64_t *ring = a.ibuf + (static_cast<uint64_t>(s) * a.stride + g) * F;
+          uint32_t pos = sta[j] + CH;
+          if (pos >= F) pos -= F;
+          if (pos >= F) pos = 0;
+          while (f < ct[j] && ring[pos] <= to) {
+            f++;
+            if (++pos >= F) pos -= F;
           }
         }
-      } else {  // QE_MSG_HEARTBEAT_RESP
-        p.probe_sent = 0;
-        if (p.state == QE_PR_REPLICATE && p.count == a.F)
-          infl_free_le(a, s, g, p, *infl(a, s, g, p.start));
-        if (p.match < li) send |= 1u << s;
+        fr[j] = f;
       }
-      pr_store(a, off, p);
+      // ---- the state machine, in message (slot) order ----
+#pragma unroll
+      for (int j = 0; j < BS; j++) {
+        const int s = b0 + j;
+        if (s >= S) continue;
+        const uint32_t t = ty[s];
+        if (t < QE_MSG_APP_RESP || t > QE_MSG_HEARTBEAT_RESP) continue;
+        const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+        PR p;
+        p.match = vals[s];
+        p.next = nx[j];
+        p.pending = pd[j];
+        p.state = fl[j] & QE_PF_STATE;
+        p.probe_sent = (fl[j] & QE_PF_PROBE_SENT) != 0;
+        p.recent_active = 1;
+        p.start = sta[j];
+        p.count = ct[j];
+        bool updated = false;
+        if (t == QE_MSG_APP_RESP_REJECT) {
+          uint64_t probe = hn[j];
+          if (lt[j] > 0) probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, lt[j]);
+          bool decr;  // MaybeDecrTo(m.Index, probe)
+          if (p.state == QE_PR_REPLICATE) {
+            decr = ix[j] > p.match;
+            if (decr) p.next = p.match + 1;
+          } else {
+            decr = (p.next - 1 == ix[j]);
+            if (decr) {
+              const uint64_t m = ix[j] < probe + 1 ? ix[j] : probe + 1;
+              p.next = m > 1 ? m : 1;
+              p.probe_sent = 0;
+            }
+          }
+          if (decr) {
+            if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
+            send |= 1u << s;
+          }
+        } else if (t == QE_MSG_APP_RESP) {
+          const uint64_t idx = ix[j];
+          if (idx > li) {
+            cnt[P_VIOL] += 1;
+          } else {
+            const bool old_paused = pr_paused(p, F);
+            if (p.match < idx) {  // MaybeUpdate
+              p.match = idx;
+              updated = true;
+              p.probe_sent = 0;
+            }
+            if (p.next < idx + 1) p.next = idx + 1;
+            if (updated) {
+              if (p.state == QE_PR_PROBE) {
+                pr_become_replicate(p);
+              } else if (p.state == QE_PR_SNAPSHOT && p.match >= p.pending) {
+                pr_become_probe(p);
+                pr_become_replicate(p);
+              } else if (p.state == QE_PR_REPLICATE && fr[j] > 0) {
+                p.count -= fr[j];
+                uint32_t st2 = p.start + fr[j];
+                if (st2 >= F) st2 -= F;
+                p.start = p.count == 0 ? 0 : st2;
+              }
+              vals[s] = p.match;
+              const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
+              if (mci > c && mci >= ts && mci <= li) {
+                c = mci;
+                bc = 1;
+              } else if (old_paused) {
+                send |= 1u << s;
+              }
+            }
+          }
+        } else {  // QE_MSG_HEARTBEAT_RESP
+          p.probe_sent = 0;
+          if (p.state == QE_PR_REPLICATE && p.count == F && fr[j] > 0) {
+            p.count -= fr[j];
+            uint32_t st2 = p.start + fr[j];
+            if (st2 >= F) st2 -= F;
+            p.start = p.count == 0 ? 0 : st2;
+          }
+          if (p.match < li) send |= 1u << s;
+        }
+        if (updated) a.match[off] = p.match;
+        a.next[off] = p.next;
+        if (p.pending != pd[j]) a.pending[off] = p.pending;
+        a.flags[off] = static_cast<uint8_t>(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
+                                            QE_PF_RECENT_ACTIVE);
+        a.istart[off] = static_cast<uint8_t>(p.start);
+        a.icount[off] = static_cast<uint8_t>(p.count);
+      }
     }
     a.committed[g] = c;
     if (a.send_mask) static_cast<MT *>(a.send_mask)[g] = static_cast<MT>(send);

@@ -257,7 +257,7 @@ def tune(key, value):
 
 class ProgressState:
     """Device-resident leader-side Progress of G groups (qe_progress):
-    match/next/pending [S][stride], flags, Inflights rings [S][F][stride],
+    match/next/pending [S][stride], flags, Inflights rings [S][stride][F],
     committed, and the leader-log model (term runs)."""
 
     def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None):

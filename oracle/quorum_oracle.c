@@ -899,8 +899,8 @@ static void pr_load(orc_pr *p, uint64_t off, uint64_t stride, uint32_t F, uint64
   p->start = istart[off];
   p->count = icount[off];
   p->size = F;
-  p->buf = ibuf + ((uint64_t)s * F) * stride + g;
-  p->bstride = stride;
+  p->buf = ibuf + ((uint64_t)s * stride + g) * F; /* ring row [S][stride][F] */
+  p->bstride = 1;
 }
 static void pr_store(const orc_pr *p, uint64_t off, uint64_t *match, uint64_t *next,
                      uint64_t *pending, uint8_t *pflags, uint8_t *istart, uint8_t *icount) {

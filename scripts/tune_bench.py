@@ -31,6 +31,7 @@ def main():
         desc, G, S, kind = bench.WORKLOADS[wl]
         stats = engine.stats_buffer(d.dev)
         step, bpu, units, _, keep = bench.setup(wl, G, S, kind, d, stats)
+        prep = keep.get("prepare") or (lambda: None)  # per-launch state restore
         variants = list(itertools.product(tpws, nts))
         res = {v: [] for v in variants}
         for _ in range(ROUNDS):
@@ -38,10 +39,12 @@ def main():
                 engine.tune("tiles_per_wave", v[0])
                 engine.tune("nontemporal", v[1])
                 for _ in range(3):
+                    prep()
                     step()
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(LAUNCHES)]
                 for a, b in ev:
+                    prep()
                     a.record()
                     step()
                     b.record()
@@ -51,7 +54,7 @@ def main():
         engine.tune("nontemporal", 3)
         for v in variants:
             ms = np.array(res[v])
-            print(f"{wl} tpw={v[0]} nt={v[1]} median {np.median(ms):.4f} ms  min {ms.min():.4f}  "
+            print(f"{os.path.basename(engine._lib.LIB_PATH)} {wl} tpw={v[0]} nt={v[1]} median {np.median(ms):.4f} ms  min {ms.min():.4f}  "
                   f"{bpu * units / np.median(ms) / 1e6:.0f} GB/s", flush=True)
         del keep
         torch.cuda.empty_cache()

@@ -49,7 +49,7 @@ def random_state(rng, G, S, F, R, masks):
     pb.istart[:] = rng.integers(0, F, n).astype(np.uint8)
     base = pb.match.copy()
     for k in range(F):
-        pb.ibuf[(np.arange(S)[:, None] * F + k) * G + np.arange(G)[None, :]] = \
+        pb.ibuf[(np.arange(S)[:, None] * G + np.arange(G)[None, :]) * F + k] = \
             (base.reshape(S, G) + 1 + 2 * ((k - pb.istart.reshape(S, G).astype(int)) % F)).astype(np.uint64)
     md = orc.mask_dtype(S)
     if "inc" in masks:
