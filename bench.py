@@ -481,7 +481,7 @@ def main():
         for name in WORKLOADS:
             if name == args.workload:
                 continue
-            r = run_workload(name, args, d, max(3, args.steps // 4), 2)
+            r = run_workload(name, args, d, max(5, args.steps // 2), max(2, args.warmup // 2))
             aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
                                            "achieved_GBs", "hbm_frac", "invariant_violations")}
     cpu = None

@@ -97,29 +97,81 @@ __device__ __forceinline__ uint64_t select_fixed(uint64_t (&v)[N]) {
 // from the top, the k-th member of a half is that half's (n/2+1)-th largest
 // acked index.  An empty half yields inf (majority.go:128-132), and the joint
 // result is the min of the halves (joint.go:49-56).
+//
+// Fast path (exact): when the group's nonzero values span less than 2^30 - 1
+// (followers of one leader ack indexes close to each other), every value maps
+// order-preservingly onto a 30-bit offset from base = max - (2^30 - 1): zero
+// -> 0, a nonzero value v -> v - base in [1, 2^30 - 1].  Key = offset << 2 |
+// payload is then a 32-bit word, and a comparator is one v_min_u32 plus one
+// v_max_u32 instead of a 64-bit compare and six selects.  Slots outside both
+// halves keep payload 0: they sort with the rest and the walk skips them.
+// Groups with a wider span take the 64-bit payload sort.
 template <int S>
-__device__ __forceinline__ uint64_t joint_committed(uint64_t (&v)[S], uint32_t inc,
-                                                    uint32_t out) {
-  uint32_t pay[S];
+__device__ __forceinline__ uint64_t joint_committed_wide(uint64_t (&v)[S], const uint32_t (&pay)[S],
+                                                         uint32_t n0, uint32_t n1) {
+  uint32_t p[S];
 #pragma unroll
-  for (int s = 0; s < S; s++) pay[s] = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
+  for (int s = 0; s < S; s++) p[s] = pay[s];
   constexpr auto net = Batcher<S>::kNet;
 #pragma unroll
   for (int c = 0; c < Batcher<S>::kSize; c++)
-    cmpx_p(v[net.e[c].a], pay[net.e[c].a], v[net.e[c].b], pay[net.e[c].b]);
-  const uint32_t n0 = popc(inc), n1 = popc(out);
+    cmpx_p(v[net.e[c].a], p[net.e[c].a], v[net.e[c].b], p[net.e[c].b]);
   const uint32_t k0 = n0 / 2 + 1, k1 = n1 / 2 + 1;
   uint32_t c0 = 0, c1 = 0;
   uint64_t r0 = n0 ? 0 : kInf, r1 = n1 ? 0 : kInf;
 #pragma unroll
-  for (int p = S - 1; p >= 0; p--) {
-    const uint32_t m0 = pay[p] & 1u, m1 = pay[p] >> 1;
+  for (int q = S - 1; q >= 0; q--) {
+    const uint32_t m0 = p[q] & 1u, m1 = p[q] >> 1;
     c0 += m0;
     c1 += m1;
-    r0 = (m0 && c0 == k0) ? v[p] : r0;
-    r1 = (m1 && c1 == k1) ? v[p] : r1;
+    r0 = (m0 && c0 == k0) ? v[q] : r0;
+    r1 = (m1 && c1 == k1) ? v[q] : r1;
   }
   return r0 < r1 ? r0 : r1;
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t joint_committed(uint64_t (&v)[S], uint32_t inc,
+                                                    uint32_t out) {
+  constexpr uint64_t kSpan = (1u << 30) - 1;
+  uint32_t pay[S];
+  uint64_t hi = 0, lo = kInf;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    pay[s] = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
+    const bool nz = v[s] != 0;
+    hi = v[s] > hi ? v[s] : hi;
+    lo = (nz && v[s] < lo) ? v[s] : lo;
+  }
+  const uint32_t n0 = popc(inc), n1 = popc(out);
+  if (hi - lo >= kSpan)  // (no nonzero value: hi - lo = 1)
+    return joint_committed_wide<S>(v, pay, n0, n1);
+  const uint64_t base = hi - kSpan;
+  uint32_t k[S];
+#pragma unroll
+  for (int s = 0; s < S; s++)
+    k[s] = v[s] != 0 ? ((static_cast<uint32_t>(v[s] - base) << 2) | pay[s]) : pay[s];
+  constexpr auto net = Batcher<S>::kNet;
+#pragma unroll
+  for (int c = 0; c < Batcher<S>::kSize; c++) {
+    const uint32_t x = k[net.e[c].a], y = k[net.e[c].b];
+    k[net.e[c].a] = x < y ? x : y;
+    k[net.e[c].b] = x < y ? y : x;
+  }
+  const uint32_t k0 = n0 / 2 + 1, k1 = n1 / 2 + 1;
+  uint32_t c0 = 0, c1 = 0, r0 = 0, r1 = 0;
+#pragma unroll
+  for (int q = S - 1; q >= 0; q--) {
+    const uint32_t m0 = k[q] & 1u, m1 = (k[q] >> 1) & 1u;
+    c0 += m0;
+    c1 += m1;
+    r0 = (m0 && c0 == k0) ? k[q] : r0;
+    r1 = (m1 && c1 == k1) ? k[q] : r1;
+  }
+  // offset 0 is the value 0; otherwise base + offset
+  const uint64_t x0 = n0 == 0 ? kInf : ((r0 >> 2) ? base + (r0 >> 2) : 0);
+  const uint64_t x1 = n1 == 0 ? kInf : ((r1 >> 2) ? base + (r1 >> 2) : 0);
+  return x0 < x1 ? x0 : x1;
 }
 
 // MajorityConfig.VoteResult over slot bitmaps (raft/quorum/majority.go:178-210).
