@@ -19,6 +19,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// MurmurHash3 32-bit finalizer (oracle/quorum_oracle.c orc_fmix32).
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
 __device__ __forceinline__ uint64_t hash4(uint64_t seed, uint64_t gid, uint32_t lane,
                                           uint32_t stream) {
   uint64_t k = (static_cast<uint64_t>(stream) << 32) | lane;

@@ -492,9 +492,11 @@ struct EArgs {
 
 enum { E_GROUPS, E_ELEC, E_LEAD, E_DOWN, E_WON, E_LOST, E_PEND, E_GR, E_RJ, E_VIOL, E_CSUM, E_N };
 
+// cnt: per-lane 32-bit step counters (flushed into 64-bit totals per chunk);
+// E_LEAD / E_DOWN equal E_WON / E_LOST and are filled in at the flush.
 __device__ __forceinline__ void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd,
                                            uint32_t gr, uint32_t gbefore, uint32_t &sta,
-                                           uint64_t (&cnt)[E_N]) {
+                                           uint32_t (&cnt)[E_N]) {
   const uint32_t voters = (mi | mo) & ~ml;
   const uint32_t gcn = popc(vd & gr & voters), rcn = popc(vd & ~gr & voters);
   const uint32_t res = joint_vote(mi, mo, vd, gr);
@@ -506,9 +508,7 @@ __device__ __forceinline__ void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml
   cnt[E_GR] += gcn;
   cnt[E_RJ] += rcn;
   cnt[E_WON] += (res == kVoteWon);
-  cnt[E_LEAD] += (res == kVoteWon);
   cnt[E_LOST] += (res == kVoteLost);
-  cnt[E_DOWN] += (res == kVoteLost);
   cnt[E_PEND] += (res == kVotePending);
   sta = res == kVoteWon ? QE_STATE_LEADER : (res == kVoteLost ? QE_STATE_FOLLOWER : sta);
 }
@@ -538,40 +538,48 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
     uint32_t vd = vdp[g] & kFull, gr = grp[g] & kFull;
     const uint32_t others = prog & ~self;
     // counter-based RNG key (oracle/quorum_oracle.c elec_gkey), once per group
-    const uint64_t gkey = mix64(a.seed + gid * kPhi) ^ 0x6A09E667F3BCC909ull;
-    for (uint32_t k = 0; promotable && k < a.steps; k++) {
-      const uint64_t step = a.step0 + k;
-      if (sta != QE_STATE_CANDIDATE) {
-        // hup -> campaign: becomeCandidate (term+1, ResetVotes), self-vote.
-        t += 1;
-        vd = self;
-        gr = self;
-        sta = QE_STATE_CANDIDATE;
-        cnt[E_ELEC] += 1;
-        elec_tally(mi, mo, ml, vd, gr, 0u, sta, cnt);
-      } else {
-        const uint64_t h = mix64(gkey + step * 0xD6E8FEB86659FD93ull);
-        uint32_t resp = 0, val = 0;
+    const uint64_t gk64 = mix64(a.seed + gid * kPhi) ^ 0x6A09E667F3BCC909ull;
+    const uint32_t gkey = static_cast<uint32_t>(gk64) ^ static_cast<uint32_t>(gk64 >> 32);
+    // 32-bit step counters per chunk of <= 2^24 steps (no overflow: at most
+    // 16 grants per step), flushed into the 64-bit totals
+    for (uint32_t k0 = 0; promotable && k0 < a.steps; k0 += (1u << 24)) {
+      const uint32_t kend = a.steps - k0 < (1u << 24) ? a.steps : k0 + (1u << 24);
+      uint32_t c32[E_N];
 #pragma unroll
-        for (int j = 0; j < (S + 1) / 2; j++) {
-          const uint64_t hs = j == 0 ? h : mix64(h + static_cast<uint64_t>(j) * kPhi);
+      for (int i = 0; i < E_N; i++) c32[i] = 0;
+      for (uint32_t k = k0; k < kend; k++) {
+        const uint64_t step = a.step0 + k;
+        if (sta != QE_STATE_CANDIDATE) {
+          // hup -> campaign: becomeCandidate (term+1, ResetVotes), self-vote.
+          t += 1;
+          vd = self;
+          gr = self;
+          sta = QE_STATE_CANDIDATE;
+          c32[E_ELEC] += 1;
+          elec_tally(mi, mo, ml, vd, gr, 0u, sta, c32);
+        } else {
+          // d = fmix32(gkey + step*C1 + s*C2) per slot (oracle elec_draw)
+          const uint32_t hb = gkey + static_cast<uint32_t>(step) * 0x9E3779B1u;
+          uint32_t resp = 0, val = 0;
 #pragma unroll
-          for (int e = 0; e < 2; e++) {
-            const int s = 2 * j + e;
-            if (s >= S) break;
-            const uint32_t d = static_cast<uint32_t>(hs >> (32 * e));
+          for (int s = 0; s < S; s++) {
+            const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u);
             const bool deliver = ((others >> s) & 1u) && (d & 0xFFFFu) >= a.p_drop;
             resp |= deliver ? (1u << s) : 0u;
             val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
           }
+          const uint32_t gbefore = popc(gr & vd & ~ml & (mi | mo));
+          const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
+          vd |= fresh;
+          gr |= fresh & val;
+          elec_tally(mi, mo, ml, vd, gr, gbefore, sta, c32);
         }
-        const uint32_t gbefore = popc(gr & vd & ~ml & (mi | mo));
-        const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
-        vd |= fresh;
-        gr |= fresh & val;
-        elec_tally(mi, mo, ml, vd, gr, gbefore, sta, cnt);
       }
-      cnt[E_GROUPS] += 1;
+      c32[E_GROUPS] = kend - k0;
+      c32[E_LEAD] = c32[E_WON];
+      c32[E_DOWN] = c32[E_LOST];
+#pragma unroll
+      for (int i = 0; i < E_N; i++) cnt[i] += c32[i];
     }
     a.term[g] = t;
     a.state[g] = static_cast<uint8_t>(sta);

@@ -495,19 +495,25 @@ static void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd, uint3
 }
 
 /* Counter-based response RNG: per group gkey = mix64(seed +
- * gid*PHI) ^ IV, per step h = mix64(gkey + step*K); slots 2j, 2j+1 take the
- * low/high 32 bits of (j == 0 ? h : mix64(h + j*PHI)), bits 0-15 the drop
- * draw and bits 16-31 the grant draw. */
-static const uint64_t ELEC_IV = 0x6A09E667F3BCC909ULL, ELEC_K = 0xD6E8FEB86659FD93ULL;
-static inline uint64_t elec_gkey(uint64_t seed, uint64_t gid) {
-  return orc_mix64(seed + gid * PHI) ^ ELEC_IV;
+ * gid*PHI) ^ IV folded to 32 bits (k = lo ^ hi); slot s at step t draws
+ * d = fmix32(k + t*C1 + s*C2) (MurmurHash3's 32-bit finalizer), bits 0-15
+ * the drop draw and bits 16-31 the grant draw. */
+static const uint64_t ELEC_IV = 0x6A09E667F3BCC909ULL;
+static const uint32_t ELEC_C1 = 0x9E3779B1u, ELEC_C2 = 0x85EBCA77u;
+static inline uint32_t elec_gkey(uint64_t seed, uint64_t gid) {
+  uint64_t k = orc_mix64(seed + gid * PHI) ^ ELEC_IV;
+  return (uint32_t)k ^ (uint32_t)(k >> 32);
 }
-static inline uint64_t elec_step_hash(uint64_t gkey, uint64_t step) {
-  return orc_mix64(gkey + step * ELEC_K);
+static inline uint32_t orc_fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
-static inline uint32_t elec_draw(uint64_t h, uint32_t s) {
-  uint64_t hs = (s >> 1) == 0 ? h : orc_mix64(h + (uint64_t)(s >> 1) * PHI);
-  return (uint32_t)(hs >> ((s & 1u) * 32));
+static inline uint32_t elec_draw(uint32_t gkey, uint64_t step, uint32_t s) {
+  return orc_fmix32(gkey + (uint32_t)step * ELEC_C1 + s * ELEC_C2);
 }
 
 void orc_election_steps_batch(uint64_t G, uint64_t goff, uint32_t S, uint64_t *term,
@@ -539,7 +545,7 @@ void orc_election_steps_batch(uint64_t G, uint64_t goff, uint32_t S, uint64_t *t
       uint64_t t = term[g];
       uint32_t sta = state[g];
       uint32_t vd = ld_mask(voted, mb, g) & full, gr = ld_mask(granted, mb, g) & full;
-      const uint64_t gkey = elec_gkey(seed, gid);
+      const uint32_t gkey = elec_gkey(seed, gid);
       for (uint32_t k = 0; k < steps && promotable; k++) {
         uint64_t step = step0 + k;
         if (sta != 1) {
@@ -552,11 +558,10 @@ void orc_election_steps_batch(uint64_t G, uint64_t goff, uint32_t S, uint64_t *t
           elec_tally(mi, mo, ml, vd, gr, 0, &sta, ls);
         } else {
           /* one round of MsgVoteResp from every other Progress peer */
-          uint64_t h = elec_step_hash(gkey, step);
           uint32_t resp = 0, val = 0;
           for (uint32_t s = 0; s < S; s++) {
             if (!((prog >> s) & 1u) || ((self >> s) & 1u)) continue;
-            uint32_t d = elec_draw(h, s);
+            uint32_t d = elec_draw(gkey, step, s);
             if ((d & 0xFFFFu) < p_drop) continue; /* dropped */
             resp |= 1u << s;
             if ((d >> 16) < p_grant) val |= 1u << s;

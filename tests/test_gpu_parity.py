@@ -195,6 +195,39 @@ def test_commit_vote_ragged_sizes(eng, orc, G):
         check_commit_vote(eng, orc, b)
 
 
+@pytest.mark.parametrize("S", [2, 5, 10, 16])
+def test_joint_key_window_boundary(eng, orc, S):
+    """joint_committed's 30-bit key fast path vs the 64-bit fallback: groups
+    whose nonzero values span exactly 2^30 - 2 (fast), 2^30 - 1 and 2^30
+    (fallback), with zeros, non-members at extreme values, ties, values near
+    2^64, and both kinds of group interleaved inside every wave."""
+    G = 64 * 40
+    rng = np.random.default_rng(4242 + S)
+    W = (1 << 30) - 1
+    md = eng.mask_np_dtype(S)
+    full = (1 << S) - 1
+    inc = rng.integers(0, 1 << S, G).astype(md)
+    out = np.where(rng.random(G) < 0.7, rng.integers(0, 1 << S, G), 0).astype(md)
+    learner = (rng.integers(0, 1 << S, G) & ~(inc.astype(np.int64) | out.astype(np.int64))
+               & full).astype(md)
+    base = rng.integers(1, 1 << 62, G, dtype=np.uint64)
+    base[rng.random(G) < 0.1] = np.uint64((1 << 64) - (1 << 31))  # near the top of u64
+    span = np.array([W - 1, W, W + 1, 0, 1, 1 << 40], np.uint64)[rng.integers(0, 6, G)]
+    m = base[None, :] + (rng.random((S, G)) * span.astype(np.float64)).astype(np.uint64)
+    # pin the extremes so the span is exact: slot 0 = min, slot S-1 = max
+    m[0] = base
+    m[S - 1] = base + span
+    m[rng.random((S, G)) < 0.15] = 0  # absent voters
+    tie = rng.random((S, G)) < 0.1
+    m[tie] = base[np.nonzero(tie)[1]]
+    m[:, rng.random(G) < 0.05] = np.uint64((1 << 64) - 1)  # all-max groups
+    voted = rng.integers(0, 1 << S, G).astype(md)
+    granted = (rng.integers(0, 1 << S, G) & voted.astype(np.int64)).astype(md)
+    b = eng.SlotBatch(G, S, DEV, masks=("inc", "out", "learner"))
+    b.load_host(m.reshape(-1), inc=inc, out=out, learner=learner, voted=voted, granted=granted)
+    check_commit_vote(eng, orc, b)
+
+
 def test_commit_vote_scalar_path_odd_stride(eng, orc):
     """stride odd -> slot rows not 16-B aligned -> scalar (non-vector) path."""
     G, S = 1001, 7
