@@ -124,7 +124,7 @@ int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
 
 template <int RM>
 static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
-  const dim3 grid(grid_for((a.G + 63) / 64, 0, 4));
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
   if (joint)
     hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM>), grid, dim3(kBlock), 0, st, a);
   else if (masked)

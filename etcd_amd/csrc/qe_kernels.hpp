@@ -726,29 +726,48 @@ enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
 
 // One round of leader-side message handling, one group per lane.  The
 // reference's per-message work is a chain of dependent memory accesses
-// (message -> Progress -> Inflights scan -> log terms); here every access a
-// batch of slots needs is issued up front, in three waves of independent
-// loads, and the state machine then runs in registers:
+// (message -> Progress -> Inflights scan -> log terms).  Here the loads are
+// grouped into stages whose addresses are known together:
 //   A  per group: masks, committed, termStart, lastIndex, run count; per slot:
 //      message type and Match (all slots: maybeCommit reads every Match)
-//   B  per slot of the batch that has a message: Next, PendingSnapshot,
-//      flags, Inflights start/count, m.Index (+ RejectHint/LogTerm of rejects)
-//   C  the first 8 Inflights entries of every ring FreeLE will scan, and the
-//      run table when a reject needs findConflictByTerm
-// Slots are processed in ascending order, as messages arrive in the
-// reference; batches of BS slots bound the registers held by B and C
-// (BS = 1: one slot's B and C in flight, 127 VGPRs, 4 waves per SIMD).
-#ifndef QE_RING_CHUNK
-#define QE_RING_CHUNK 8
-#endif
-#ifndef QE_PSTEP_BATCH
-#define QE_PSTEP_BATCH 1  // slots per batch: 1 measured best (occupancy 4 vs 1 at 5)
-#endif
-constexpr int kRingChunk = QE_RING_CHUNK;
+//   B  per slot with a message: Next, PendingSnapshot, flags, Inflights
+//      start/count, m.Index (+ RejectHint/LogTerm of a reject)
+//   C  the first 8 Inflights entries FreeLE will scan, and (once per group)
+//      the run table when a reject needs findConflictByTerm
+// and software-pipelined over the slots: slot s+1's B loads are issued
+// before slot s's C loads, so every slot after the first costs one memory
+// round trip (S + 2 in all, not 2S + 1).  The state machine runs in
+// registers, slots in ascending (message) order.
+constexpr int kRingChunk = 8;
 
+struct PB {  // stage-B registers of one slot
+  uint64_t nx, pd, ix, hn, lt;
+  uint32_t fl, st, ct;
+};
+
+__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t off, uint32_t t, PB &b) {
+  b.nx = b.pd = b.ix = b.hn = b.lt = 0;
+  b.fl = b.st = b.ct = 0;
+  if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
+    b.nx = a.next[off];
+    b.pd = a.pending[off];
+    b.fl = a.flags[off];
+    b.st = a.istart[off];
+    b.ct = a.icount[off];
+  }
+  if (t == QE_MSG_APP_RESP || t == QE_MSG_APP_RESP_REJECT) b.ix = a.mindex[off];
+  if (t == QE_MSG_APP_RESP_REJECT) {
+    b.hn = a.mhint[off];
+    b.lt = a.mlogterm[off];
+  }
+}
+
+#ifndef QE_PSTEP_WAVES
+#define QE_PSTEP_WAVES 1  // min waves per SIMD requested (VGPR budget)
+#endif
 template <int S, typename MT, bool MASKED, bool JOINT, int RM>
-__global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
-  constexpr int BS = S <= QE_PSTEP_BATCH ? S : QE_PSTEP_BATCH;
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
+                          amdgpu_waves_per_eu(QE_PSTEP_WAVES))) void k_progress_step(PArgs a) {
   constexpr int CH = kRingChunk;
   uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
   const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
@@ -773,123 +792,83 @@ __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
     bool have_runs = false;
     uint64_t c = c0;
     uint32_t send = 0, bc = 0;
+    PB cur;
+    pb_load(a, g, ty[0], cur);
 #pragma unroll
-    for (int b0 = 0; b0 < S; b0 += BS) {
-      // ---- B ----
-      uint64_t nx[BS], pd[BS], ix[BS], hn[BS], lt[BS];
-      uint32_t fl[BS], sta[BS], ct[BS];
-#pragma unroll
-      for (int j = 0; j < BS; j++) {
-        const int s = b0 + j;
-        nx[j] = pd[j] = ix[j] = hn[j] = lt[j] = 0;
-        fl[j] = sta[j] = ct[j] = 0;
-        if (s >= S) continue;
-        const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
-        const uint32_t t = ty[s];
-        if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
-          nx[j] = a.next[off];
-          pd[j] = a.pending[off];
-          fl[j] = a.flags[off];
-          sta[j] = a.istart[off];
-          ct[j] = a.icount[off];
-        }
-        if (t == QE_MSG_APP_RESP || t == QE_MSG_APP_RESP_REJECT) ix[j] = a.mindex[off];
-        if (t == QE_MSG_APP_RESP_REJECT) {
-          hn[j] = a.mhint[off];
-          lt[j] = a.mlogterm[off];
-        }
-      }
+    for (int s = 0; s < S; s++) {
+      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+      const uint32_t t = ty[s];
+      // ---- B of the next slot, in flight with this slot's C ----
+      PB nxt;
+      if (s + 1 < S) pb_load(a, off + a.stride, ty[s + 1], nxt);
       // ---- C ----
-      bool need_runs = false;
-#pragma unroll
-      for (int j = 0; j < BS; j++)
-        if (b0 + j < S) need_runs |= ty[b0 + j] == QE_MSG_APP_RESP_REJECT && lt[j] > 0;
-      if (need_runs && !have_runs) {
+      if (t == QE_MSG_APP_RESP_REJECT && cur.lt > 0 && !have_runs) {
 #pragma unroll
         for (int r = 0; r < RM; r++) {
-          rf[r] = static_cast<uint32_t>(r) < nr ? a.run_first[static_cast<uint64_t>(r) * a.stride + g] : 0;
-          rt[r] = static_cast<uint32_t>(r) < nr ? a.run_term[static_cast<uint64_t>(r) * a.stride + g] : 0;
+          const bool ld = static_cast<uint32_t>(r) < nr;
+          rf[r] = ld ? a.run_first[static_cast<uint64_t>(r) * a.stride + g] : 0;
+          rt[r] = ld ? a.run_term[static_cast<uint64_t>(r) * a.stride + g] : 0;
         }
         have_runs = true;
       }
-      // FreeLE scans (inflights.go:87-113): an accept that raises Match of a
+      // FreeLE scan (inflights.go:87-113): an accept that raises Match of a
       // Replicate peer frees entries <= m.Index; a heartbeat response on a
       // full ring frees entries <= the first one (FreeFirstOne).
-      uint64_t e[BS][CH];
-      uint32_t nscan[BS];
+      const bool repl = (cur.fl & QE_PF_STATE) == QE_PR_REPLICATE;
+      const bool acc = t == QE_MSG_APP_RESP && repl && cur.ix <= li && vals[s] < cur.ix;
+      const bool hb = t == QE_MSG_HEARTBEAT_RESP && repl && cur.ct == F;
+      const uint32_t nscan = (acc || hb) ? (cur.ct < CH ? cur.ct : CH) : 0u;
+      const uint64_t *ring = a.ibuf + off * F;
+      uint64_t e[CH];
 #pragma unroll
-      for (int j = 0; j < BS; j++) {
-        const int s = b0 + j;
-        nscan[j] = 0;
-        if (s < S) {
-          const uint32_t t = ty[s];
-          const bool repl = (fl[j] & QE_PF_STATE) == QE_PR_REPLICATE;
-          const bool acc = t == QE_MSG_APP_RESP && repl && ix[j] <= li && vals[s] < ix[j];
-          const bool hb = t == QE_MSG_HEARTBEAT_RESP && repl && ct[j] == F;
-          if (acc || hb) nscan[j] = ct[j] < CH ? ct[j] : CH;
-        }
-        const uint64_t *ring = a.ibuf + (static_cast<uint64_t>(s < S ? s : 0) * a.stride + g) * F;
-#pragma unroll
-        for (int k = 0; k < CH; k++) {
-          uint32_t pos = sta[j] + k;
-          if (pos >= F) pos -= F;
-          if (pos >= F) pos = 0;  // corrupt Inflights.start: stay inside the row
-          e[j][k] = static_cast<uint32_t>(k) < nscan[j] ? ring[pos] : 0;
-        }
+      for (int k = 0; k < CH; k++) {
+        uint32_t pos = cur.st + k;
+        if (pos >= F) pos -= F;
+        if (pos >= F) pos = 0;  // corrupt Inflights.start: stay inside the row
+        e[k] = static_cast<uint32_t>(k) < nscan ? ring[pos] : 0;
       }
-      uint32_t fr[BS];
-#pragma unroll
-      for (int j = 0; j < BS; j++) {
-        const int s = b0 + j;
-        const uint64_t to = ty[s < S ? s : 0] == QE_MSG_HEARTBEAT_RESP ? e[j][0] : ix[j];
-        uint32_t f = 0;
+      uint32_t fr = 0;
+      {
+        const uint64_t to = hb ? e[0] : cur.ix;
         bool go = true;
 #pragma unroll
         for (int k = 0; k < CH; k++) {
-          go = go && static_cast<uint32_t>(k) < nscan[j] && e[j][k] <= to;
-          f += go ? 1u : 0u;
+          go = go && static_cast<uint32_t>(k) < nscan && e[k] <= to;
+          fr += go ? 1u : 0u;
         }
-        if (f == CH && ct[j] > CH) {  // MaxInflightMsgs > 8: scan on
-          const uint64_t *ring = a.ibuf + (static_cast<uint64_t>(s) * a.stride + g) * F;
-          uint32_t pos = sta[j] + CH;
+        if (fr == CH && cur.ct > CH) {  // MaxInflightMsgs > 8: scan on
+          uint32_t pos = cur.st + CH;
           if (pos >= F) pos -= F;
           if (pos >= F) pos = 0;
-          while (f < ct[j] && ring[pos] <= to) {
-            f++;
+          while (fr < cur.ct && ring[pos] <= to) {
+            fr++;
             if (++pos >= F) pos -= F;
           }
         }
-        fr[j] = f;
       }
-      // ---- the state machine, in message (slot) order ----
-#pragma unroll
-      for (int j = 0; j < BS; j++) {
-        const int s = b0 + j;
-        if (s >= S) continue;
-        const uint32_t t = ty[s];
-        if (t < QE_MSG_APP_RESP || t > QE_MSG_HEARTBEAT_RESP) continue;
-        const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
+      // ---- the state machine for this slot's message ----
+      if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
         PR p;
         p.match = vals[s];
-        p.next = nx[j];
-        p.pending = pd[j];
-        p.state = fl[j] & QE_PF_STATE;
-        p.probe_sent = (fl[j] & QE_PF_PROBE_SENT) != 0;
+        p.next = cur.nx;
+        p.pending = cur.pd;
+        p.state = cur.fl & QE_PF_STATE;
+        p.probe_sent = (cur.fl & QE_PF_PROBE_SENT) != 0;
         p.recent_active = 1;
-        p.start = sta[j];
-        p.count = ct[j];
+        p.start = cur.st;
+        p.count = cur.ct;
         bool updated = false;
         if (t == QE_MSG_APP_RESP_REJECT) {
-          uint64_t probe = hn[j];
-          if (lt[j] > 0) probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, lt[j]);
+          uint64_t probe = cur.hn;
+          if (cur.lt > 0) probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, cur.lt);
           bool decr;  // MaybeDecrTo(m.Index, probe)
           if (p.state == QE_PR_REPLICATE) {
-            decr = ix[j] > p.match;
+            decr = cur.ix > p.match;
             if (decr) p.next = p.match + 1;
           } else {
-            decr = (p.next - 1 == ix[j]);
+            decr = (p.next - 1 == cur.ix);
             if (decr) {
-              const uint64_t m = ix[j] < probe + 1 ? ix[j] : probe + 1;
+              const uint64_t m = cur.ix < probe + 1 ? cur.ix : probe + 1;
               p.next = m > 1 ? m : 1;
               p.probe_sent = 0;
             }
@@ -899,7 +878,7 @@ __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
             send |= 1u << s;
           }
         } else if (t == QE_MSG_APP_RESP) {
-          const uint64_t idx = ix[j];
+          const uint64_t idx = cur.ix;
           if (idx > li) {
             cnt[P_VIOL] += 1;
           } else {
@@ -916,9 +895,9 @@ __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
               } else if (p.state == QE_PR_SNAPSHOT && p.match >= p.pending) {
                 pr_become_probe(p);
                 pr_become_replicate(p);
-              } else if (p.state == QE_PR_REPLICATE && fr[j] > 0) {
-                p.count -= fr[j];
-                uint32_t st2 = p.start + fr[j];
+              } else if (p.state == QE_PR_REPLICATE && fr > 0) {
+                p.count -= fr;
+                uint32_t st2 = p.start + fr;
                 if (st2 >= F) st2 -= F;
                 p.start = p.count == 0 ? 0 : st2;
               }
@@ -934,9 +913,9 @@ __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
           }
         } else {  // QE_MSG_HEARTBEAT_RESP
           p.probe_sent = 0;
-          if (p.state == QE_PR_REPLICATE && p.count == F && fr[j] > 0) {
-            p.count -= fr[j];
-            uint32_t st2 = p.start + fr[j];
+          if (p.state == QE_PR_REPLICATE && p.count == F && fr > 0) {
+            p.count -= fr;
+            uint32_t st2 = p.start + fr;
             if (st2 >= F) st2 -= F;
             p.start = p.count == 0 ? 0 : st2;
           }
@@ -944,12 +923,13 @@ __global__ __launch_bounds__(kBlock) void k_progress_step(PArgs a) {
         }
         if (updated) a.match[off] = p.match;
         a.next[off] = p.next;
-        if (p.pending != pd[j]) a.pending[off] = p.pending;
+        if (p.pending != cur.pd) a.pending[off] = p.pending;
         a.flags[off] = static_cast<uint8_t>(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
                                             QE_PF_RECENT_ACTIVE);
         a.istart[off] = static_cast<uint8_t>(p.start);
         a.icount[off] = static_cast<uint8_t>(p.count);
       }
+      if (s + 1 < S) cur = nxt;
     }
     a.committed[g] = c;
     if (a.send_mask) static_cast<MT *>(a.send_mask)[g] = static_cast<MT>(send);
