@@ -3,6 +3,7 @@
 #pragma once
 #include "qe_kernels.hpp"
 #include "qe_stream.hpp"
+#include "qe_progress.hpp"
 
 namespace qe {
 

@@ -724,228 +724,7 @@ __device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t i
 
 enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
 
-// One round of leader-side message handling, one group per lane.  The
-// reference's per-message work is a chain of dependent memory accesses
-// (message -> Progress -> Inflights scan -> log terms).  Here the loads are
-// grouped into stages whose addresses are known together:
-//   A  per group: masks, committed, termStart, lastIndex, run count; per slot:
-//      message type and Match (all slots: maybeCommit reads every Match)
-//   B  per slot with a message: Next, PendingSnapshot, flags, Inflights
-//      start/count, m.Index (+ RejectHint/LogTerm of a reject)
-//   C  the first 8 Inflights entries FreeLE will scan, and (once per group)
-//      the run table when a reject needs findConflictByTerm
-// and software-pipelined over the slots: slot s+1's B loads are issued
-// before slot s's C loads, so every slot after the first costs one memory
-// round trip (S + 2 in all, not 2S + 1).  The state machine runs in
-// registers, slots in ascending (message) order.
-constexpr int kRingChunk = 8;
-
-struct PB {  // stage-B registers of one slot
-  uint64_t nx, pd, ix, hn, lt;
-  uint32_t fl, st, ct;
-};
-
-__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t off, uint32_t t, PB &b) {
-  b.nx = b.pd = b.ix = b.hn = b.lt = 0;
-  b.fl = b.st = b.ct = 0;
-  if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
-    b.nx = a.next[off];
-    b.pd = a.pending[off];
-    b.fl = a.flags[off];
-    b.st = a.istart[off];
-    b.ct = a.icount[off];
-  }
-  if (t == QE_MSG_APP_RESP || t == QE_MSG_APP_RESP_REJECT) b.ix = a.mindex[off];
-  if (t == QE_MSG_APP_RESP_REJECT) {
-    b.hn = a.mhint[off];
-    b.lt = a.mlogterm[off];
-  }
-}
-
-#ifndef QE_PSTEP_WAVES
-#define QE_PSTEP_WAVES 1  // min waves per SIMD requested (VGPR budget)
-#endif
-template <int S, typename MT, bool MASKED, bool JOINT, int RM>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
-                          amdgpu_waves_per_eu(QE_PSTEP_WAVES))) void k_progress_step(PArgs a) {
-  constexpr int CH = kRingChunk;
-  uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
-  const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
-  const uint32_t F = a.F;
-  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
-       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    constexpr uint32_t kFull = (1u << S) - 1u;
-    // ---- A ----
-    const uint32_t mi = MASKED ? (incp[g] & kFull) : kFull;
-    const uint32_t mo = JOINT ? (outp[g] & kFull) : 0u;
-    const uint64_t li = a.last_index[g], ts = a.term_start[g], c0 = a.committed[g];
-    const uint32_t nr = a.run_count[g] < a.R ? a.run_count[g] : a.R;
-    uint64_t vals[S];
-    uint32_t ty[S];
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
-      vals[s] = a.match[off];
-      ty[s] = a.mtype[off];
-    }
-    uint64_t rf[RM], rt[RM];
-    bool have_runs = false;
-    uint64_t c = c0;
-    uint32_t send = 0, bc = 0;
-    PB cur;
-    pb_load(a, g, ty[0], cur);
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
-      const uint32_t t = ty[s];
-      // ---- B of the next slot, in flight with this slot's C ----
-      PB nxt;
-      if (s + 1 < S) pb_load(a, off + a.stride, ty[s + 1], nxt);
-      // ---- C ----
-      if (t == QE_MSG_APP_RESP_REJECT && cur.lt > 0 && !have_runs) {
-#pragma unroll
-        for (int r = 0; r < RM; r++) {
-          const bool ld = static_cast<uint32_t>(r) < nr;
-          rf[r] = ld ? a.run_first[static_cast<uint64_t>(r) * a.stride + g] : 0;
-          rt[r] = ld ? a.run_term[static_cast<uint64_t>(r) * a.stride + g] : 0;
-        }
-        have_runs = true;
-      }
-      // FreeLE scan (inflights.go:87-113): an accept that raises Match of a
-      // Replicate peer frees entries <= m.Index; a heartbeat response on a
-      // full ring frees entries <= the first one (FreeFirstOne).
-      const bool repl = (cur.fl & QE_PF_STATE) == QE_PR_REPLICATE;
-      const bool acc = t == QE_MSG_APP_RESP && repl && cur.ix <= li && vals[s] < cur.ix;
-      const bool hb = t == QE_MSG_HEARTBEAT_RESP && repl && cur.ct == F;
-      const uint32_t nscan = (acc || hb) ? (cur.ct < CH ? cur.ct : CH) : 0u;
-      const uint64_t *ring = a.ibuf + off * F;
-      uint64_t e[CH];
-#pragma unroll
-      for (int k = 0; k < CH; k++) {
-        uint32_t pos = cur.st + k;
-        if (pos >= F) pos -= F;
-        if (pos >= F) pos = 0;  // corrupt Inflights.start: stay inside the row
-        e[k] = static_cast<uint32_t>(k) < nscan ? ring[pos] : 0;
-      }
-      uint32_t fr = 0;
-      {
-        const uint64_t to = hb ? e[0] : cur.ix;
-        bool go = true;
-#pragma unroll
-        for (int k = 0; k < CH; k++) {
-          go = go && static_cast<uint32_t>(k) < nscan && e[k] <= to;
-          fr += go ? 1u : 0u;
-        }
-        if (fr == CH && cur.ct > CH) {  // MaxInflightMsgs > 8: scan on
-          uint32_t pos = cur.st + CH;
-          if (pos >= F) pos -= F;
-          if (pos >= F) pos = 0;
-          while (fr < cur.ct && ring[pos] <= to) {
-            fr++;
-            if (++pos >= F) pos -= F;
-          }
-        }
-      }
-      // ---- the state machine for this slot's message ----
-      if (t >= QE_MSG_APP_RESP && t <= QE_MSG_HEARTBEAT_RESP) {
-        PR p;
-        p.match = vals[s];
-        p.next = cur.nx;
-        p.pending = cur.pd;
-        p.state = cur.fl & QE_PF_STATE;
-        p.probe_sent = (cur.fl & QE_PF_PROBE_SENT) != 0;
-        p.recent_active = 1;
-        p.start = cur.st;
-        p.count = cur.ct;
-        bool updated = false;
-        if (t == QE_MSG_APP_RESP_REJECT) {
-          uint64_t probe = cur.hn;
-          if (cur.lt > 0) probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, cur.lt);
-          bool decr;  // MaybeDecrTo(m.Index, probe)
-          if (p.state == QE_PR_REPLICATE) {
-            decr = cur.ix > p.match;
-            if (decr) p.next = p.match + 1;
-          } else {
-            decr = (p.next - 1 == cur.ix);
-            if (decr) {
-              const uint64_t m = cur.ix < probe + 1 ? cur.ix : probe + 1;
-              p.next = m > 1 ? m : 1;
-              p.probe_sent = 0;
-            }
-          }
-          if (decr) {
-            if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
-            send |= 1u << s;
-          }
-        } else if (t == QE_MSG_APP_RESP) {
-          const uint64_t idx = cur.ix;
-          if (idx > li) {
-            cnt[P_VIOL] += 1;
-          } else {
-            const bool old_paused = pr_paused(p, F);
-            if (p.match < idx) {  // MaybeUpdate
-              p.match = idx;
-              updated = true;
-              p.probe_sent = 0;
-            }
-            if (p.next < idx + 1) p.next = idx + 1;
-            if (updated) {
-              if (p.state == QE_PR_PROBE) {
-                pr_become_replicate(p);
-              } else if (p.state == QE_PR_SNAPSHOT && p.match >= p.pending) {
-                pr_become_probe(p);
-                pr_become_replicate(p);
-              } else if (p.state == QE_PR_REPLICATE && fr > 0) {
-                p.count -= fr;
-                uint32_t st2 = p.start + fr;
-                if (st2 >= F) st2 -= F;
-                p.start = p.count == 0 ? 0 : st2;
-              }
-              vals[s] = p.match;
-              const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
-              if (mci > c && mci >= ts && mci <= li) {
-                c = mci;
-                bc = 1;
-              } else if (old_paused) {
-                send |= 1u << s;
-              }
-            }
-          }
-        } else {  // QE_MSG_HEARTBEAT_RESP
-          p.probe_sent = 0;
-          if (p.state == QE_PR_REPLICATE && p.count == F && fr > 0) {
-            p.count -= fr;
-            uint32_t st2 = p.start + fr;
-            if (st2 >= F) st2 -= F;
-            p.start = p.count == 0 ? 0 : st2;
-          }
-          if (p.match < li) send |= 1u << s;
-        }
-        if (updated) a.match[off] = p.match;
-        a.next[off] = p.next;
-        if (p.pending != cur.pd) a.pending[off] = p.pending;
-        a.flags[off] = static_cast<uint8_t>(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
-                                            QE_PF_RECENT_ACTIVE);
-        a.istart[off] = static_cast<uint8_t>(p.start);
-        a.icount[off] = static_cast<uint8_t>(p.count);
-      }
-      if (s + 1 < S) cur = nxt;
-    }
-    a.committed[g] = c;
-    if (a.send_mask) static_cast<MT *>(a.send_mask)[g] = static_cast<MT>(send);
-    if (a.bcast) a.bcast[g] = static_cast<uint8_t>(bc);
-    cnt[P_GROUPS] += 1;
-    cnt[P_SUM] += c;
-    cnt[P_ADV] += (c != c0);
-    const uint64_t tag = (static_cast<uint64_t>(send) << 40) | (static_cast<uint64_t>(bc) << 62);
-    cnt[P_CSUM] += mix64(((a.goff + g) * kPhi) ^ c ^ tag);
-  }
-  if (a.stats) {
-    const int idx[P_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
-                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
-    block_stats_add<P_N, kBlock>(cnt, idx, a.stats);
-  }
-}
+// k_progress_step: qe_progress.hpp
 
 template <int S, typename MT>
 __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
