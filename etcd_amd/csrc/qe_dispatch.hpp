@@ -4,6 +4,7 @@
 #include "qe_kernels.hpp"
 #include "qe_stream.hpp"
 #include "qe_progress.hpp"
+#include "qe_repl.hpp"
 
 namespace qe {
 

@@ -102,8 +102,45 @@ static int launch_repl(const RArgs &a, hipStream_t st) {
   return launch_repl_k<J, M, V, false>(a, st);
 }
 
+// Stream replication kernel (qe_repl.hpp); chunking as launch_cv_stream.
+template <bool M, bool J, bool NTL, bool NTS>
+static int launch_repl_stream(RArgs a, hipStream_t st) {
+  auto kern = k_repl_stream<S, M, J, MT, NTL, NTS>;
+  const uint64_t tiles = (a.G + 63) / 64;
+  uint64_t chunk;
+  if (g_tiles_per_wave > 0) {
+    chunk = static_cast<uint64_t>(g_tiles_per_wave);
+  } else {
+    const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
+    chunk = (tiles + waves - 1) / waves;
+    if (chunk < 2) chunk = 2;
+  }
+  if (chunk > QE_STREAM_TPW) chunk = QE_STREAM_TPW;
+  a.chunk = static_cast<uint32_t>(chunk);
+  const uint64_t per_block = (kBlock / 64) * chunk;
+  const uint64_t blocks = (tiles + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
+template <bool M, bool J>
+static int launch_repl_s(const RArgs &a, hipStream_t st) {
+  switch (g_nontemporal & 3) {
+    case 1: return launch_repl_stream<M, J, true, false>(a, st);
+    case 2: return launch_repl_stream<M, J, false, true>(a, st);
+    case 3: return launch_repl_stream<M, J, true, true>(a, st);
+    default: return launch_repl_stream<M, J, false, false>(a, st);
+  }
+}
+
 int QE_CAT(dispatch_repl_, QE_S)(const RArgs &a, bool masked, bool joint, bool vec,
                                  hipStream_t st) {
+  if (g_repl_kernel != 0) {  // default: stream kernel (no alignment requirement)
+    if (joint) return launch_repl_s<true, true>(a, st);
+    if (masked) return launch_repl_s<true, false>(a, st);
+    return launch_repl_s<false, false>(a, st);
+  }
   if (vec) {
     if (joint) return launch_repl<true, true, true>(a, st);
     if (masked) return launch_repl<false, true, true>(a, st);

@@ -28,6 +28,7 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 extern int g_blocks_per_cu;
 extern int g_nontemporal;  // bit 0: loads, bit 1: stores
 extern int g_cv_kernel;    // qe_commit_vote: 0 pair kernel, 1 stream kernel, -1 default
+extern int g_repl_kernel;  // qe_replication_round: 0 pair kernel, 1 stream kernel, -1 default
 
 inline int num_cus() {
   static int cached[64] = {0};
@@ -379,6 +380,7 @@ struct RArgs {
   const void *inc, *out, *resp_mask, *read_acks;
   uint8_t *read_ok, *adv;
   uint64_t *stats;
+  uint32_t chunk;  // k_repl_stream: tiles per wave chunk
 };
 
 enum { R_GROUPS, R_SUM, R_ADV, R_READ, R_VIOL, R_CSUM, R_N };
