@@ -28,7 +28,7 @@ DOMINANT = {
     "config2_n5": "void qe::k_cv_stream<5, 0,",
     "config2_n7": "void qe::k_cv_stream<7, 0,",
     "config3_joint": "void qe::k_cv_stream<10, 2,",  # bucketed + rotated runs share it
-    "config4_repl": "void qe::k_replication<5,",
+    "config4_repl": "void qe::k_repl_stream<5,",
     "config5_elec": "void qe::k_election<5,",
     "progress_step": "void qe::k_progress_step<5,",
 }
