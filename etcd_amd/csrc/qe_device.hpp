@@ -106,16 +106,8 @@ __device__ __forceinline__ uint64_t select_fixed(uint64_t (&v)[N]) {
 // (bit0: member of JointConfig[0], bit1: member of JointConfig[1]); walking
 // from the top, the k-th member of a half is that half's (n/2+1)-th largest
 // acked index.  An empty half yields inf (majority.go:128-132), and the joint
-// result is the min of the halves (joint.go:49-56).
-//
-// Fast path (exact): when the group's nonzero values span less than 2^30 - 1
-// (followers of one leader ack indexes close to each other), every value maps
-// order-preservingly onto a 30-bit offset from base = max - (2^30 - 1): zero
-// -> 0, a nonzero value v -> v - base in [1, 2^30 - 1].  Key = offset << 2 |
-// payload is then a 32-bit word, and a comparator is one v_min_u32 plus one
-// v_max_u32 instead of a 64-bit compare and six selects.  Slots outside both
-// halves keep payload 0: they sort with the rest and the walk skips them.
-// Groups with a wider span take the 64-bit payload sort.
+// result is the min of the halves (joint.go:49-56).  This is the general
+// (64-bit) path.
 template <int S>
 __device__ __forceinline__ uint64_t joint_committed_wide(uint64_t (&v)[S], const uint32_t (&pay)[S],
                                                          uint32_t n0, uint32_t n1) {
@@ -140,48 +132,111 @@ __device__ __forceinline__ uint64_t joint_committed_wide(uint64_t (&v)[S], const
   return r0 < r1 ? r0 : r1;
 }
 
+// Fast path (exact): when every nonzero value of the group shares bits 29..63
+// (followers of one leader ack indexes close to each other; checked as "same
+// high word and same bits 29..60" with two 32-bit maxima), a nonzero value
+// v maps order-preservingly onto the 30-bit offset (v & (2^29 - 1)) | 2^29
+// and zero onto offset 0.  Key = offset << 2 | payload is a 32-bit word, and
+// a comparator is one v_min_u32 plus one v_max_u32 instead of a 64-bit
+// compare and six selects.  Slots outside both halves keep payload 0: they
+// sort with the rest and are never selected.  Groups whose nonzero values
+// differ above bit 28 take the 64-bit payload sort.
+//
+// Selection without a walk: after the sort, the payload bits of all S
+// positions are gathered into one word P (one v_alignbit per position).  The
+// k-th largest member of a half with n members is its (n-k+1)-th member from
+// the bottom, i.e. the lowest set bit of the half's membership bits after
+// clearing the n-k = (n-1)/2 lowest ones.  Keys ascend with position, so
+// min(CI(half 0), CI(half 1)) (joint.go:49-56) is the key at the lower of the
+// two positions: the lowest set bit of the OR of both cleared masks.  An
+// empty half contributes no bit (its CommittedIndex is inf,
+// majority.go:128-132); both empty gives inf.
+
+// k[q] for a per-lane index q < S: a binary select tree over q's bits.
+template <int S>
+__device__ __forceinline__ uint32_t pick_lane(const uint32_t (&k)[S], uint32_t q) {
+  uint32_t c[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) c[i] = k[i];
+  int n = S;
+#pragma unroll
+  for (int bit = 0; (1 << bit) < S; bit++) {
+    // all-ones where q has this bit: one v_bfi_b32 per pair (a select on a
+    // compare would be folded back into an index compare chain)
+    const uint32_t m = 0u - ((q >> bit) & 1u);
+#pragma unroll
+    for (int i = 0; i < (n + 1) / 2; i++)
+      c[i] = 2 * i + 1 < n ? ((c[2 * i + 1] & m) | (c[2 * i] & ~m)) : c[2 * i];
+    n = (n + 1) / 2;
+  }
+  return c[0];
+}
+
+// Clears the d lowest set bits of x, for d <= DMAX.
+template <int DMAX>
+__device__ __forceinline__ uint32_t clear_low_bits(uint32_t x, uint32_t d) {
+#pragma unroll
+  for (int i = 0; i < DMAX; i++) x = static_cast<uint32_t>(i) < d ? (x & (x - 1u)) : x;
+  return x;
+}
+
 template <int S>
 __device__ __forceinline__ uint64_t joint_committed(uint64_t (&v)[S], uint32_t inc,
                                                     uint32_t out) {
-  constexpr uint64_t kSpan = (1u << 30) - 1;
-  uint32_t pay[S];
-  uint64_t hi = 0, lo = kInf;
+  static_assert(S >= 1 && S <= 16, "slot count");
+  constexpr uint32_t kM = (1u << 29) - 1u;
+  // every nonzero value must share its high word and bits 29..60 with the
+  // maxima of those fields over the group (zeros never raise a maximum)
+  uint32_t y[S];
+  uint32_t hmax = 0, ymax = 0;
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    pay[s] = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
-    const bool nz = v[s] != 0;
-    hi = v[s] > hi ? v[s] : hi;
-    lo = (nz && v[s] < lo) ? v[s] : lo;
+    const uint32_t lo = static_cast<uint32_t>(v[s]), hi = static_cast<uint32_t>(v[s] >> 32);
+    y[s] = __builtin_amdgcn_alignbit(hi, lo, 29);  // bits 29..60 of v
+    ymax = y[s] > ymax ? y[s] : ymax;
+    hmax = hi > hmax ? hi : hmax;
   }
-  const uint32_t n0 = popc(inc), n1 = popc(out);
-  if (hi - lo >= kSpan)  // (no nonzero value: hi - lo = 1)
-    return joint_committed_wide<S>(v, pay, n0, n1);
-  const uint64_t base = hi - kSpan;
-  uint32_t k[S];
+  bool fast = true;
 #pragma unroll
   for (int s = 0; s < S; s++)
-    k[s] = v[s] != 0 ? ((static_cast<uint32_t>(v[s] - base) << 2) | pay[s]) : pay[s];
+    fast &= ((y[s] == ymax) & (static_cast<uint32_t>(v[s] >> 32) == hmax)) | (v[s] == 0);
+  const uint32_t n0 = popc(inc), n1 = popc(out);
+  if (!fast) {
+    uint32_t pay[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) pay[s] = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
+    return joint_committed_wide<S>(v, pay, n0, n1);
+  }
+  uint32_t k[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const uint32_t pay = ((inc >> s) & 1u) | (((out >> s) & 1u) << 1);
+    const uint32_t off = v[s] != 0 ? ((static_cast<uint32_t>(v[s]) & kM) | (1u << 29)) : 0u;
+    k[s] = (off << 2) | pay;
+  }
   constexpr auto net = Batcher<S>::kNet;
 #pragma unroll
   for (int c = 0; c < Batcher<S>::kSize; c++) {
-    const uint32_t x = k[net.e[c].a], y = k[net.e[c].b];
-    k[net.e[c].a] = x < y ? x : y;
-    k[net.e[c].b] = x < y ? y : x;
+    const uint32_t x = k[net.e[c].a], yv = k[net.e[c].b];
+    k[net.e[c].a] = x < yv ? x : yv;
+    k[net.e[c].b] = x < yv ? yv : x;
   }
-  const uint32_t k0 = n0 / 2 + 1, k1 = n1 / 2 + 1;
-  uint32_t c0 = 0, c1 = 0, r0 = 0, r1 = 0;
+  // position q's payload lands at bits B + 2q, B + 2q + 1
+  constexpr int B = 32 - 2 * S;
+  uint32_t P = 0;
 #pragma unroll
-  for (int q = S - 1; q >= 0; q--) {
-    const uint32_t m0 = k[q] & 1u, m1 = (k[q] >> 1) & 1u;
-    c0 += m0;
-    c1 += m1;
-    r0 = (m0 && c0 == k0) ? k[q] : r0;
-    r1 = (m1 && c1 == k1) ? k[q] : r1;
-  }
-  // offset 0 is the value 0; otherwise base + offset
-  const uint64_t x0 = n0 == 0 ? kInf : ((r0 >> 2) ? base + (r0 >> 2) : 0);
-  const uint64_t x1 = n1 == 0 ? kInf : ((r1 >> 2) ? base + (r1 >> 2) : 0);
-  return x0 < x1 ? x0 : x1;
+  for (int q = 0; q < S; q++) P = __builtin_amdgcn_alignbit(k[q], P, 2);
+  const uint32_t h0 = P & 0x55555555u, h1 = (P >> 1) & 0x55555555u;
+  constexpr int DMAX = (S - 1) / 2;
+  const uint32_t x0 = clear_low_bits<DMAX>(h0, (n0 - 1u) >> 1);
+  const uint32_t x1 = clear_low_bits<DMAX>(h1, (n1 - 1u) >> 1);
+  const uint32_t x = x0 | x1;
+  if (x == 0) return kInf;  // both halves empty
+  const uint32_t q = (static_cast<uint32_t>(__builtin_ctz(x)) - B) >> 1;
+  const uint32_t off = pick_lane<S>(k, q) >> 2;
+  if (off == 0) return 0;
+  const uint32_t lo = (ymax << 29) | (off & kM);
+  return (static_cast<uint64_t>(hmax) << 32) | lo;
 }
 
 // MajorityConfig.VoteResult over slot bitmaps (raft/quorum/majority.go:178-210).

@@ -197,9 +197,8 @@ def test_commit_vote_ragged_sizes(eng, orc, G):
 
 @pytest.mark.parametrize("S", [2, 5, 10, 16])
 def test_joint_key_window_boundary(eng, orc, S):
-    """joint_committed's 30-bit key fast path vs the 64-bit fallback: groups
-    whose nonzero values span exactly 2^30 - 2 (fast), 2^30 - 1 and 2^30
-    (fallback), with zeros, non-members at extreme values, ties, values near
+    """joint_committed's 32-bit key fast path vs the 64-bit fallback on
+    random spans around 2^30, with zeros, non-members at extreme values, ties, values near
     2^64, and both kinds of group interleaved inside every wave."""
     G = 64 * 40
     rng = np.random.default_rng(4242 + S)
@@ -223,6 +222,41 @@ def test_joint_key_window_boundary(eng, orc, S):
     m[:, rng.random(G) < 0.05] = np.uint64((1 << 64) - 1)  # all-max groups
     voted = rng.integers(0, 1 << S, G).astype(md)
     granted = (rng.integers(0, 1 << S, G) & voted.astype(np.int64)).astype(md)
+    b = eng.SlotBatch(G, S, DEV, masks=("inc", "out", "learner"))
+    b.load_host(m.reshape(-1), inc=inc, out=out, learner=learner, voted=voted, granted=granted)
+    check_commit_vote(eng, orc, b)
+
+
+@pytest.mark.parametrize("S", [2, 5, 10, 16])
+def test_joint_key_prefix_boundary(eng, orc, S):
+    """joint_committed's fast path needs every nonzero value to share bits
+    29..63.  Groups sit just below, on and across a 2^29 block edge, across
+    a 2^32 edge (same bits 29..60, different high word) and across a 2^61
+    edge, so both paths and every kind of prefix mismatch occur inside each
+    wave; values inside one block exercise offset 0 (the block's first
+    value) next to absent (0) voters."""
+    G = 64 * 48
+    rng = np.random.default_rng(9191 + S)
+    md = eng.mask_np_dtype(S)
+    full = (1 << S) - 1
+    inc = rng.integers(0, 1 << S, G).astype(md)
+    out = np.where(rng.random(G) < 0.7, rng.integers(0, 1 << S, G), 0).astype(md)
+    B = np.uint64(1 << 29)
+    blk = rng.integers(0, 1 << 34, G, dtype=np.uint64) * B  # a 2^29-aligned block start
+    edge = np.array([1 << 29, 1 << 32, 1 << 61, 1 << 63], np.uint64)[rng.integers(0, 4, G)]
+    blk = np.where(rng.random(G) < 0.5, blk, (blk // edge) * edge)  # on a larger edge
+    kind = rng.integers(0, 4, G)
+    lo = np.where(kind == 0, blk, np.where(kind == 1, blk + B - np.uint64(1),
+                                            blk - np.uint64(3)))  # kind 2/3 straddle
+    lo = np.where(lo == 0, np.uint64(1), lo)
+    width = np.where(kind == 1, 1, np.where(kind == 0, (1 << 29) - 1, 7)).astype(np.uint64)
+    m = lo[None, :] + (rng.random((S, G)) * width.astype(np.float64)).astype(np.uint64)
+    m[0] = lo
+    m[rng.random((S, G)) < 0.15] = 0
+    voted = rng.integers(0, 1 << S, G).astype(md)
+    granted = (rng.integers(0, 1 << S, G) & voted.astype(np.int64)).astype(md)
+    learner = (rng.integers(0, 1 << S, G) & ~(inc.astype(np.int64) | out.astype(np.int64))
+               & full).astype(md)
     b = eng.SlotBatch(G, S, DEV, masks=("inc", "out", "learner"))
     b.load_host(m.reshape(-1), inc=inc, out=out, learner=learner, voted=voted, granted=granted)
     check_commit_vote(eng, orc, b)
