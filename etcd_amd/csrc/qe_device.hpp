@@ -239,6 +239,33 @@ __device__ __forceinline__ uint64_t joint_committed(uint64_t (&v)[S], uint32_t i
   return (static_cast<uint64_t>(hmax) << 32) | lo;
 }
 
+// joint_committed over the first `top` slots only, where `top` is
+// wave-uniform and no lane of the wave has a voter in slots >= top (the
+// shape-bucketed layout puts every voter in the low slots).
+// The smaller network is picked with a scalar branch; slots >= top hold
+// only absent, non-member values, which never change a result.
+template <int S, int N>
+__device__ __forceinline__ uint64_t joint_committed_first(const uint64_t (&v)[S], uint32_t inc,
+                                                          uint32_t out) {
+  uint64_t w[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) w[i] = v[i];
+  return joint_committed<N>(w, inc, out);
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t joint_committed_top(uint64_t (&v)[S], uint32_t inc,
+                                                        uint32_t out, uint32_t top) {
+  if constexpr (S >= 6) {
+    if (top <= S - 5) return joint_committed_first<S, S - 5>(v, inc, out);
+    if (top <= S - 4) return joint_committed_first<S, S - 4>(v, inc, out);
+    if (top <= S - 3) return joint_committed_first<S, S - 3>(v, inc, out);
+    if (top <= S - 2) return joint_committed_first<S, S - 2>(v, inc, out);
+    if (top <= S - 1) return joint_committed_first<S, S - 1>(v, inc, out);
+  }
+  return joint_committed<S>(v, inc, out);
+}
+
 // MajorityConfig.VoteResult over slot bitmaps (raft/quorum/majority.go:178-210).
 __device__ __forceinline__ uint32_t majority_vote(uint32_t member, uint32_t voted,
                                                   uint32_t granted) {

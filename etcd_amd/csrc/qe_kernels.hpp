@@ -181,7 +181,7 @@ template <int S, int MODE>
 __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint32_t out,
                                            uint32_t learner, uint32_t voted, uint32_t granted,
                                            uint64_t &commit, uint32_t &vote, uint32_t &gc,
-                                           uint32_t &rc) {
+                                           uint32_t &rc, uint32_t top = S) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   if constexpr (MODE == 0) {
     commit = select_fixed<S>(v);
@@ -189,7 +189,7 @@ __device__ __forceinline__ void eval_group(uint64_t (&v)[S], uint32_t inc, uint3
     out = 0;
   } else {
     if constexpr (MODE == 1) out = 0;
-    commit = joint_committed<S>(v, inc, out);
+    commit = joint_committed_top<S>(v, inc, out, top);
   }
   vote = joint_vote(inc, out, voted, granted);
   const uint32_t voters = (inc | out) & ~learner;

@@ -45,8 +45,8 @@ __device__ __forceinline__ void rs_issue(const RArgs &a, uint64_t t, uint32_t la
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const uint64_t row = static_cast<uint64_t>(s) * a.stride + tile0;
-    const uint32_t om = ((need_m >> s) & 1u) ? off : kOOB;
-    const uint32_t orr = ((rm >> s) & 1u) ? off : kOOB;
+    const uint32_t om = bit_off(need_m, s, off);
+    const uint32_t orr = bit_off(rm, s, off);
     x.m[s] = __builtin_bit_cast(
         uint64_t, __builtin_amdgcn_raw_buffer_load_b64(mk_rsrc(a.match + row, n * 8), om, 0, aux));
     x.n[s] = __builtin_bit_cast(

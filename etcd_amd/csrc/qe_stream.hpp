@@ -21,6 +21,13 @@ namespace qe {
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t kOOB = 0x80000000u;  // > any num_records used here: load returns 0
 
+// off when bit s of mask is set, else off | kOOB (dropped by the bounds
+// check): a shift and one v_and_or_b32 instead of a compare and a select.
+// off < 2^31.
+__device__ __forceinline__ uint32_t bit_off(uint32_t mask, int s, uint32_t off) {
+  return ((~mask << (31 - s)) & kOOB) | off;
+}
+
 __device__ __forceinline__ rsrc_t mk_rsrc(const void *p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, static_cast<int>(bytes),
                                            0x00020000);
@@ -72,7 +79,7 @@ __device__ __forceinline__ void st_issue(const CVArgs &a, uint64_t t, uint32_t l
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const rsrc_t r = mk_rsrc(a.match + s * a.stride + tile0, n * 8);
-    const uint32_t o = (MODE == 0 || ((use >> s) & 1u)) ? off : kOOB;
+    const uint32_t o = MODE == 0 ? off : bit_off(use, s, off);
     v[s] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, NTL ? 2 : 0));
   }
   const MT *lp = static_cast<const MT *>(a.learner), *vp = static_cast<const MT *>(a.voted);
@@ -84,8 +91,8 @@ __device__ __forceinline__ void st_issue(const CVArgs &a, uint64_t t, uint32_t l
 
 template <int S, int MODE, bool NTS>
 __device__ __forceinline__ void st_finish(const CVArgs &a, uint64_t t, uint32_t lane,
-                                          bool want_stats, uint32_t mio, uint64_t (&v)[S],
-                                          const STile &x, CVStats &st) {
+                                          bool want_stats, uint32_t mio, uint32_t top,
+                                          uint64_t (&v)[S], const STile &x, CVStats &st) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   const uint64_t tile0 = t * 64;
   const uint32_t n = tile_n(a.G, t);
@@ -94,7 +101,7 @@ __device__ __forceinline__ void st_finish(const CVArgs &a, uint64_t t, uint32_t 
   const uint32_t lrn = x.lrn & kFull, vv = x.vd & kFull, gg = x.gr & kFull;
   uint64_t c;
   uint32_t vt, gc, rc;
-  eval_group<S, MODE>(v, inc, out, lrn, vv, gg, c, vt, gc, rc);
+  eval_group<S, MODE>(v, inc, out, lrn, vv, gg, c, vt, gc, rc, top);
   if (want_stats && lane < n) {
     st.groups += 1;
     st.inf += (c == kInf);
@@ -143,6 +150,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
       t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < chunk ? ntiles - t0 : chunk) : 0u;
   const bool want_stats = a.stats != nullptr;
   CVStats st;
+  uint32_t top = S;
   if (nt > 0) {
     // ---- stage the chunk's voter masks in LDS (one exposed latency per chunk) ----
     if constexpr (MODE >= 1) {
@@ -155,8 +163,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
         if constexpr (MODE == 2) m |= bld_mask<MT>(a.out, tile0, n, lane) << 16;
         mv[k] = m;
       }
+      uint32_t any = 0;
 #pragma unroll
-      for (int k = 0; k < TPW; k++) lds_m[w][k][lane] = mv[k];
+      for (int k = 0; k < TPW; k++) {
+        lds_m[w][k][lane] = mv[k];
+        any |= mv[k];
+      }
+      // slots >= top hold no voter of any group in the chunk (wave-uniform)
+      top = 32u - __builtin_clz(wave_or((any | (any >> 16)) & 0xFFFFu) | 1u);
     }
     auto use_of = [&](uint32_t k) -> uint32_t {
       if constexpr (MODE == 0) return 0u;
@@ -179,10 +193,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
       // tile k from set A while tile k+1 streams into set B, then swap
       st_issue<S, MODE, MT, NTL>(a, tix(k + 1), lane, use_of((k + 1) % TPW), vb, xb);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compute
-      st_finish<S, MODE, NTS>(a, tix(k), lane, want_stats, mio_of(k), va, xa, st);
+      st_finish<S, MODE, NTS>(a, tix(k), lane, want_stats, mio_of(k), top, va, xa, st);
       st_issue<S, MODE, MT, NTL>(a, tix(k + 2), lane, use_of((k + 2) % TPW), va, xa);
       __builtin_amdgcn_sched_barrier(0);
-      st_finish<S, MODE, NTS>(a, tix(k + 1), lane, want_stats, mio_of((k + 1) % TPW), vb, xb, st);
+      st_finish<S, MODE, NTS>(a, tix(k + 1), lane, want_stats, mio_of((k + 1) % TPW), top, vb,
+                              xb, st);
     }
   }
   if (want_stats) {

@@ -315,6 +315,42 @@ def test_commit_vote_bucketed_across_buckets(eng, orc):
         check_commit_vote(eng, orc, b, goff=goff)
 
 
+@pytest.mark.parametrize("S", [6, 10, 16])
+@pytest.mark.parametrize("joint", [False, True])
+def test_commit_vote_low_slot_chunks(eng, orc, S, joint):
+    """Chunk-uniform "top" specialisation (joint_committed_top): every run of
+    256..1024 groups keeps its voters below a random top slot (1..S), so each
+    smaller selection network runs, chunks straddle runs, and learners sit
+    both above and below top."""
+    G = 64 * 8 * 37 + 29
+    rng = np.random.default_rng(31 * S + joint)
+    md = eng.mask_np_dtype(S)
+    tops = np.empty(G, np.int64)
+    i = 0
+    while i < G:
+        n = int(rng.integers(256, 1025))
+        tops[i:i + n] = rng.integers(1, S + 1)
+        i += n
+    lim = (np.int64(1) << tops) - 1
+    inc = rng.integers(0, 1 << S, G) & lim
+    out = (rng.integers(0, 1 << S, G) & lim) if joint else np.zeros(G, np.int64)
+    out[rng.random(G) < 0.2] = 0
+    learner = rng.integers(0, 1 << S, G) & ~(inc | out) & ((1 << S) - 1)
+    base = rng.integers(1, 1 << 50, G, dtype=np.uint64)
+    m = base[None, :] + rng.integers(0, 1 << 20, (S, G), dtype=np.uint64)
+    m[rng.random((S, G)) < 0.15] = 0
+    voted = rng.integers(0, 1 << S, G)
+    granted = rng.integers(0, 1 << S, G) & voted
+    masks = ("inc", "out", "learner") if joint else ("inc", "learner")
+    b = eng.SlotBatch(G, S, DEV, masks=masks)
+    kw = dict(inc=inc.astype(md), learner=learner.astype(md), voted=voted.astype(md),
+              granted=granted.astype(md))
+    if joint:
+        kw["out"] = out.astype(md)
+    b.load_host(m.reshape(-1), **kw)
+    check_commit_vote(eng, orc, b)
+
+
 def test_full_size_config3_properties(eng, orc):
     """BASELINE config 3 at full size (128M joint 5+5 groups): the order-free
     stats vector (incl. checksum) matches the oracle, and the result is
