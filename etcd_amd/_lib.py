@@ -118,6 +118,27 @@ QE_PACK_LEARNER_NEXT_NOT_OUTGOING = 4
 QE_PACK_ZERO_ID = 8
 
 
+class QeConf(C.Structure):
+    _fields_ = [
+        ("num_groups", u64), ("num_slots", u32), ("reserved", u32), ("slot_ids", vp),
+        ("inc_mask", vp), ("out_mask", vp), ("learner_mask", vp), ("learners_next_mask", vp),
+        ("is_learner", vp), ("tracked", vp), ("auto_leave", vp),
+    ]
+
+
+class QeConfChanges(C.Structure):
+    _fields_ = [
+        ("max_changes", u32), ("reserved", u32), ("stride", u64), ("op", vp), ("count", vp),
+        ("type", vp), ("node_id", vp), ("last_index", vp), ("result", vp),
+        ("new_progress", vp),
+    ]
+
+
+QE_CC_ADD_NODE, QE_CC_REMOVE_NODE, QE_CC_UPDATE_NODE, QE_CC_ADD_LEARNER_NODE = 0, 1, 2, 3
+QE_CC_OP_NONE, QE_CC_OP_SIMPLE, QE_CC_OP_ENTER_JOINT, QE_CC_OP_ENTER_JOINT_AUTO, \
+    QE_CC_OP_LEAVE_JOINT = 0, 1, 2, 3, 4
+
+
 # Every symbol include/etcd_quorum.h declares, with its prototype.
 PROTOTYPES = {
     "qe_abi_version": (C.c_int, []),
@@ -142,6 +163,8 @@ PROTOTYPES = {
     "qe_pack_threads": (C.c_int, [C.c_int]),
     "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, u32, vp, vp, vp]),
+    "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),
+                                C.POINTER(QeProgress), vp]),
 }
 
 

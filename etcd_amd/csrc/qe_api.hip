@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include "qe_dispatch.hpp"
+#include "qe_conf.hpp"
 
 namespace qe {
 
@@ -424,6 +425,61 @@ int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_em
   a.sent = sent;
   a.snap = snap;
   return dispatch_progress(p->num_slots, a, 1, false, false, static_cast<hipStream_t>(stream));
+}
+
+int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress *p,
+                  void *stream) {
+  if (!c || !ch) return QE_EINVAL;
+  if (c->num_slots == 0 || c->num_slots > QE_MAX_SLOTS || c->reserved) return QE_EINVAL;
+  if (c->num_groups == 0) return QE_OK;
+  if (!c->slot_ids || !c->inc_mask || !c->out_mask || !c->learner_mask ||
+      !c->learners_next_mask || !c->is_learner || !c->tracked || !c->auto_leave)
+    return QE_EINVAL;
+  if (!ch->op || !ch->count || !ch->last_index || !ch->result) return QE_EINVAL;
+  if (ch->max_changes > 0 && (!ch->type || !ch->node_id || ch->stride < c->num_groups))
+    return QE_EINVAL;
+  CCArgs a{};
+  a.G = c->num_groups;
+  a.S = c->num_slots;
+  a.C = ch->max_changes;
+  a.stride = ch->stride;
+  a.ids = c->slot_ids;
+  a.inc = c->inc_mask;
+  a.out = c->out_mask;
+  a.lrn = c->learner_mask;
+  a.lnx = c->learners_next_mask;
+  a.isl = c->is_learner;
+  a.trk = c->tracked;
+  a.auto_leave = c->auto_leave;
+  a.op = ch->op;
+  a.count = ch->count;
+  a.type = ch->type;
+  a.node = ch->node_id;
+  a.last_index = ch->last_index;
+  a.result = ch->result;
+  a.new_progress = ch->new_progress;
+  if (p) {
+    if (p->num_groups != c->num_groups || p->num_slots != c->num_slots ||
+        p->stride < p->num_groups)
+      return QE_EINVAL;
+    if (!p->match || !p->next || !p->pending_snapshot || !p->flags || !p->infl_start ||
+        !p->infl_count)
+      return QE_EINVAL;
+    a.pstride = p->stride;
+    a.p_match = p->match;
+    a.p_next = p->next;
+    a.p_pending = p->pending_snapshot;
+    a.p_flags = p->flags;
+    a.p_istart = p->infl_start;
+    a.p_icount = p->infl_count;
+  }
+  const dim3 grid(static_cast<unsigned>((a.G + kBlock - 1) / kBlock));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (a.S <= 8)
+    hipLaunchKernelGGL(k_confchange<uint8_t>, grid, dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_confchange<uint16_t>, grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
 }
 
 int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream) {

@@ -360,3 +360,67 @@ def progress_send(ps, want, send_if_empty=False, max_ents=1):
         C.byref(p), _ptr(want), int(bool(send_if_empty)), int(max_ents), _ptr(sent), _ptr(snap),
         _stream(ps.device)))
     return sent, snap
+
+
+class ConfState:
+    """Device-resident tracker.Config + ProgressMap key set of G groups in
+    slot form (qe_conf): slot_ids [G][S], slot masks for Voters[0],
+    Voters[1], Learners, LearnersNext, Progress.IsLearner and tracked slots,
+    and AutoLeave."""
+
+    MASKS = ("inc", "out", "learner", "learners_next", "is_learner", "tracked")
+
+    def __init__(self, G, S, device="cuda"):
+        if not 1 <= S <= _lib.QE_MAX_SLOTS:
+            raise ValueError("bad num_slots")
+        self.G, self.S, self.device = int(G), int(S), torch.device(device)
+        md = mask_torch_dtype(S)
+        self.slot_ids = torch.zeros(self.G * self.S, dtype=torch.int64, device=self.device)
+        for k in self.MASKS:
+            setattr(self, k, torch.zeros(self.G, dtype=md, device=self.device))
+        self.auto_leave = torch.zeros(self.G, dtype=torch.uint8, device=self.device)
+
+    def struct(self):
+        return _lib.QeConf(self.G, self.S, 0, _ptr(self.slot_ids), _ptr(self.inc), _ptr(self.out),
+                           _ptr(self.learner), _ptr(self.learners_next), _ptr(self.is_learner),
+                           _ptr(self.tracked), _ptr(self.auto_leave))
+
+    def host(self):
+        md = mask_np_dtype(self.S)
+        out = {"slot_ids": self.slot_ids.cpu().numpy().view(np.uint64).reshape(self.G, self.S),
+               "auto_leave": self.auto_leave.cpu().numpy()}
+        for k in self.MASKS:
+            out[k] = getattr(self, k).cpu().numpy().view(md)
+        return out
+
+
+class ConfChanges:
+    """One configuration-change operation per group (qe_conf_changes):
+    op [G], count [G], type/node_id [C][stride], last_index [G]; result and
+    new_progress are outputs."""
+
+    def __init__(self, G, S, C_max, device="cuda"):
+        self.G, self.C = int(G), int(C_max)
+        self.stride = max(1, self.G)
+        dev = torch.device(device)
+        self.op = torch.zeros(self.G, dtype=torch.uint8, device=dev)
+        self.count = torch.zeros(self.G, dtype=torch.uint8, device=dev)
+        self.type = torch.zeros(max(1, self.C) * self.stride, dtype=torch.uint8, device=dev)
+        self.node_id = torch.zeros(max(1, self.C) * self.stride, dtype=torch.int64, device=dev)
+        self.last_index = torch.zeros(self.G, dtype=torch.int64, device=dev)
+        self.result = torch.zeros(self.G, dtype=torch.uint8, device=dev)
+        self.new_progress = torch.zeros(self.G, dtype=mask_torch_dtype(S), device=dev)
+
+    def struct(self):
+        return _lib.QeConfChanges(self.C, 0, self.stride, _ptr(self.op), _ptr(self.count),
+                                  _ptr(self.type), _ptr(self.node_id), _ptr(self.last_index),
+                                  _ptr(self.result), _ptr(self.new_progress))
+
+
+def confchange(cs, ch, ps=None):
+    """Changer.Simple / EnterJoint / LeaveJoint per group on the GPU
+    (qe_confchange, raft/confchange/confchange.go:49-274)."""
+    c, x = cs.struct(), ch.struct()
+    p = C.byref(ps.struct()) if ps is not None else None
+    check("qe_confchange", _lib.lib().qe_confchange(C.byref(c), C.byref(x), p,
+                                                     _stream(cs.device)))

@@ -391,6 +391,81 @@ int qe_slot_lookup(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot
 /* Host packing threads (0 = min(16, hardware threads)). */
 int qe_pack_threads(int n);
 
+/* ---- configuration changes (raft/confchange/confchange.go) ------------- */
+
+/* ConfChangeSingle.Type (raft/raftpb/raft.pb.go:224-227) */
+#define QE_CC_ADD_NODE 0
+#define QE_CC_REMOVE_NODE 1
+#define QE_CC_UPDATE_NODE 2
+#define QE_CC_ADD_LEARNER_NODE 3
+
+/* per-group operation */
+#define QE_CC_OP_NONE 0
+#define QE_CC_OP_SIMPLE 1            /* Changer.Simple          (:130-147) */
+#define QE_CC_OP_ENTER_JOINT 2       /* Changer.EnterJoint(false, ...)     */
+#define QE_CC_OP_ENTER_JOINT_AUTO 3  /* Changer.EnterJoint(true, ...) (:49-76) */
+#define QE_CC_OP_LEAVE_JOINT 4       /* Changer.LeaveJoint      (:92-123) */
+
+/* per-group result (a group with an error keeps its state, as the caller of
+ * the reference Changer discards the returned config on error) */
+#define QE_CC_OK 0
+#define QE_CC_ERR_INVARIANT 1        /* checkInvariants on the input (:186-241) */
+#define QE_CC_ERR_ALREADY_JOINT 2    /* "config is already joint"              */
+#define QE_CC_ERR_ZERO_VOTER_JOINT 3 /* "can't make a zero-voter config joint" */
+#define QE_CC_ERR_NOT_JOINT 4        /* "can't leave a non-joint config"       */
+#define QE_CC_ERR_SIMPLE_IN_JOINT 5  /* "can't apply simple config change in joint config" */
+#define QE_CC_ERR_BAD_TYPE 6         /* "unexpected conf type %d"              */
+#define QE_CC_ERR_REMOVED_ALL 7      /* "removed all voters"                   */
+#define QE_CC_ERR_SIMPLE_MULTI 8     /* "more than one voter changed without entering joint config" */
+#define QE_CC_ERR_INVARIANT_OUT 9    /* checkInvariants on the result          */
+#define QE_CC_ERR_NO_SLOT 10         /* slot model: a new peer found no free slot */
+
+/* tracker.Config + the ProgressMap key set of G groups in slot form.  A slot
+ * is tracked when it holds a Progress (ProgressMap key); Voters[0],
+ * Voters[1], Learners and LearnersNext are slot masks ([G], u8 for
+ * num_slots <= 8, else u16) over tracked slots; is_learner is
+ * Progress.IsLearner.  slot_ids is [G][S] as written by qe_pack_confstate;
+ * the ids of untracked slots are ignored on input and written as 0. */
+typedef struct qe_conf {
+  uint64_t num_groups;
+  uint32_t num_slots;
+  uint32_t reserved;
+  uint64_t *slot_ids;           /* [G][S]                                   */
+  void *inc_mask, *out_mask;    /* Voters[0], Voters[1]                     */
+  void *learner_mask;           /* Learners                                 */
+  void *learners_next_mask;     /* LearnersNext                             */
+  void *is_learner;             /* Progress.IsLearner                       */
+  void *tracked;                /* slots holding a Progress                 */
+  uint8_t *auto_leave;          /* [G] Config.AutoLeave                     */
+} qe_conf;
+
+/* One operation per group with up to max_changes ConfChangeSingle entries:
+ * change c of group g at [c*stride + g]. */
+typedef struct qe_conf_changes {
+  uint32_t max_changes;
+  uint32_t reserved;
+  uint64_t stride;              /* >= num_groups                            */
+  const uint8_t *op;            /* [G] QE_CC_OP_*                           */
+  const uint8_t *count;         /* [G] changes of group g (<= max_changes)  */
+  const uint8_t *type;          /* [C][stride] QE_CC_ADD_NODE ...           */
+  const uint64_t *node_id;      /* [C][stride] NodeID (0 = ignored, :154-160) */
+  const uint64_t *last_index;   /* [G] Changer.LastIndex                    */
+  uint8_t *result;              /* [G] out: QE_CC_*                         */
+  void *new_progress;           /* [G] out mask (may be NULL): slots whose
+                                   Progress initProgress created           */
+} qe_conf_changes;
+
+/* Changer.Simple / EnterJoint / LeaveJoint per group (raft/confchange/
+ * confchange.go:49-274): makeVoter, makeLearner (LearnersNext while the
+ * peer is an outgoing voter), remove (keeps the Progress of an outgoing
+ * voter), symdiff over voter ids, checkInvariants before and after.  A new
+ * peer takes the lowest untracked slot.  When `p` is non-NULL (same G and S)
+ * the Progress of every created slot is initialised as initProgress does
+ * (:262-273): Match 0, Next = last_index, StateProbe, RecentActive, empty
+ * Inflights, no pending snapshot. */
+int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress *p,
+                  void *stream);
+
 /* ---- statistics -------------------------------------------------------- */
 
 /* out[QE_STATS_COUNTERS] (device) = sum over shards of stats (device). */

@@ -22,10 +22,16 @@ Sources (read as text; nothing from the reference is executed):
   * TestInflightsAdd / TestInflightFreeTo / TestInflightFreeFirstOne
     (raft/tracker/inflights_test.go:22-190), transcribed as op sequences.
   * TestFastLogRejection leader-side rows, raft/raft_test.go:4319-4540.
+  * raft/confchange/testdata/*.txt -- TestConfChangeDataDriven
+    (raft/confchange/datadriven_test.go:29-98): per file, the command
+    sequence (simple / enter-joint [autoleave=..] / leave-joint), its input
+    tokens (vN voter, lN learner, rN remove, uN update) and the expected
+    output lines (Config.String + ProgressMap.String, or the error text).
 
 Outputs (data only: inputs + expected outputs):
   tests/golden/quorum_testdata.jsonl   127 rows
   tests/golden/raft_tables.json        the three tables
+  tests/golden/confchange_testdata.json  9 files of confchange steps
 """
 import json
 import os
@@ -275,6 +281,36 @@ def fast_log_rejection_table():
                       "-> rejection -> next MsgApp)", "rows": rows}
 
 
+def confchange_files():
+    """datadriven blocks: `cmd [args]`, input lines, `----`, output up to a
+    blank line."""
+    d = os.path.join(REF, "confchange", "testdata")
+    files = {}
+    for name in sorted(os.listdir(d)):
+        lines = open(os.path.join(d, name), encoding="utf-8").read().split("\n")
+        steps, i = [], 0
+        while i < len(lines):
+            line = lines[i]
+            if line.split(" ")[0] in ("simple", "enter-joint", "leave-joint"):
+                cmd, _, args = line.partition(" ")
+                j, inp = i + 1, []
+                while lines[j] != "----":
+                    inp.append(lines[j])
+                    j += 1
+                j += 1
+                out = []
+                while j < len(lines) and lines[j] != "":
+                    out.append(lines[j])
+                    j += 1
+                steps.append({"line": i + 1, "cmd": cmd, "args": args,
+                              "input": " ".join(inp).strip(), "expect": out})
+                i = j
+            else:
+                i += 1
+        files[name] = {"source": f"raft/confchange/testdata/{name}", "steps": steps}
+    return files
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are already committed")
@@ -307,6 +343,10 @@ def main():
         for r in tables["TestLeaderElectionInOneRoundRPC"]["rows"]:
             votes = ",".join(f"{i}:{int(v)}" for i, v in r["votes"])
             f.write(f"{r['size']} {r['state']} votes={votes}\n")
+    cc = confchange_files()
+    with open(os.path.join(HERE, "confchange_testdata.json"), "w", encoding="utf-8") as f:
+        json.dump(cc, f, indent=1)
+    print("wrote", sum(len(v["steps"]) for v in cc.values()), "confchange steps in", len(cc), "files")
     counts = {}
     for r in rows:
         k = r["source"].split("/")[-1].split(":")[0]

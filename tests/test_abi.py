@@ -57,6 +57,9 @@ int main(void) {
   Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
   Z(qe_progress) F(qe_progress, infl_buf) F(qe_progress, log_runs) F(qe_progress, out_mask)
   Z(qe_peer_msgs) F(qe_peer_msgs, bcast)
+  Z(qe_conf) F(qe_conf, slot_ids) F(qe_conf, tracked) F(qe_conf, auto_leave)
+  Z(qe_conf_changes) F(qe_conf_changes, stride) F(qe_conf_changes, node_id)
+  F(qe_conf_changes, new_progress)
   return 0;
 }
 """
@@ -66,7 +69,8 @@ CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
           "qe_election_state": _lib.QeElectionState,
           "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams,
           "qe_confstate_csr": _lib.QeConfStateCSR, "qe_progress": _lib.QeProgress,
-          "qe_peer_msgs": _lib.QePeerMsgs}
+          "qe_peer_msgs": _lib.QePeerMsgs, "qe_conf": _lib.QeConf,
+          "qe_conf_changes": _lib.QeConfChanges}
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -123,6 +127,11 @@ def test_argument_errors_without_gpu():
     assert L.qe_progress_step(C.byref(pr), C.byref(_lib.QePeerMsgs()), None, None) == _lib.QE_ERANGE
     pr = _lib.QeProgress(num_groups=1, num_slots=3, inflight_cap=4, stride=1, log_runs=17)
     assert L.qe_progress_send(C.byref(pr), None, 0, 1, None, None, None) == _lib.QE_ERANGE
+    assert L.qe_confchange(None, None, None, None) == _lib.QE_EINVAL
+    cf = _lib.QeConf(num_groups=4, num_slots=17)
+    assert L.qe_confchange(C.byref(cf), C.byref(_lib.QeConfChanges()), None, None) == _lib.QE_EINVAL
+    cf = _lib.QeConf(num_groups=0, num_slots=5)  # empty batch is a no-op
+    assert L.qe_confchange(C.byref(cf), C.byref(_lib.QeConfChanges()), None, None) == _lib.QE_OK
     p = _lib.QeElectionParams(p_drop_q16=70000)
     st = _lib.QeElectionState(num_groups=1, num_slots=3, term=C.c_void_p(64),
                               state=C.c_void_p(64), voted=C.c_void_p(64),

@@ -1,0 +1,250 @@
+"""qe_confchange (Changer.Simple / EnterJoint / LeaveJoint on slot masks) on
+the GPU against the map-based oracle (oracle/confchange_ref.py), which is
+pinned to the reference's raft/confchange/testdata (test_confchange_oracle.py).
+
+* every step of the 9 testdata files, one file per group, replayed through
+  the kernel and compared as text (Config.String + ProgressMap.String or the
+  error text);
+* random multi-step differential runs over S = 2..16 with ID pools that fit
+  the slots, zero node IDs, UpdateNode and invalid types;
+* ID pools larger than the slots: QE_CC_ERR_NO_SLOT exactly when the
+  reference change would hold more than S Progress entries at some point
+  before its own outcome;
+* corrupted inputs: QE_CC_ERR_INVARIANT exactly when checkInvariants fails.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import confchange_ref as cc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from etcd_amd import engine
+    return engine
+
+
+def to_oracle(h, ps_h, g, S):
+    """Slot state of group g -> (Config, {id: Progress})."""
+    ids = h["slot_ids"][g]
+
+    def ids_of(mask):
+        m = int(mask[g])
+        return {int(ids[s]) for s in range(S) if (m >> s) & 1}
+    cfg = cc.Config()
+    cfg.inc, cfg.out = ids_of(h["inc"]), ids_of(h["out"])
+    cfg.learners, cfg.lnext = ids_of(h["learner"]), ids_of(h["learners_next"])
+    cfg.auto_leave = bool(h["auto_leave"][g])
+    prs = {}
+    trk, isl = int(h["tracked"][g]), int(h["is_learner"][g])
+    for s in range(S):
+        if (trk >> s) & 1:
+            p = cc.Progress(0, bool((isl >> s) & 1))
+            if ps_h is not None:
+                r = s * ps_h["stride"] + g
+                p.match, p.next = int(ps_h["match"][r]), int(ps_h["next"][r])
+                fl = int(ps_h["flags"][r])
+                p.state = ("StateProbe", "StateReplicate", "StateSnapshot", "?")[fl & 3]
+                p.probe_sent, p.recent_active = bool(fl & 4), bool(fl & 8)
+                p.pending = int(ps_h["pending"][r])
+            prs[int(ids[s])] = p
+    return cfg, prs
+
+
+def set_changes(ch, ops, ccs, last_index):
+    G = len(ops)
+    typ = np.zeros((ch.C, ch.stride), np.uint8)
+    node = np.zeros((ch.C, ch.stride), np.uint64)
+    cnt = np.zeros(G, np.uint8)
+    for g, lst in enumerate(ccs):
+        cnt[g] = len(lst)
+        for k, (t, n) in enumerate(lst):
+            typ[k, g], node[k, g] = t, n
+    ch.op.copy_(torch.tensor(ops, dtype=torch.uint8))
+    ch.count.copy_(torch.from_numpy(cnt))
+    ch.type.copy_(torch.from_numpy(typ.reshape(-1)))
+    ch.node_id.copy_(torch.from_numpy(node.reshape(-1).view(np.int64)))
+    ch.last_index.copy_(torch.tensor(last_index, dtype=torch.int64))
+
+
+def ps_host(ps):
+    h = ps.host()
+    h["stride"] = ps.stride
+    return h
+
+
+def test_testdata_replay(eng):
+    files = json.load(open(os.path.join(HERE, "golden", "confchange_testdata.json")))
+    names = sorted(files)
+    G, S = len(names), 8
+    C = max(len(st["input"].split()) for f in files.values() for st in f["steps"])
+    cs = eng.ConfState(G, S, DEV)
+    ps = eng.ProgressState(G, S, 1, 1, DEV)
+    ch = eng.ConfChanges(G, S, C, DEV)
+    nsteps = max(len(files[n]["steps"]) for n in names)
+    checked = 0
+    for k in range(nsteps):
+        ops, ccs = [], []
+        for n in names:
+            steps = files[n]["steps"]
+            if k >= len(steps):
+                ops.append(cc.OP_NONE)
+                ccs.append([])
+                continue
+            st = steps[k]
+            if st["cmd"] == "simple":
+                ops.append(cc.OP_SIMPLE)
+            elif st["cmd"] == "enter-joint":
+                ops.append(cc.OP_ENTER_JOINT_AUTO if "autoleave=true" in st["args"]
+                           else cc.OP_ENTER_JOINT)
+            else:
+                assert st["input"] == ""
+                ops.append(cc.OP_LEAVE_JOINT)
+            ccs.append(cc.parse_changes(st["input"]))
+        set_changes(ch, ops, ccs, [k] * G)  # LastIndex = step number
+        eng.confchange(cs, ch, ps)
+        torch.cuda.synchronize()
+        res = ch.result.cpu().numpy()
+        h, hp = cs.host(), ps_host(ps)
+        for g, n in enumerate(names):
+            steps = files[n]["steps"]
+            if k >= len(steps):
+                continue
+            st = steps[k]
+            if res[g] != cc.OK:
+                got = [cc.MESSAGES.get(int(res[g]), f"error {res[g]}")]
+            else:
+                cfg, prs = to_oracle(h, hp, g, S)
+                got = [cfg.string()] + cc.progress_string(prs)
+            assert got == st["expect"], f"{n}:{st['line']}"
+            checked += 1
+    assert checked == 58
+
+
+def random_ccs(rng, pool, nmax):
+    out = []
+    for _ in range(rng.randrange(0, nmax + 1)):
+        r = rng.random()
+        t = (cc.ADD_NODE if r < 0.4 else cc.ADD_LEARNER_NODE if r < 0.65 else
+             cc.REMOVE_NODE if r < 0.9 else cc.UPDATE_NODE if r < 0.98 else 7)
+        node = 0 if rng.random() < 0.03 else rng.choice(pool)
+        out.append((t, node))
+    return out
+
+
+def run_differential(eng, S, pool_size, G, steps, seed, nmax=4):
+    rng = random.Random(seed)
+    pools = [rng.sample(range(1, 1 << 40), pool_size) for _ in range(G)]
+    changers = [cc.Changer() for _ in range(G)]
+    cs = eng.ConfState(G, S, DEV)
+    ps = eng.ProgressState(G, S, 1, 1, DEV)
+    ch = eng.ConfChanges(G, S, nmax, DEV)
+    seen = set()
+    for k in range(steps):
+        ops, ccs = [], []
+        for g in range(G):
+            ops.append(rng.choice([cc.OP_SIMPLE] * 3 + [cc.OP_ENTER_JOINT, cc.OP_ENTER_JOINT_AUTO,
+                                   cc.OP_LEAVE_JOINT, cc.OP_NONE]))
+            ccs.append(random_ccs(rng, pools[g], nmax) if ops[-1] != cc.OP_LEAVE_JOINT else [])
+        li = k * 10 + 3
+        set_changes(ch, ops, ccs, [li] * G)
+        eng.confchange(cs, ch, ps)
+        torch.cuda.synchronize()
+        res = ch.result.cpu().numpy()
+        newp = ch.new_progress.cpu().numpy()
+        h, hp = cs.host(), ps_host(ps)
+        for g in range(G):
+            o = changers[g]
+            o.last_index = li
+            before = (o.cfg.clone(), {i: p.copy() for i, p in o.prs.items()})
+            want = o.run(ops[g], ccs[g])
+            if o.peak > S:
+                # the change needs more Progress entries than there are slots
+                # at some point before the reference's own outcome
+                assert res[g] == cc.ERR_NO_SLOT, (S, g, k, ops[g], ccs[g])
+                o.cfg, o.prs = before
+                seen.add("no_slot")
+            else:
+                assert res[g] == want, (S, g, k, ops[g], ccs[g])
+            seen.add(int(res[g]))
+            cfg, prs = to_oracle(h, hp, g, S)
+            assert cfg.string() == o.cfg.string(), (S, g, k)
+            assert cc.progress_string(prs) == cc.progress_string(o.prs), (S, g, k)
+            if res[g] == cc.OK:
+                created = {int(h["slot_ids"][g][s]) for s in range(S) if (int(newp[g]) >> s) & 1}
+                fresh = {i for i, p in o.prs.items()
+                         if i not in before[1] or p.next != before[1][i].next}
+                assert created >= fresh, (g, k)
+                assert all(o.prs[i].next == li for i in created), (g, k)
+    return seen
+
+
+@pytest.mark.parametrize("S", [2, 3, 5, 8, 9, 16])
+def test_random_differential(eng, S):
+    seen = run_differential(eng, S, S, 512, 12, 1000 + S)
+    assert cc.OK in seen and cc.ERR_REMOVED_ALL in seen
+
+
+@pytest.mark.parametrize("S", [3, 6, 12])
+def test_no_slot(eng, S):
+    seen = run_differential(eng, S, 2 * S, 512, 10, 2000 + S, nmax=S + 2)
+    assert "no_slot" in seen
+
+
+def test_invalid_inputs(eng):
+    """Corrupted slot states: QE_CC_ERR_INVARIANT iff checkInvariants fails
+    (duplicate tracked ids and id 0 are invalid slot states too)."""
+    S, G = 6, 4096
+    rng = np.random.default_rng(7)
+    cs = eng.ConfState(G, S, DEV)
+    md = eng.mask_np_dtype(S)
+    ids = rng.integers(1, 9, (G, S)).astype(np.uint64)  # duplicates likely
+    ids[rng.random((G, S)) < 0.02] = 0
+    trk = rng.integers(0, 1 << S, G)
+
+    def sub(p):  # subset of the tracked slots with probability p
+        return np.where(rng.random(G) < p, rng.integers(0, 1 << S, G) & trk,
+                        rng.integers(0, 1 << S, G))
+    inc = sub(0.9)
+    out = np.where(rng.random(G) < 0.5, sub(0.9), 0)
+    lrn = np.where(rng.random(G) < 0.8, sub(0.9) & ~(inc | out), rng.integers(0, 1 << S, G))
+    lnx = np.where(rng.random(G) < 0.3, sub(0.9) & out, 0)
+    isl = (lrn | rng.integers(0, 1 << S, G)) & ~np.where(rng.random(G) < 0.9, lnx, 0)
+    al = (rng.random(G) < 0.2).astype(np.uint8)
+    cs.slot_ids.copy_(torch.from_numpy(ids.reshape(-1).view(np.int64)).to(DEV))
+    for k, v in (("inc", inc), ("out", out), ("learner", lrn), ("learners_next", lnx),
+                 ("is_learner", isl), ("tracked", trk)):
+        getattr(cs, k).copy_(torch.from_numpy(v.astype(md)).to(DEV))
+    cs.auto_leave.copy_(torch.from_numpy(al).to(DEV))
+    ch = eng.ConfChanges(G, S, 1, DEV)
+    ch.op.fill_(cc.OP_SIMPLE)
+    eng.confchange(cs, ch)
+    torch.cuda.synchronize()
+    res = ch.result.cpu().numpy()
+    state = {"slot_ids": ids, "tracked": trk, "is_learner": isl, "inc": inc, "out": out,
+             "learner": lrn, "learners_next": lnx, "auto_leave": al}
+    n_bad = 0
+    for g in range(G):
+        t = int(trk[g])
+        tracked_ids = [int(ids[g, s]) for s in range(S) if (t >> s) & 1]
+        bad = 0 in tracked_ids or len(set(tracked_ids)) != len(tracked_ids)
+        # a set member without a Progress: "no progress for %d"
+        bad |= ((int(inc[g]) | int(out[g]) | int(lrn[g]) | int(lnx[g])) & ~t) != 0
+        if not bad:
+            cfg, prs = to_oracle(state, None, g, S)
+            bad = cc.check_invariants(cfg, prs) is not None
+        if bad:
+            assert res[g] == cc.ERR_INVARIANT, g
+            n_bad += 1
+        else:
+            assert res[g] != cc.ERR_INVARIANT, g
+    assert 100 < n_bad < G - 100
