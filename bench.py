@@ -50,6 +50,9 @@ WORKLOADS = {
     "progress_step": ("16M groups x 5 peers: one round of MsgAppResp accept/reject + "
                       "MsgHeartbeatResp through the full Progress state machine "
                       "(inflights F=8, leader-log model R=4)", 1 << 24, 5, "progress"),
+    "confchange": ("16M groups x Changer.Simple(AddNode(learner), AddLearnerNode(new)) on "
+                   "slot masks: promote a learner, add a learner with initProgress "
+                   "(3 voters + 1 learner + 1 free slot)", 1 << 24, 5, "confchange"),
 }
 
 
@@ -303,6 +306,53 @@ def setup(name, G, S, kind, d, stats):
                          lib.qe_progress_step(C.byref(p_), C.byref(m_), sp, stream))
 
         return step, bpg, G, "group-rounds", {"ps": ps, "msgs": msgs, "prepare": prepare}
+    if kind == "confchange":
+        cs = engine.ConfState(G, S, d.dev)
+        ps = engine.ProgressState(G, S, 1, 1, d.dev)
+        ch = engine.ConfChanges(G, S, 2, d.dev)
+        gid = torch.arange(G, device=d.dev, dtype=torch.int64) + goff
+        ids = gid.view(G, 1) * 8 + torch.arange(1, S + 1, device=d.dev).view(1, S)
+        ids[:, 4] = 0  # slot 4 free
+        cs.slot_ids.copy_(ids.reshape(-1))
+        cs.inc.fill_(0b00111)
+        cs.learner.fill_(0b01000)
+        cs.is_learner.fill_(0b01000)
+        cs.tracked.fill_(0b01111)
+        ch.op.fill_(1)  # QE_CC_OP_SIMPLE
+        ch.count.fill_(2)
+        ch.type.view(2, G)[0].fill_(0)  # AddNode(learner in slot 3): promote
+        ch.type.view(2, G)[1].fill_(3)  # AddLearnerNode(new id)
+        ch.node_id.view(2, G)[0].copy_(gid * 8 + 4)
+        ch.node_id.view(2, G)[1].copy_(gid * 8 + 7)
+        ch.last_index.copy_(gid + 100)
+        mutable = ("slot_ids", "inc", "out", "learner", "learners_next", "is_learner",
+                   "tracked", "auto_leave")
+        pristine = {k: getattr(cs, k).clone() for k in mutable}
+
+        def prepare():
+            for k in mutable:
+                getattr(cs, k).copy_(pristine[k])
+
+        # every input read once (op, count, 2 changes, last_index, 6 masks,
+        # auto_leave, S ids) and every output written once (result,
+        # new_progress, 6 masks, auto_leave, S ids, one initialised Progress
+        # row: match/next/pending + flags/istart/icount)
+        bpg = (1 + 1 + 2 * 9 + 8 + 6 + 1 + 8 * S) + (1 + 1 + 6 + 1 + 8 * S + 27)
+        import ctypes as C
+        c_, x_, p_ = cs.struct(), ch.struct(), ps.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+
+        def step():
+            engine.check("qe_confchange",
+                         lib.qe_confchange(C.byref(c_), C.byref(x_), C.byref(p_), stream))
+
+        def verify():
+            ok = bool((ch.result == 0).all()) and bool((cs.inc == 0b01111).all())
+            return ok and bool((cs.learner == 0b10000).all())
+
+        return step, bpg, G, "group-changes", {"cs": cs, "ps": ps, "ch": ch,
+                                               "prepare": prepare, "verify": verify}
     raise ValueError(kind)
 
 
@@ -396,6 +446,9 @@ def run_workload(name, args, d, steps, warmup):
     torch.cuda.synchronize(d.dev)
     prepare = keep.get("prepare")
     wall, kern_ms = time_steps(step, d, steps, warmup, prepare)
+    if keep.get("verify"):
+        torch.cuda.synchronize(d.dev)
+        assert keep["verify"](), f"{name}: unexpected result"
     kern_avg = d.max(float(np.mean(kern_ms)))
     # with a per-launch state restore the wall clock also holds the restore
     # copies: the step time is then the launch's own HIP-event time

@@ -440,7 +440,6 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
     return QE_EINVAL;
   CCArgs a{};
   a.G = c->num_groups;
-  a.S = c->num_slots;
   a.C = ch->max_changes;
   a.stride = ch->stride;
   a.ids = c->slot_ids;
@@ -475,10 +474,14 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
   }
   const dim3 grid(static_cast<unsigned>((a.G + kBlock - 1) / kBlock));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (a.S <= 8)
-    hipLaunchKernelGGL(k_confchange<uint8_t>, grid, dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL(k_confchange<uint16_t>, grid, dim3(kBlock), 0, st, a);
+  switch (c->num_slots) {
+#define QE_CC_CASE(n) \
+  case n: hipLaunchKernelGGL(k_confchange<n>, grid, dim3(kBlock), 0, st, a); break;
+    QE_CC_CASE(1) QE_CC_CASE(2) QE_CC_CASE(3) QE_CC_CASE(4) QE_CC_CASE(5) QE_CC_CASE(6)
+    QE_CC_CASE(7) QE_CC_CASE(8) QE_CC_CASE(9) QE_CC_CASE(10) QE_CC_CASE(11) QE_CC_CASE(12)
+    QE_CC_CASE(13) QE_CC_CASE(14) QE_CC_CASE(15) QE_CC_CASE(16)
+#undef QE_CC_CASE
+  }
   return hip_status(hipGetLastError());
 }
 

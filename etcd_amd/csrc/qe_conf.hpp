@@ -18,7 +18,7 @@ constexpr int kCCMax = 16;  // QE_MAX_SLOTS
 
 struct CCArgs {
   uint64_t G, stride, pstride;
-  uint32_t S, C;
+  uint32_t C;
   uint64_t *ids;
   void *inc, *out, *lrn, *lnx, *isl, *trk;
   uint8_t *auto_leave;
@@ -38,8 +38,8 @@ struct CCState {
 // checkInvariants (raft/confchange/confchange.go:186-241) on slot masks,
 // plus what the map model guarantees by construction: tracked ids are
 // distinct and nonzero (raft.None is never a peer).
-__device__ __forceinline__ bool cc_invariants(const CCState &c, const uint64_t (&id)[kCCMax],
-                                              uint32_t S) {
+template <int S>
+__device__ __forceinline__ bool cc_invariants(const CCState &c, const uint64_t (&id)[kCCMax]) {
   bool ok = ((c.inc | c.out | c.lrn | c.lnx) & ~c.trk) == 0;  // "no progress for %d"
   ok &= (c.lnx & ~c.out) == 0;                                  // LearnersNext ⊆ Voters[1]
   ok &= (c.lnx & c.isl) == 0;                                   // staged, not yet learner
@@ -47,12 +47,12 @@ __device__ __forceinline__ bool cc_invariants(const CCState &c, const uint64_t (
   ok &= (c.lrn & ~c.isl) == 0;                                  // learners marked IsLearner
   ok &= c.out != 0 || (c.lnx == 0 && c.al == 0);                // non-joint: nil / false
 #pragma unroll
-  for (int s = 0; s < kCCMax; s++) {
-    const bool ts = static_cast<uint32_t>(s) < S && ((c.trk >> s) & 1u);
+  for (int s = 0; s < S; s++) {
+    const bool ts = (c.trk >> s) & 1u;
     ok &= !ts || id[s] != 0;
 #pragma unroll
-    for (int t = s + 1; t < kCCMax; t++) {
-      const bool tt = static_cast<uint32_t>(t) < S && ((c.trk >> t) & 1u);
+    for (int t = s + 1; t < S; t++) {
+      const bool tt = (c.trk >> t) & 1u;
       ok &= !(ts && tt && id[s] == id[t]);
     }
   }
@@ -60,22 +60,24 @@ __device__ __forceinline__ bool cc_invariants(const CCState &c, const uint64_t (
 }
 
 // Slot bit of tracked peer `node`, 0 if it has no Progress.
+template <int S>
 __device__ __forceinline__ uint32_t cc_find(const uint64_t (&id)[kCCMax], uint32_t trk,
                                             uint64_t node) {
   uint32_t m = 0;
 #pragma unroll
-  for (int s = 0; s < kCCMax; s++) m |= (((trk >> s) & 1u) && id[s] == node) ? (1u << s) : 0u;
+  for (int s = 0; s < S; s++) m |= (((trk >> s) & 1u) && id[s] == node) ? (1u << s) : 0u;
   return m & (0u - m);
 }
 
 // initProgress (:251-274): the lowest untracked slot gets the peer.
-__device__ __forceinline__ int cc_init(CCState &c, uint64_t (&id)[kCCMax], uint32_t full,
-                                       uint64_t node, bool learner) {
-  const uint32_t free = ~c.trk & full;
+template <int S>
+__device__ __forceinline__ int cc_init(CCState &c, uint64_t (&id)[kCCMax], uint64_t node,
+                                       bool learner) {
+  const uint32_t free = ~c.trk & ((1u << S) - 1u);
   if (free == 0) return QE_CC_ERR_NO_SLOT;
   const uint32_t b = free & (0u - free);
 #pragma unroll
-  for (int s = 0; s < kCCMax; s++) id[s] = b == (1u << s) ? node : id[s];
+  for (int s = 0; s < S; s++) id[s] = b == (1u << s) ? node : id[s];
   c.trk |= b;
   c.newp |= b;
   if (learner) {
@@ -102,17 +104,18 @@ __device__ __forceinline__ void cc_remove(CCState &c, uint32_t b) {
 }
 
 // apply (:152-177).
+template <int S>
 __device__ __forceinline__ int cc_apply(const CCArgs &a, uint64_t g, CCState &c,
-                                        uint64_t (&id)[kCCMax], uint32_t full) {
+                                        uint64_t (&id)[kCCMax]) {
   const uint32_t n = a.count[g] < a.C ? a.count[g] : a.C;
   for (uint32_t k = 0; k < n; k++) {
     const uint64_t node = a.node[k * a.stride + g];
     const uint32_t typ = a.type[k * a.stride + g];
     if (node == 0) continue;  // etcd's "do not apply" marker (:154-160)
-    const uint32_t b = cc_find(id, c.trk, node);
+    const uint32_t b = cc_find<S>(id, c.trk, node);
     if (typ == QE_CC_ADD_NODE) {  // makeVoter (:181-193)
       if (b == 0) {
-        const int rc = cc_init(c, id, full, node, false);
+        const int rc = cc_init<S>(c, id, node, false);
         if (rc) return rc;
       } else {
         c.isl &= ~b;
@@ -122,7 +125,7 @@ __device__ __forceinline__ int cc_apply(const CCArgs &a, uint64_t g, CCState &c,
       }
     } else if (typ == QE_CC_ADD_LEARNER_NODE) {  // makeLearner (:207-231)
       if (b == 0) {
-        const int rc = cc_init(c, id, full, node, true);
+        const int rc = cc_init<S>(c, id, node, true);
         if (rc) return rc;
       } else if ((c.isl & b) == 0) {
         // remove(), but the Progress is put back (prs[id] = pr)
@@ -145,11 +148,12 @@ __device__ __forceinline__ int cc_apply(const CCArgs &a, uint64_t g, CCState &c,
   return c.inc == 0 ? QE_CC_ERR_REMOVED_ALL : QE_CC_OK;
 }
 
-template <typename MT>
+template <int S>
 __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
+  using MT = typename std::conditional<(S <= 8), uint8_t, uint16_t>::type;
   const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (g >= a.G) return;
-  const uint32_t S = a.S, full = (1u << S) - 1u;
+  constexpr uint32_t full = (1u << S) - 1u;
   const uint32_t op = a.op[g];
   if (op == QE_CC_OP_NONE) {
     a.result[g] = QE_CC_OK;
@@ -162,23 +166,23 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
   uint64_t id[kCCMax], id0[kCCMax];
 #pragma unroll
   for (int s = 0; s < kCCMax; s++) {
-    id[s] = static_cast<uint32_t>(s) < S ? a.ids[g * S + s] : 0;
+    id[s] = s < S ? a.ids[g * S + s] : 0;
     id0[s] = id[s];
   }
   const uint32_t inc0 = c.inc;
-  int rc = cc_invariants(c, id, S) ? QE_CC_OK : QE_CC_ERR_INVARIANT;  // checkAndCopy
+  int rc = cc_invariants<S>(c, id) ? QE_CC_OK : QE_CC_ERR_INVARIANT;  // checkAndCopy
   if (rc == QE_CC_OK) {
     if (op == QE_CC_OP_SIMPLE) {  // :130-147
       if (c.out) rc = QE_CC_ERR_SIMPLE_IN_JOINT;
-      if (rc == QE_CC_OK) rc = cc_apply(a, g, c, id, full);
+      if (rc == QE_CC_OK) rc = cc_apply<S>(a, g, c, id);
       if (rc == QE_CC_OK) {
         // symdiff of the incoming voter ids (:384-401)
         uint32_t diff = 0;
 #pragma unroll
-        for (int s = 0; s < kCCMax; s++) {
+        for (int s = 0; s < S; s++) {
           bool in_new = false, in_old = false;
 #pragma unroll
-          for (int t = 0; t < kCCMax; t++) {
+          for (int t = 0; t < S; t++) {
             in_new |= ((c.inc >> t) & 1u) && id[t] == id0[s];
             in_old |= ((inc0 >> t) & 1u) && id0[t] == id[s];
           }
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
       else if (c.inc == 0) rc = QE_CC_ERR_ZERO_VOTER_JOINT;
       if (rc == QE_CC_OK) {
         c.out = c.inc;
-        rc = cc_apply(a, g, c, id, full);
+        rc = cc_apply<S>(a, g, c, id);
         c.al = op == QE_CC_OP_ENTER_JOINT_AUTO ? 1u : 0u;
       }
     } else if (op == QE_CC_OP_LEAVE_JOINT) {  // :92-123
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
     } else {
       rc = QE_CC_ERR_BAD_TYPE;
     }
-    if (rc == QE_CC_OK && !cc_invariants(c, id, S)) rc = QE_CC_ERR_INVARIANT_OUT;
+    if (rc == QE_CC_OK && !cc_invariants<S>(c, id)) rc = QE_CC_ERR_INVARIANT_OUT;
   }
   a.result[g] = static_cast<uint8_t>(rc);
   const uint32_t created = rc == QE_CC_OK ? (c.newp & c.trk) : 0u;
@@ -226,11 +230,10 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
   st(a.trk, c.trk);
   a.auto_leave[g] = static_cast<uint8_t>(c.al);
 #pragma unroll
-  for (int s = 0; s < kCCMax; s++)
-    if (static_cast<uint32_t>(s) < S) a.ids[g * S + s] = ((c.trk >> s) & 1u) ? id[s] : 0;
+  for (int s = 0; s < S; s++) a.ids[g * S + s] = ((c.trk >> s) & 1u) ? id[s] : 0;
   if (a.p_match && created) {
     const uint64_t li = a.last_index[g];
-    for (uint32_t s = 0; s < S; s++) {
+    for (int s = 0; s < S; s++) {
       if (((created >> s) & 1u) == 0) continue;
       const uint64_t r = s * a.pstride + g;
       a.p_match[r] = 0;

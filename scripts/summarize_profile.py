@@ -31,6 +31,7 @@ DOMINANT = {
     "config4_repl": "void qe::k_repl_stream<5,",
     "config5_elec": "void qe::k_election<5,",
     "progress_step": "void qe::k_progress_step<5,",
+    "confchange": "void qe::k_confchange<",
 }
 
 
