@@ -291,6 +291,17 @@ std::vector<VoteResult> VoteResultBatch(const std::vector<JointConfig> &cfgs,
 
 namespace tracker {
 
+std::string Progress::String() const {
+  static const char *kState[] = {"StateProbe", "StateReplicate", "StateSnapshot"};
+  std::string s = std::string(kState[State <= StateSnapshot ? State : 0]) +
+                  " match=" + std::to_string(Match) + " next=" + std::to_string(Next);
+  if (IsLearner) s += " learner";
+  if (State == StateProbe && ProbeSent) s += " paused";
+  if (PendingSnapshot > 0) s += " pendingSnap=" + std::to_string(PendingSnapshot);
+  if (!RecentActive) s += " inactive";
+  return s;
+}
+
 std::string Config::String() const {
   std::string s = "voters=" + Voters.String();
   if (!Learners.empty()) s += " learners=" + quorum::MajorityConfig(Learners).String();
@@ -373,4 +384,176 @@ std::vector<bool> QuorumActiveBatch(const std::vector<const ProgressTracker *> &
 }
 
 }  // namespace tracker
+
+namespace confchange {
+
+namespace {
+
+const char *cc_error_text(int rc) {
+  switch (rc) {
+    case QE_CC_ERR_INVARIANT: return "invalid input configuration (checkInvariants)";
+    case QE_CC_ERR_ALREADY_JOINT: return "config is already joint";
+    case QE_CC_ERR_ZERO_VOTER_JOINT: return "can't make a zero-voter config joint";
+    case QE_CC_ERR_NOT_JOINT: return "can't leave a non-joint config";
+    case QE_CC_ERR_SIMPLE_IN_JOINT: return "can't apply simple config change in joint config";
+    case QE_CC_ERR_BAD_TYPE: return "unexpected conf type";
+    case QE_CC_ERR_REMOVED_ALL: return "removed all voters";
+    case QE_CC_ERR_SIMPLE_MULTI:
+      return "more than one voter changed without entering joint config";
+    case QE_CC_ERR_INVARIANT_OUT: return "invalid resulting configuration (checkInvariants)";
+    case QE_CC_ERR_NO_SLOT: return "more than 16 peers";
+  }
+  return "unknown confchange result";
+}
+
+}  // namespace
+
+// Packs every tracker into slots (its Progress ids ascending), runs
+// qe_confchange once for the batch and unpacks the results.  All groups
+// share S = the largest (peers + changes) of the batch, capped at 16.
+std::vector<Result> ChangeBatch(const std::vector<const Changer *> &changers,
+                                const std::vector<Op> &ops,
+                                const std::vector<std::vector<ConfChangeSingle>> &ccs) {
+  const uint64_t G = changers.size();
+  if (ops.size() != G || ccs.size() != G)
+    throw std::invalid_argument("ChangeBatch: ops/ccs size mismatch");
+  std::vector<Result> out(G);
+  if (G == 0) return out;
+  size_t need = 1, C = 0;
+  for (uint64_t g = 0; g < G; g++) {
+    need = std::max(need, changers[g]->Tracker.Progress.size() + ccs[g].size());
+    C = std::max(C, ccs[g].size());
+  }
+  const uint32_t S = static_cast<uint32_t>(std::min<size_t>(need, QE_MAX_SLOTS));
+  const size_t mb = qe_mask_bytes(S), Cs = std::max<size_t>(C, 1);
+  // one host image: ids | 6 masks | auto_leave | op | count | last_index |
+  // type | node | result | new_progress
+  const size_t o_ids = 0, o_m = o_ids + 8 * G * S, o_al = o_m + 6 * mb * G, o_op = o_al + G,
+               o_cnt = o_op + G, o_li = (o_cnt + G + 7) / 8 * 8, o_node = o_li + 8 * G,
+               o_type = o_node + 8 * Cs * G, o_res = o_type + Cs * G, o_np = o_res + G,
+               size = o_np + mb * G;
+  std::vector<uint8_t> h(size, 0);
+  auto put_mask = [&](int k, uint64_t g, uint32_t v) {
+    memcpy(&h[o_m + (k * G + g) * mb], &v, mb);  // little endian
+  };
+  std::vector<std::vector<uint64_t>> slot_of(G);
+  std::vector<bool> too_many(G, false);
+  for (uint64_t g = 0; g < G; g++) {
+    const tracker::ProgressTracker &t = changers[g]->Tracker;
+    if (t.Progress.size() > S) {
+      too_many[g] = true;
+      continue;
+    }
+    uint32_t m[6] = {0, 0, 0, 0, 0, 0};  // inc out lrn lnx isl trk
+    uint32_t s = 0;
+    for (const auto &kv : t.Progress) {
+      const uint64_t id = kv.first, b = 1u << s;
+      memcpy(&h[o_ids + 8 * (g * S + s)], &id, 8);
+      m[0] |= t.Voters.c[0].ids.count(id) ? b : 0;
+      m[1] |= t.Voters.c[1].ids.count(id) ? b : 0;
+      m[2] |= t.Learners.count(id) ? b : 0;
+      m[3] |= t.LearnersNext.count(id) ? b : 0;
+      m[4] |= kv.second.IsLearner ? b : 0;
+      m[5] |= b;
+      s++;
+    }
+    // set members without a Progress cannot be placed: an invalid input
+    bool orphan = false;
+    for (const auto *set : {&t.Voters.c[0].ids, &t.Voters.c[1].ids, &t.Learners, &t.LearnersNext})
+      for (uint64_t id : *set) orphan |= t.Progress.count(id) == 0;
+    for (int k = 0; k < 6; k++) put_mask(k, g, m[k]);
+    h[o_al + g] = t.AutoLeave ? 1 : 0;
+    h[o_op + g] = orphan ? 0 : static_cast<uint8_t>(ops[g]);
+    if (orphan) too_many[g] = true;  // reported below as an invariant error
+    h[o_cnt + g] = static_cast<uint8_t>(ccs[g].size());
+    memcpy(&h[o_li + 8 * g], &changers[g]->LastIndex, 8);
+    for (size_t k = 0; k < ccs[g].size(); k++) {
+      memcpy(&h[o_node + 8 * (k * G + g)], &ccs[g][k].NodeID, 8);
+      h[o_type + k * G + g] = ccs[g][k].Type;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_arena.mu);
+    uint8_t *d = static_cast<uint8_t *>(g_arena.get(size));
+    hip_check("hipMemcpy", hipMemcpy(d, h.data(), size, hipMemcpyHostToDevice));
+    qe_conf c{};
+    c.num_groups = G;
+    c.num_slots = S;
+    c.slot_ids = reinterpret_cast<uint64_t *>(d + o_ids);
+    c.inc_mask = d + o_m;
+    c.out_mask = d + o_m + mb * G;
+    c.learner_mask = d + o_m + 2 * mb * G;
+    c.learners_next_mask = d + o_m + 3 * mb * G;
+    c.is_learner = d + o_m + 4 * mb * G;
+    c.tracked = d + o_m + 5 * mb * G;
+    c.auto_leave = d + o_al;
+    qe_conf_changes x{};
+    x.max_changes = static_cast<uint32_t>(C);
+    x.stride = G;
+    x.op = d + o_op;
+    x.count = d + o_cnt;
+    x.type = d + o_type;
+    x.node_id = reinterpret_cast<const uint64_t *>(d + o_node);
+    x.last_index = reinterpret_cast<const uint64_t *>(d + o_li);
+    x.result = d + o_res;
+    x.new_progress = d + o_np;
+    check("qe_confchange", qe_confchange(&c, &x, nullptr, nullptr));
+    hip_check("hipMemcpy", hipMemcpy(h.data(), d, size, hipMemcpyDeviceToHost));
+  }
+  auto get_mask = [&](size_t off, uint64_t g) {
+    uint32_t v = 0;
+    memcpy(&v, &h[off + g * mb], mb);
+    return v;
+  };
+  for (uint64_t g = 0; g < G; g++) {
+    Result &r = out[g];
+    const Changer &ch = *changers[g];
+    const int rc = too_many[g] ? (ch.Tracker.Progress.size() > S ? QE_CC_ERR_NO_SLOT
+                                                                 : QE_CC_ERR_INVARIANT)
+                               : h[o_res + g];
+    if (rc != QE_CC_OK) {
+      r.Err = cc_error_text(rc);
+      continue;
+    }
+    const uint32_t inc = get_mask(o_m, g), outm = get_mask(o_m + mb * G, g),
+                   lrn = get_mask(o_m + 2 * mb * G, g), lnx = get_mask(o_m + 3 * mb * G, g),
+                   isl = get_mask(o_m + 4 * mb * G, g), trk = get_mask(o_m + 5 * mb * G, g),
+                   np = get_mask(o_np, g);
+    r.Config.AutoLeave = h[o_al + g] != 0;
+    for (uint32_t s = 0; s < S; s++) {
+      if (((trk >> s) & 1u) == 0) continue;
+      uint64_t id;
+      memcpy(&id, &h[o_ids + 8 * (g * S + s)], 8);
+      if ((inc >> s) & 1u) r.Config.Voters.c[0].ids.insert(id);
+      if ((outm >> s) & 1u) r.Config.Voters.c[1].ids.insert(id);
+      if ((lrn >> s) & 1u) r.Config.Learners.insert(id);
+      if ((lnx >> s) & 1u) r.Config.LearnersNext.insert(id);
+      tracker::Progress pr;
+      auto it = ch.Tracker.Progress.find(id);
+      if (((np >> s) & 1u) || it == ch.Tracker.Progress.end()) {
+        pr.Match = 0;  // initProgress (:262-273)
+        pr.Next = ch.LastIndex;
+        pr.State = tracker::StateProbe;
+        pr.RecentActive = true;
+      } else {
+        pr = it->second;
+      }
+      pr.IsLearner = (isl >> s) & 1u;
+      r.Progress[id] = pr;
+    }
+  }
+  return out;
+}
+
+Result Changer::EnterJoint(bool autoLeave, const std::vector<ConfChangeSingle> &ccs) const {
+  return ChangeBatch({this}, {autoLeave ? Op::EnterJointAutoLeave : Op::EnterJoint}, {ccs})[0];
+}
+
+Result Changer::LeaveJoint() const { return ChangeBatch({this}, {Op::LeaveJoint}, {{}})[0]; }
+
+Result Changer::Simple(const std::vector<ConfChangeSingle> &ccs) const {
+  return ChangeBatch({this}, {Op::Simple}, {ccs})[0];
+}
+
+}  // namespace confchange
 }  // namespace etcd_amd

@@ -102,6 +102,7 @@ struct Progress {
   bool RecentActive = false;
   bool ProbeSent = false;
   bool IsLearner = false;
+  std::string String() const;  // progress.go:214-236 (the fields kept here)
 };
 
 // tracker.Config (raft/tracker/tracker.go:27-78).
@@ -143,4 +144,49 @@ std::vector<TallyResult> TallyVotesBatch(const std::vector<const ProgressTracker
 std::vector<bool> QuorumActiveBatch(const std::vector<const ProgressTracker *> &pts);
 
 }  // namespace tracker
+
+namespace confchange {
+
+// raftpb.ConfChangeType (raft/raftpb/raft.pb.go:224-227).
+enum ConfChangeType : uint8_t {
+  ConfChangeAddNode = 0,
+  ConfChangeRemoveNode = 1,
+  ConfChangeUpdateNode = 2,
+  ConfChangeAddLearnerNode = 3,
+};
+
+struct ConfChangeSingle {
+  ConfChangeType Type;
+  uint64_t NodeID;
+};
+
+// (tracker.Config, tracker.ProgressMap, error) of the reference's Changer
+// methods; Err is empty on success and holds the reference's error text
+// otherwise.
+struct Result {
+  tracker::Config Config;
+  std::map<uint64_t, tracker::Progress> Progress;
+  std::string Err;
+  bool ok() const { return Err.empty(); }
+};
+
+// confchange.Changer (raft/confchange/confchange.go:31-34).  Each method runs
+// the change on the GPU (qe_confchange) for this one tracker; ChangeBatch
+// runs one change per tracker in one launch.
+class Changer {
+ public:
+  tracker::ProgressTracker Tracker;
+  uint64_t LastIndex = 0;
+  Result EnterJoint(bool autoLeave, const std::vector<ConfChangeSingle> &ccs) const;  // :49-76
+  Result LeaveJoint() const;                                                        // :92-123
+  Result Simple(const std::vector<ConfChangeSingle> &ccs) const;                    // :130-147
+};
+
+enum class Op : uint8_t { Simple = 1, EnterJoint = 2, EnterJointAutoLeave = 3, LeaveJoint = 4 };
+
+std::vector<Result> ChangeBatch(const std::vector<const Changer *> &changers,
+                                const std::vector<Op> &ops,
+                                const std::vector<std::vector<ConfChangeSingle>> &ccs);
+
+}  // namespace confchange
 }  // namespace etcd_amd

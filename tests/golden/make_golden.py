@@ -32,6 +32,7 @@ Outputs (data only: inputs + expected outputs):
   tests/golden/quorum_testdata.jsonl   127 rows
   tests/golden/raft_tables.json        the three tables
   tests/golden/confchange_testdata.json  9 files of confchange steps
+  tests/golden/confchange_testdata.txt   the same, tab-separated (C++ test)
 """
 import json
 import os
@@ -346,6 +347,13 @@ def main():
     cc = confchange_files()
     with open(os.path.join(HERE, "confchange_testdata.json"), "w", encoding="utf-8") as f:
         json.dump(cc, f, indent=1)
+    # the same steps in a tab-separated line format for the C++ test:
+    # <file> <line> <cmd> <args> <input> <expected lines joined by '|'>
+    with open(os.path.join(HERE, "confchange_testdata.txt"), "w", encoding="utf-8") as f:
+        for name, v in cc.items():
+            for st in v["steps"]:
+                f.write("\t".join([name, str(st["line"]), st["cmd"], st["args"], st["input"],
+                                   "|".join(st["expect"])]) + "\n")
     print("wrote", sum(len(v["steps"]) for v in cc.values()), "confchange steps in", len(cc), "files")
     counts = {}
     for r in rows:

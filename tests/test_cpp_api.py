@@ -26,7 +26,9 @@ def test_cpp_test_builds_and_links():
                 "etcd_amd::quorum::JointConfig::VoteResult",
                 "etcd_amd::quorum::CommittedIndexBatch",
                 "etcd_amd::tracker::ProgressTracker::TallyVotes",
-                "etcd_amd::tracker::ProgressTracker::QuorumActive"):
+                "etcd_amd::tracker::ProgressTracker::QuorumActive",
+                "etcd_amd::confchange::Changer::EnterJoint",
+                "etcd_amd::confchange::ChangeBatch"):
         assert sym in out, sym
 
 
@@ -36,3 +38,14 @@ def test_cpp_datadriven_on_gpu():
     r = subprocess.run([BIN, ROOT], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS: 127 datadriven cases, 13 election rows" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_confchange_datadriven_on_gpu():
+    """TestConfChangeDataDriven (raft/confchange/datadriven_test.go) through
+    etcd_amd::confchange::Changer and the qe_confchange kernel."""
+    _build()
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "confchange_golden_test")
+    r = subprocess.run([exe, ROOT], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS: 58 confchange steps" in r.stdout
