@@ -12,5 +12,6 @@ from .quorum import (INF, AckedIndexer, CommittedIndexBatch, Index, JointConfig,
                      VoteResultBatch, VoteWon)
 from .tracker import (CommittedBatch, MakeProgressTracker, Progress,  # noqa: F401
                       ProgressTracker, QuorumActiveBatch, TallyVotesBatch)
+from . import confchange  # noqa: F401  (raft/confchange mirror)
 
 __version__ = "0.1.0"

@@ -248,3 +248,38 @@ def test_invalid_inputs(eng):
         else:
             assert res[g] != cc.ERR_INVARIANT, g
     assert 100 < n_bad < G - 100
+
+
+def test_python_mirror_testdata():
+    """etcd_amd.confchange.Changer (the Python host mirror of the Go API)
+    replays TestConfChangeDataDriven text-identically."""
+    from etcd_amd import confchange as C
+    from etcd_amd import tracker as T
+    files = json.load(open(os.path.join(HERE, "golden", "confchange_testdata.json")))
+    kinds = {"v": C.ConfChangeAddNode, "l": C.ConfChangeAddLearnerNode,
+             "r": C.ConfChangeRemoveNode, "u": C.ConfChangeUpdateNode}
+    states = ("StateProbe", "StateReplicate", "StateSnapshot")
+    n = 0
+    for name, f in sorted(files.items()):
+        ch = C.Changer(T.MakeProgressTracker(10), 0, DEV)
+        for st in f["steps"]:
+            ccs = [C.ConfChangeSingle(kinds[t[0]], int(t[1:])) for t in st["input"].split()]
+            if st["cmd"] == "simple":
+                cfg, prs, err = ch.Simple(ccs)
+            elif st["cmd"] == "enter-joint":
+                cfg, prs, err = ch.EnterJoint("autoleave=true" in st["args"], ccs)
+            else:
+                cfg, prs, err = ch.LeaveJoint()
+            if err is not None:
+                got = [str(err)]
+            else:
+                t = ch.Tracker
+                t.Voters, t.Learners, t.LearnersNext = cfg.Voters, cfg.Learners, cfg.LearnersNext
+                t.AutoLeave, t.Progress = cfg.AutoLeave, prs
+                got = [cfg.String()] + [
+                    f"{i}: {states[p.State]} match={p.Match} next={p.Next}"
+                    + (" learner" if p.IsLearner else "") for i, p in sorted(prs.items())]
+            ch.LastIndex += 1
+            assert got == st["expect"], f"{name}:{st['line']}"
+            n += 1
+    assert n == 58
