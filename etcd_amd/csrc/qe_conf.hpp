@@ -148,27 +148,24 @@ __device__ __forceinline__ int cc_apply(const CCArgs &a, uint64_t g, CCState &c,
   return c.inc == 0 ? QE_CC_ERR_REMOVED_ALL : QE_CC_OK;
 }
 
+// One group's change.  `id` holds the group's slot IDs on entry and the
+// IDs to store on exit; returns true when the group's state changed.
 template <int S>
-__global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
+__device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (&id)[kCCMax]) {
   using MT = typename std::conditional<(S <= 8), uint8_t, uint16_t>::type;
-  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (g >= a.G) return;
   constexpr uint32_t full = (1u << S) - 1u;
   const uint32_t op = a.op[g];
   if (op == QE_CC_OP_NONE) {
     a.result[g] = QE_CC_OK;
     if (a.new_progress) static_cast<MT *>(a.new_progress)[g] = 0;
-    return;
+    return false;
   }
   auto ld = [&](const void *p) -> uint32_t { return static_cast<const MT *>(p)[g] & full; };
   CCState c{ld(a.inc), ld(a.out), ld(a.lrn), ld(a.lnx), ld(a.isl), ld(a.trk),
             a.auto_leave[g] != 0 ? 1u : 0u, 0u};
-  uint64_t id[kCCMax], id0[kCCMax];
+  uint64_t id0[kCCMax];
 #pragma unroll
-  for (int s = 0; s < kCCMax; s++) {
-    id[s] = s < S ? a.ids[g * S + s] : 0;
-    id0[s] = id[s];
-  }
+  for (int s = 0; s < kCCMax; s++) id0[s] = id[s];
   const uint32_t inc0 = c.inc;
   int rc = cc_invariants<S>(c, id) ? QE_CC_OK : QE_CC_ERR_INVARIANT;  // checkAndCopy
   if (rc == QE_CC_OK) {
@@ -220,7 +217,11 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
   a.result[g] = static_cast<uint8_t>(rc);
   const uint32_t created = rc == QE_CC_OK ? (c.newp & c.trk) : 0u;
   if (a.new_progress) static_cast<MT *>(a.new_progress)[g] = static_cast<MT>(created);
-  if (rc != QE_CC_OK) return;
+  if (rc != QE_CC_OK) {  // a failed change keeps the group's state
+#pragma unroll
+    for (int s = 0; s < kCCMax; s++) id[s] = id0[s];
+    return false;
+  }
   auto st = [&](void *p, uint32_t v) { static_cast<MT *>(p)[g] = static_cast<MT>(v); };
   st(a.inc, c.inc);
   st(a.out, c.out);
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
   st(a.trk, c.trk);
   a.auto_leave[g] = static_cast<uint8_t>(c.al);
 #pragma unroll
-  for (int s = 0; s < S; s++) a.ids[g * S + s] = ((c.trk >> s) & 1u) ? id[s] : 0;
+  for (int s = 0; s < S; s++) id[s] = ((c.trk >> s) & 1u) ? id[s] : 0;
   if (a.p_match && created) {
     const uint64_t li = a.last_index[g];
     for (int s = 0; s < S; s++) {
@@ -243,6 +244,38 @@ __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
       a.p_istart[r] = 0;
       a.p_icount[r] = 0;
     }
+  }
+  return true;
+}
+
+// The slot IDs are [G][S] (the packer's layout): a lane's S IDs sit S*8
+// bytes apart from its neighbour's.  The block stages its kBlock*S IDs
+// through LDS with consecutive-lane 8-B loads and stores (every wave
+// instruction moves one contiguous 512 B), and lanes read and write their
+// own S IDs in LDS.  IDs go back to HBM only from blocks where some group's
+// change succeeded.
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
+  __shared__ uint64_t sid[kBlock * S];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t gb = static_cast<uint64_t>(blockIdx.x) * kBlock;
+  const uint64_t left = a.G - gb;
+  const uint32_t nb = left < kBlock ? static_cast<uint32_t>(left) : kBlock;
+  const uint32_t nw = nb * S;
+  uint64_t *blk = a.ids + gb * S;
+  for (uint32_t i = tid; i < nw; i += kBlock) sid[i] = __builtin_nontemporal_load(blk + i);
+  __syncthreads();
+  uint64_t id[kCCMax];
+#pragma unroll
+  for (int s = 0; s < kCCMax; s++) id[s] = (s < S && tid < nb) ? sid[tid * S + s] : 0;
+  bool changed = false;
+  if (tid < nb) changed = cc_group<S>(a, gb + tid, id);
+  if (changed) {
+#pragma unroll
+    for (int s = 0; s < S; s++) sid[tid * S + s] = id[s];
+  }
+  if (__syncthreads_or(changed)) {
+    for (uint32_t i = tid; i < nw; i += kBlock) __builtin_nontemporal_store(sid[i], blk + i);
   }
 }
 
