@@ -254,15 +254,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
         }
         if (p.match < li) send |= 1u << s;
       }
-      // ---- stores: the peer's new Progress (unchanged words skipped) ----
+      // ---- stores: the peer's new Progress (unchanged words and bytes skipped) ----
       const uint32_t w8 = msg ? o8 : kOOB, w1 = msg ? lane : kOOB;
+      const uint32_t fl = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) | QE_PF_RECENT_ACTIVE;
       bst64(p.match, mk_rsrc(a.match + row, n * 8), updated ? o8 : kOOB);
-      bst64(p.next, mk_rsrc(a.next + row, n * 8), w8);
+      bst64(p.next, mk_rsrc(a.next + row, n * 8), p.next != cur.nx ? w8 : kOOB);
       bst64(p.pending, mk_rsrc(a.pending + row, n * 8), p.pending != cur.pd ? w8 : kOOB);
-      bst8(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) | QE_PF_RECENT_ACTIVE,
-           mk_rsrc(a.flags + row, n), w1);
-      bst8(p.start, mk_rsrc(a.istart + row, n), w1);
-      bst8(p.count, mk_rsrc(a.icount + row, n), w1);
+      bst8(fl, mk_rsrc(a.flags + row, n), fl != cur.fl ? w1 : kOOB);
+      bst8(p.start, mk_rsrc(a.istart + row, n), p.start != cur.st ? w1 : kOOB);
+      bst8(p.count, mk_rsrc(a.icount + row, n), p.count != cur.ct ? w1 : kOOB);
       if (s + 1 < S) cur = nxt;
     }
     bst64(c, r_commit, o8);
