@@ -194,6 +194,14 @@ def test_random_differential(eng, S):
     assert cc.OK in seen and cc.ERR_REMOVED_ALL in seen
 
 
+@pytest.mark.parametrize("S,G", [(5, 1), (7, 300), (16, 777)])
+def test_random_differential_ragged(eng, S, G):
+    """Ragged batches: the last block stages fewer than 256 groups' slot IDs
+    through LDS (qe_conf.hpp k_confchange)."""
+    seen = run_differential(eng, S, S, G, 8, 3000 + S)
+    assert cc.OK in seen
+
+
 @pytest.mark.parametrize("S", [3, 6, 12])
 def test_no_slot(eng, S):
     seen = run_differential(eng, S, 2 * S, 512, 10, 2000 + S, nmax=S + 2)
@@ -230,6 +238,10 @@ def test_invalid_inputs(eng):
     eng.confchange(cs, ch)
     torch.cuda.synchronize()
     res = ch.result.cpu().numpy()
+    # a failed change keeps the group's slot IDs (the block writes them back)
+    ids_after = cs.slot_ids.cpu().numpy().view(np.uint64).reshape(G, S)
+    failed = res != cc.OK
+    assert failed.any() and (ids_after[failed] == ids[failed]).all()
     state = {"slot_ids": ids, "tracked": trk, "is_learner": isl, "inc": inc, "out": out,
              "learner": lrn, "learners_next": lnx, "auto_leave": al}
     n_bad = 0
