@@ -16,6 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
+QE_ABI_VERSION = 2
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -98,17 +99,22 @@ class QeProgress(C.Structure):
         ("term_start", vp), ("first_index", vp), ("last_index", vp), ("log_runs", u32),
         ("reserved", u32), ("run_first", vp), ("run_term", vp), ("run_count", vp),
         ("inc_mask", vp), ("out_mask", vp),
+        # ABI 2
+        ("tracked", vp), ("self_slot", vp), ("lead_transferee", vp), ("snap_index", vp),
+        ("max_ents", u32), ("reserved2", u32),
     ]
 
 
 class QePeerMsgs(C.Structure):
     _fields_ = [("type", vp), ("index", vp), ("reject_hint", vp), ("log_term", vp),
-                ("send_mask", vp), ("bcast", vp)]
+                ("sent", vp), ("bcast", vp), ("snap", vp), ("timeout_now", vp),
+                ("msg_count", vp), ("msg_index", vp), ("bytes_requested", vp)]
 
 
 QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
 QE_PF_STATE, QE_PF_PROBE_SENT, QE_PF_RECENT_ACTIVE = 3, 4, 8
 QE_MSG_NONE, QE_MSG_APP_RESP, QE_MSG_APP_RESP_REJECT, QE_MSG_HEARTBEAT_RESP = 0, 1, 2, 3
+QE_MSG_SNAP_STATUS, QE_MSG_SNAP_STATUS_REJECT, QE_MSG_UNREACHABLE = 4, 5, 6
 QE_MAX_INFLIGHT = 255
 QE_MAX_LOG_RUNS = 16
 
@@ -185,7 +191,7 @@ def _load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.qe_abi_version() != 1:
+    if lib.qe_abi_version() != QE_ABI_VERSION:
         raise ImportError("etcd_amd: ABI version mismatch")
     return lib
 

@@ -352,7 +352,8 @@ int qe_apply_append_resps(uint64_t num_groups, uint32_t num_slots, uint64_t stri
 
 static int progress_args(const qe_progress *p, PArgs &a) {
   if (!p) return QE_EINVAL;
-  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved) return QE_EINVAL;
+  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
+    return QE_EINVAL;
   if (p->inflight_cap == 0 || p->inflight_cap > QE_MAX_INFLIGHT) return QE_ERANGE;
   if (p->log_runs > QE_MAX_LOG_RUNS) return QE_ERANGE;
   if (p->num_groups && p->stride < p->num_groups) return QE_EINVAL;
@@ -364,6 +365,9 @@ static int progress_args(const qe_progress *p, PArgs &a) {
     return QE_EINVAL;
   if (p->num_groups && p->log_runs && (!p->run_first || !p->run_term || !p->run_count))
     return QE_EINVAL;
+  // ring rows are addressed with 32-bit offsets per 64-group tile
+  if (static_cast<uint64_t>(p->inflight_cap) * 8 * 64 * QE_MAX_SLOTS > 0x7FFFFFFFull)
+    return QE_ERANGE;
   a = PArgs{};
   a.G = p->num_groups;
   a.goff = p->group_offset;
@@ -381,15 +385,18 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.term_start = p->term_start;
   a.first_index = p->first_index;
   a.last_index = p->last_index;
+  a.snap_index = p->snap_index;
   a.run_first = p->run_first;
   a.run_term = p->run_term;
   a.run_count = p->run_count;
   a.inc = p->inc_mask;
   a.out = p->out_mask;
+  a.tracked = p->tracked;
+  a.self_slot = p->self_slot;
+  a.transferee = p->lead_transferee;
+  a.max_ents = p->max_ents;
   return QE_OK;
 }
-
-static const uint8_t kZeroRuns[1] = {0};
 
 int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
                      void *stream) {
@@ -404,11 +411,16 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
   a.mindex = m->index;
   a.mhint = m->reject_hint;
   a.mlogterm = m->log_term;
-  a.send_mask = m->send_mask;
+  a.sent = m->sent;
   a.bcast = m->bcast;
+  a.snap = m->snap;
+  a.tnow = m->timeout_now;
+  a.msg_count = m->msg_count;
+  a.msg_index = m->msg_index;
+  a.acct = m->bytes_requested;
   a.stats = stats;
-  (void)kZeroRuns;
-  return dispatch_progress(p->num_slots, a, 0, p->inc_mask != nullptr, p->out_mask != nullptr,
+  const int kind = m->bytes_requested ? 2 : 0;
+  return dispatch_progress(p->num_slots, a, kind, p->inc_mask != nullptr, p->out_mask != nullptr,
                            static_cast<hipStream_t>(stream));
 }
 

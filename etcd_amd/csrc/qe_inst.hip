@@ -159,29 +159,4 @@ int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
-template <int RM>
-static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
-  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
-  if (joint)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM>), grid, dim3(kBlock), 0, st, a);
-  else if (masked)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM>), grid, dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM>), grid, dim3(kBlock), 0, st, a);
-  return hip_status(hipGetLastError());
-}
-
-int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
-                                     hipStream_t st) {
-  if (kind == 1) {
-    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 4)),
-                       dim3(kBlock), 0, st, a);
-    return hip_status(hipGetLastError());
-  }
-  // run table in registers: 4 runs cover the common leader log (one or two
-  // older terms before the current one); up to QE_MAX_LOG_RUNS otherwise
-  if (a.R <= 4) return launch_progress_step<4>(a, masked, joint, st);
-  return launch_progress_step<QE_MAX_LOG_RUNS>(a, masked, joint, st);
-}
-
 }  // namespace qe

@@ -1,0 +1,51 @@
+// qe_inst_prog.hip — per-slot-count instantiations of the Progress state
+// machine kernels (qe_progress.hpp).  Compiled once per S (1..16) with
+// -DQE_S=<S>, separately from qe_inst.hip so the two kernel families rebuild
+// independently.
+#include "qe_dispatch.hpp"
+
+#ifndef QE_S
+#error "compile with -DQE_S=<slots>"
+#endif
+
+namespace qe {
+
+namespace {
+constexpr int S = QE_S;
+using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
+}  // namespace
+
+#define QE_CAT2(a, b) a##b
+#define QE_CAT(a, b) QE_CAT2(a, b)
+
+template <int RM, bool ACCT>
+static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  if (joint)
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT>), grid, dim3(kBlock), 0, st, a);
+  else if (masked)
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT>), grid, dim3(kBlock), 0, st,
+                       a);
+  else
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT>), grid, dim3(kBlock), 0, st,
+                       a);
+  return hip_status(hipGetLastError());
+}
+
+// kind 0: qe_progress_step, 1: qe_progress_send, 2: qe_progress_step with
+// byte accounting (instrumented variant, measurement only)
+int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
+                                     hipStream_t st) {
+  if (kind == 1) {
+    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
+                       dim3(kBlock), 0, st, a);
+    return hip_status(hipGetLastError());
+  }
+  // run table in registers: 4 runs cover the common leader log (one or two
+  // older terms before the current one); up to QE_MAX_LOG_RUNS otherwise
+  if (kind == 2) return launch_progress_step<QE_MAX_LOG_RUNS, true>(a, masked, joint, st);
+  if (a.R <= 4) return launch_progress_step<4, false>(a, masked, joint, st);
+  return launch_progress_step<QE_MAX_LOG_RUNS, false>(a, masked, joint, st);
+}
+
+}  // namespace qe

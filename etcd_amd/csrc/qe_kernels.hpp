@@ -612,59 +612,32 @@ struct PArgs {
   uint8_t *flags, *istart, *icount;
   uint64_t *ibuf;
   uint64_t *committed;
-  const uint64_t *term_start, *first_index, *last_index;
+  const uint64_t *term_start, *first_index, *last_index, *snap_index;
   const uint64_t *run_first, *run_term;
   const uint8_t *run_count;
-  const void *inc, *out;
-  // step messages
+  const void *inc, *out, *tracked;
+  const uint8_t *self_slot, *transferee;
+  uint32_t max_ents;
+  // step messages and outputs
   const uint8_t *mtype;
   const uint64_t *mindex, *mhint, *mlogterm;
-  void *send_mask;
-  uint8_t *bcast;
+  void *sent, *snap, *tnow;
+  uint8_t *bcast, *msg_count;
+  uint64_t *msg_index, *acct;
   uint64_t *stats;
   // send
   const void *want;
-  uint32_t send_if_empty, max_ents;
-  void *sent, *snap;
+  uint32_t send_if_empty;
 };
 
 struct PR {
   uint64_t match, next, pending;
   uint32_t state, probe_sent, recent_active, start, count;
+  uint32_t reset;  // ResetState ran: PendingSnapshot must be written back
 };
 
-__device__ __forceinline__ PR pr_load(const PArgs &a, uint64_t off) {
-  PR p;
-  p.match = a.match[off];
-  p.next = a.next[off];
-  p.pending = a.pending[off];
-  const uint32_t f = a.flags[off];
-  p.state = f & QE_PF_STATE;
-  p.probe_sent = (f & QE_PF_PROBE_SENT) != 0;
-  p.recent_active = (f & QE_PF_RECENT_ACTIVE) != 0;
-  p.start = a.istart[off];
-  p.count = a.icount[off];
-  return p;
-}
-
-__device__ __forceinline__ void pr_store(const PArgs &a, uint64_t off, const PR &p) {
-  a.match[off] = p.match;
-  a.next[off] = p.next;
-  a.pending[off] = p.pending;
-  a.flags[off] = static_cast<uint8_t>(p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
-                                      (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u));
-  a.istart[off] = static_cast<uint8_t>(p.start);
-  a.icount[off] = static_cast<uint8_t>(p.count);
-}
-
-// Inflights entry k of peer (s, g): ibuf[(s*stride + g)*F + k].  A peer's
-// ring is one contiguous F*8-byte row, so FreeLE's scan touches one HBM
-// burst per 8 entries instead of one per entry.
-__device__ __forceinline__ uint64_t *infl(const PArgs &a, uint32_t s, uint64_t g, uint32_t k) {
-  return a.ibuf + (static_cast<uint64_t>(s) * a.stride + g) * a.F + k;
-}
-
 __device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:84-90
+  p.reset = 1;
   p.probe_sent = 0;
   p.pending = 0;
   p.state = st;
@@ -728,50 +701,7 @@ enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
 
 // k_progress_step: qe_progress.hpp
 
-template <int S, typename MT>
-__global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
-  constexpr uint32_t kFull = (1u << S) - 1u;
-  const MT *wantp = static_cast<const MT *>(a.want);
-  for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; g < a.G;
-       g += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    const uint32_t w = wantp[g] & kFull;
-    const uint64_t fi = a.first_index[g], li = a.last_index[g];
-    uint32_t sm = 0, sn = 0;
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      if (!((w >> s) & 1u)) continue;
-      const uint64_t off = static_cast<uint64_t>(s) * a.stride + g;
-      PR p = pr_load(a, off);
-      if (pr_paused(p, a.F)) continue;
-      if (p.next > li) {  // no entries to send
-        if (!a.send_if_empty) continue;
-        sm |= 1u << s;
-      } else if (p.next < fi) {  // entries compacted: send a snapshot
-        if (!p.recent_active) continue;
-        pr_reset(p, QE_PR_SNAPSHOT);  // BecomeSnapshot(firstIndex - 1)
-        p.pending = fi - 1;
-        sm |= 1u << s;
-        sn |= 1u << s;
-      } else {
-        uint64_t last = p.next + (a.max_ents ? a.max_ents : 1u) - 1;
-        if (last > li || last < p.next) last = li;
-        if (p.state == QE_PR_REPLICATE) {
-          p.next = last + 1;  // OptimisticUpdate
-          uint32_t nx = p.start + p.count;  // Inflights.Add
-          if (nx >= a.F) nx -= a.F;
-          *infl(a, s, g, nx) = last;
-          p.count++;
-        } else if (p.state == QE_PR_PROBE) {
-          p.probe_sent = 1;
-        }
-        sm |= 1u << s;
-      }
-      pr_store(a, off, p);
-    }
-    if (a.sent) static_cast<MT *>(a.sent)[g] = static_cast<MT>(sm);
-    if (a.snap) static_cast<MT *>(a.snap)[g] = static_cast<MT>(sn);
-  }
-}
+// k_progress_send: qe_progress.hpp
 
 // ---------------------------------------------------------------------------
 // Small bitmap kernels: QuorumActive, RecordVote.

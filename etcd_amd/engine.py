@@ -258,14 +258,18 @@ def tune(key, value):
 class ProgressState:
     """Device-resident leader-side Progress of G groups (qe_progress):
     match/next/pending [S][stride], flags, Inflights rings [S][stride][F],
-    committed, and the leader-log model (term runs)."""
+    committed, and the leader-log model (term runs).  `extras` allocates the
+    optional per-group arrays of ABI 2: "tracked" (slot mask), "self_slot",
+    "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""
 
-    def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None):
+    def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None,
+                 extras=(), max_ents=0):
         if not 1 <= S <= _lib.QE_MAX_SLOTS or not 1 <= F <= _lib.QE_MAX_INFLIGHT:
             raise ValueError("bad num_slots / inflight_cap")
         if not 1 <= R <= _lib.QE_MAX_LOG_RUNS:
             raise ValueError("bad log_runs")
         self.G, self.S, self.F, self.R = int(G), int(S), int(F), int(R)
+        self.max_ents = int(max_ents)
         self.device = torch.device(device)
         self.group_offset = int(group_offset)
         self.stride = int(stride) if stride else max(ROW_ALIGN, -(-self.G // ROW_ALIGN) * ROW_ALIGN)
@@ -288,6 +292,13 @@ class ProgressState:
         md = mask_torch_dtype(S)
         self.inc = torch.zeros(self.G, dtype=md, device=dev) if "inc" in masks else None
         self.out = torch.zeros(self.G, dtype=md, device=dev) if "out" in masks else None
+        self.tracked = torch.zeros(self.G, dtype=md, device=dev) if "tracked" in extras else None
+        self.self_slot = (torch.full((self.G,), 0xFF, dtype=u8, device=dev)
+                          if "self_slot" in extras else None)
+        self.lead_transferee = (torch.full((self.G,), 0xFF, dtype=u8, device=dev)
+                                if "lead_transferee" in extras else None)
+        self.snap_index = (torch.zeros(self.G, dtype=i64, device=dev)
+                           if "snap_index" in extras else None)
 
     def struct(self):
         return _lib.QeProgress(
@@ -295,11 +306,13 @@ class ProgressState:
             _ptr(self.next), _ptr(self.pending), _ptr(self.flags), _ptr(self.istart),
             _ptr(self.icount), _ptr(self.ibuf), _ptr(self.committed), _ptr(self.term_start),
             _ptr(self.first_index), _ptr(self.last_index), self.R, 0, _ptr(self.run_first),
-            _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out))
+            _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
+            _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
+            _ptr(self.snap_index), self.max_ents, 0)
 
     ARRAYS = ("match", "next", "pending", "flags", "istart", "icount", "ibuf", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
-              "inc", "out")
+              "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
 
     def load_host(self, **arrays):
         """numpy arrays (uint64 as uint64, masks/flags as uint8/uint16)."""
@@ -330,20 +343,30 @@ class ProgressState:
 
 
 class PeerMsgs:
-    """One round of per-peer messages for qe_progress_step ([S][stride])."""
+    """One round of per-peer messages for qe_progress_step ([S][stride]) and
+    its outputs (sent / snap / timeout_now masks and bcast count per group,
+    msg_count / msg_index per peer)."""
 
-    def __init__(self, ps):
+    def __init__(self, ps, outputs=True):
         dev, n = ps.device, ps.S * ps.stride
+        md = mask_torch_dtype(ps.S)
         self.type = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.index = torch.zeros(n, dtype=torch.int64, device=dev)
         self.reject_hint = torch.zeros(n, dtype=torch.int64, device=dev)
         self.log_term = torch.zeros(n, dtype=torch.int64, device=dev)
-        self.send_mask = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=dev)
-        self.bcast = torch.zeros(ps.G, dtype=torch.uint8, device=dev)
+        self.sent = torch.zeros(ps.G, dtype=md, device=dev) if outputs else None
+        self.bcast = torch.zeros(ps.G, dtype=torch.uint8, device=dev) if outputs else None
+        self.snap = torch.zeros(ps.G, dtype=md, device=dev) if outputs else None
+        self.timeout_now = torch.zeros(ps.G, dtype=md, device=dev) if outputs else None
+        self.msg_count = torch.zeros(n, dtype=torch.uint8, device=dev) if outputs else None
+        self.msg_index = torch.zeros(n, dtype=torch.int64, device=dev) if outputs else None
+        self.bytes_requested = None
 
     def struct(self):
         return _lib.QePeerMsgs(_ptr(self.type), _ptr(self.index), _ptr(self.reject_hint),
-                               _ptr(self.log_term), _ptr(self.send_mask), _ptr(self.bcast))
+                               _ptr(self.log_term), _ptr(self.sent), _ptr(self.bcast),
+                               _ptr(self.snap), _ptr(self.timeout_now), _ptr(self.msg_count),
+                               _ptr(self.msg_index), _ptr(self.bytes_requested))
 
 
 def progress_step(ps, msgs, stats=None):
@@ -352,7 +375,20 @@ def progress_step(ps, msgs, stats=None):
                                                            _stream(ps.device)))
 
 
-def progress_send(ps, want, send_if_empty=False, max_ents=1):
+def progress_bytes_requested(ps, msgs):
+    """Run one round through the instrumented kernel variant and return the
+    bytes it requested (reads + writes at field granularity): the
+    algorithmic bytes of that round.  Mutates the state like progress_step."""
+    acct = torch.zeros(1, dtype=torch.int64, device=ps.device)
+    msgs.bytes_requested = acct
+    try:
+        progress_step(ps, msgs)
+    finally:
+        msgs.bytes_requested = None
+    return int(acct.item())
+
+
+def progress_send(ps, want, send_if_empty=False, max_ents=0):
     sent = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
     snap = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
     p = ps.struct()

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 1
+#define QE_ABI_VERSION 2  /* 2: qe_progress / qe_peer_msgs extended (stepLeader sends) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -262,15 +262,22 @@ int qe_election_steps(const qe_election_state *st,
 
 /* message kinds of qe_peer_msgs.type (any other value: no message) */
 #define QE_MSG_NONE 0
-#define QE_MSG_APP_RESP 1         /* MsgAppResp, Reject=false                */
-#define QE_MSG_APP_RESP_REJECT 2  /* MsgAppResp, Reject=true                 */
-#define QE_MSG_HEARTBEAT_RESP 3   /* MsgHeartbeatResp                        */
+#define QE_MSG_APP_RESP 1             /* MsgAppResp, Reject=false            */
+#define QE_MSG_APP_RESP_REJECT 2      /* MsgAppResp, Reject=true             */
+#define QE_MSG_HEARTBEAT_RESP 3       /* MsgHeartbeatResp                    */
+#define QE_MSG_SNAP_STATUS 4          /* MsgSnapStatus, Reject=false         */
+#define QE_MSG_SNAP_STATUS_REJECT 5   /* MsgSnapStatus, Reject=true          */
+#define QE_MSG_UNREACHABLE 6          /* MsgUnreachable                      */
 
 /* Leader-side Progress of every peer of G groups (raft/tracker/progress.go:
  * 30-80) plus the leader's log model: term runs r < run_count[g] covering
  * [run_first[r], run_first[r+1]) with run_term[r] (run 0 starts at the
  * snapshot/dummy index = first_index - 1), ending at last_index; the current
- * term's entries are [term_start, last_index]. */
+ * term's entries are [term_start, last_index].  Entries exist in
+ * [first_index, last_index]; max_ents models MaxSizePerMsg for equal-size
+ * entries (entries per MsgApp, at least one; 0 = noLimit).  Inflights.start
+ * must be < inflight_cap (results are unspecified otherwise; memory stays in
+ * bounds). */
 typedef struct qe_progress {
   uint64_t num_groups;
   uint64_t group_offset;
@@ -295,38 +302,76 @@ typedef struct qe_progress {
   const uint8_t *run_count;     /* [G] valid runs, 1..R                       */
   const void *inc_mask;         /* [G] as in qe_groups (NULL = all slots)    */
   const void *out_mask;         /* [G] or NULL                               */
+  /* ABI 2 */
+  const void *tracked;          /* [G] slots holding a Progress (ProgressMap
+                                   keys); NULL = every slot                  */
+  const uint8_t *self_slot;     /* [G] the leader's own slot (bcastAppend
+                                   skips it); NULL or >= S = none            */
+  const uint8_t *lead_transferee; /* [G] slot of r.leadTransferee; NULL or
+                                   >= S = no transfer in progress            */
+  const uint64_t *snap_index;   /* [G] index of the snapshot a MsgSnap
+                                   carries; NULL = first_index - 1           */
+  uint32_t max_ents;            /* entries per MsgApp (0 = noLimit)          */
+  uint32_t reserved2;
 } qe_progress;
 
 /* One round of peer responses: message of slot s for group g at
- * [s*stride + g]. */
+ * [s*stride + g].  Outputs may be NULL. */
 typedef struct qe_peer_msgs {
   const uint8_t *type;          /* QE_MSG_*                                  */
   const uint64_t *index;        /* m.Index                                   */
   const uint64_t *reject_hint;  /* m.RejectHint                              */
   const uint64_t *log_term;     /* m.LogTerm                                 */
-  void *send_mask;              /* [G] out: slots sendAppend(m.From) ran for */
-  uint8_t *bcast;               /* [G] out: maybeCommit advanced -> bcastAppend */
+  void *sent;                   /* [G] out: slots sent >= 1 MsgApp/MsgSnap   */
+  uint8_t *bcast;               /* [G] out: bcastAppend calls (commit advances) */
+  void *snap;                   /* [G] out: slots sent a MsgSnap             */
+  void *timeout_now;            /* [G] out: slots sent MsgTimeoutNow         */
+  uint8_t *msg_count;           /* [S][stride] out: MsgApp/MsgSnap sent to the
+                                   peer this round (saturates at 255)        */
+  uint64_t *msg_index;          /* [S][stride] out: m.Index of the first of
+                                   them (MsgSnap: the snapshot index);
+                                   written only where msg_count > 0          */
+  uint64_t *bytes_requested;    /* measurement aid, normally NULL: when set,
+                                   an instrumented kernel adds the bytes the
+                                   round reads and writes (field granularity)
+                                   to *bytes_requested                       */
 } qe_peer_msgs;
 
 /* Leader-side handling of one message per peer, slots in ascending order
- * (raft/raft.go:1106-1296): RecentActive; reject -> findConflictByTerm
- * (raft/log.go:147-168) + MaybeDecrTo (progress.go:170-193), Replicate ->
- * BecomeProbe, sendAppend; accept -> IsPaused, MaybeUpdate, Probe ->
- * BecomeReplicate / Snapshot caught up -> BecomeProbe+BecomeReplicate /
- * Replicate -> Inflights.FreeLE, maybeCommit (bcast) else sendAppend if it
- * was paused; heartbeat response -> ProbeSent=false, FreeFirstOne when the
- * inflights are full, sendAppend if Match < lastIndex.  An accept with
- * index > lastIndex is invalid input: ignored and counted as an invariant
- * violation. */
+ * (stepLeader, raft/raft.go:1099-1338), with every send the reference makes
+ * while handling the message executed in place:
+ *   MsgAppResp reject: RecentActive; findConflictByTerm (raft/log.go:147-168)
+ *     when LogTerm > 0; MaybeDecrTo (progress.go:170-193) -> Replicate ->
+ *     BecomeProbe, sendAppend.
+ *   MsgAppResp accept: RecentActive; IsPaused; MaybeUpdate -> Probe ->
+ *     BecomeReplicate / Snapshot caught up -> BecomeProbe + BecomeReplicate /
+ *     Replicate -> Inflights.FreeLE; maybeCommit -> bcastAppend (every tracked
+ *     slot but self_slot) or sendAppend if it was paused; then
+ *     `for maybeSendAppend(from, false) {}`; MsgTimeoutNow to the lead
+ *     transferee once its Match == lastIndex (raft.go:1275-1281).
+ *   MsgHeartbeatResp: RecentActive, ProbeSent = false, FreeFirstOne when the
+ *     inflights are full, sendAppend if Match < lastIndex.
+ *   MsgSnapStatus (StateSnapshot only): reject -> PendingSnapshot = 0;
+ *     BecomeProbe; ProbeSent = true (raft.go:1310-1331).
+ *   MsgUnreachable: Replicate -> BecomeProbe (raft.go:1332-1338).
+ * A send is raft.maybeSendAppend (raft.go:432-492) on the log model; see
+ * qe_progress_send.  Messages from untracked slots are dropped.  An accept
+ * with index > lastIndex is processed as the reference does and counted as
+ * an invariant violation. */
 int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
                      void *stream);
 
-/* raft.maybeSendAppend (raft/raft.go:432-492) for the slots of want[g]:
- * skip paused peers; Next > lastIndex sends an empty MsgApp only when
- * send_if_empty; Next < firstIndex sends a snapshot to recently active peers
- * (BecomeSnapshot(firstIndex-1)); otherwise up to max_ents entries:
- * Replicate -> OptimisticUpdate + Inflights.Add, Probe -> ProbeSent.
- * sent / snap (mask-typed [G], may be NULL) report the outcome. */
+/* raft.sendAppend / maybeSendAppend(to, send_if_empty) once for the slots of
+ * want[g] (raft.go:432-492; bcastAppend after a proposal is want = every
+ * tracked slot but the leader's, send_if_empty = 1): paused peers get
+ * nothing; with no entries to send (Next > lastIndex, or Next < firstIndex
+ * where entries() fails with ErrCompacted) nothing is sent unless
+ * send_if_empty -- this check comes before the snapshot branch; Next >
+ * lastIndex sends an empty MsgApp; Next < firstIndex sends a MsgSnap to a
+ * recently active peer (BecomeSnapshot(snap_index)); otherwise up to
+ * max_ents entries (0 = noLimit): Replicate -> OptimisticUpdate +
+ * Inflights.Add, Probe -> ProbeSent.  sent / snap (mask-typed [G], may be
+ * NULL) report the outcome. */
 int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
                      uint32_t max_ents, void *sent, void *snap, void *stream);
 

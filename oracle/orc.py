@@ -57,9 +57,8 @@ def _declare(L):
         "orc_gf_run": (dbl, [vp, vp, vp, i32, i32]),
         "orc_soa_run": (dbl, [u64, u32, u64, vp, vp, vp, vp, vp, vp, vp, i32, i32]),
         "orc_max_threads": (i32, []),
-        "orc_progress_step_batch": (None, [u64, u64, u32, u32, u64] + [vp] * 10 + [u32]
-                                    + [vp] * 12 + [i32]),
-        "orc_progress_send_batch": (None, [u64, u32, u32, u64] + [vp] * 10 + [u32, u32, vp, vp]),
+        "orc_progress_step_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcMsgs), vp, i32]),
+        "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
         "orc_pr_maybe_decr_to": (i32, [u32, vp, vp, u64, u64]),
@@ -152,12 +151,40 @@ def max_threads():
     return lib().orc_max_threads()
 
 
-class ProgressBatch:
-    """Host mirror of qe_progress (numpy arrays, same layout)."""
+class OrcProg(C.Structure):
+    """orc_prog (oracle/quorum_oracle.c), the oracle's mirror of qe_progress."""
+    _fields_ = [
+        ("G", C.c_uint64), ("goff", C.c_uint64), ("S", C.c_uint32), ("F", C.c_uint32),
+        ("stride", C.c_uint64), ("match", C.c_void_p), ("next", C.c_void_p),
+        ("pending", C.c_void_p), ("flags", C.c_void_p), ("istart", C.c_void_p),
+        ("icount", C.c_void_p), ("ibuf", C.c_void_p), ("committed", C.c_void_p),
+        ("term_start", C.c_void_p), ("first_index", C.c_void_p), ("last_index", C.c_void_p),
+        ("R", C.c_uint32), ("reserved", C.c_uint32), ("run_first", C.c_void_p),
+        ("run_term", C.c_void_p), ("run_count", C.c_void_p), ("inc", C.c_void_p),
+        ("out", C.c_void_p), ("tracked", C.c_void_p), ("self_slot", C.c_void_p),
+        ("lead_transferee", C.c_void_p), ("snap_index", C.c_void_p), ("max_ents", C.c_uint32),
+        ("reserved2", C.c_uint32),
+    ]
 
-    def __init__(self, G, S, F, R, stride=None):
+
+class OrcMsgs(C.Structure):
+    _fields_ = [("type", C.c_void_p), ("index", C.c_void_p), ("hint", C.c_void_p),
+                ("logterm", C.c_void_p), ("sent", C.c_void_p), ("bcast", C.c_void_p),
+                ("snap", C.c_void_p), ("timeout_now", C.c_void_p), ("msg_count", C.c_void_p),
+                ("msg_index", C.c_void_p)]
+
+
+class ProgressBatch:
+    """Host mirror of qe_progress (numpy arrays, same layout).  Optional
+    per-group arrays (tracked, self_slot, lead_transferee, snap_index) are
+    None unless set."""
+
+    OPTIONAL = ("inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
+
+    def __init__(self, G, S, F, R, stride=None, max_ents=0):
         self.G, self.S, self.F, self.R = G, S, F, R
         self.stride = stride or G
+        self.max_ents = max_ents
         n = S * self.stride
         self.match = np.zeros(n, np.uint64)
         self.next = np.ones(n, np.uint64)
@@ -173,8 +200,8 @@ class ProgressBatch:
         self.run_first = np.zeros(max(R, 1) * self.stride, np.uint64)
         self.run_term = np.zeros(max(R, 1) * self.stride, np.uint64)
         self.run_count = np.zeros(G, np.uint8)
-        self.inc = None
-        self.out = None
+        for k in self.OPTIONAL:
+            setattr(self, k, None)
 
     def copy(self):
         c = ProgressBatch.__new__(ProgressBatch)
@@ -182,25 +209,43 @@ class ProgressBatch:
             setattr(c, k, v.copy() if isinstance(v, np.ndarray) else v)
         return c
 
+    def struct(self, goff=0):
+        return OrcProg(self.G, goff, self.S, self.F, self.stride, P(self.match), P(self.next),
+                       P(self.pending), P(self.flags), P(self.istart), P(self.icount),
+                       P(self.ibuf), P(self.committed), P(self.term_start), P(self.first_index),
+                       P(self.last_index), self.R, 0, P(self.run_first), P(self.run_term),
+                       P(self.run_count), P(self.inc), P(self.out), P(self.tracked),
+                       P(self.self_slot), P(self.lead_transferee), P(self.snap_index),
+                       self.max_ents, 0)
+
+
+class StepOut:
+    """Outputs of one oracle progress_step round."""
+
+    def __init__(self, pb):
+        md = mask_dtype(pb.S)
+        self.sent = np.zeros(pb.G, md)
+        self.bcast = np.zeros(pb.G, np.uint8)
+        self.snap = np.zeros(pb.G, md)
+        self.timeout_now = np.zeros(pb.G, md)
+        self.msg_count = np.zeros(pb.S * pb.stride, np.uint8)
+        self.msg_index = np.zeros(pb.S * pb.stride, np.uint64)
+        self.stats = np.zeros(NSTAT, np.uint64)
+
 
 def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0):
-    send = np.zeros(pb.G, mask_dtype(pb.S))
-    bcast = np.zeros(pb.G, np.uint8)
-    stats = np.zeros(NSTAT, np.uint64)
-    lib().orc_progress_step_batch(
-        pb.G, goff, pb.S, pb.F, pb.stride, P(pb.match), P(pb.next), P(pb.pending), P(pb.flags),
-        P(pb.istart), P(pb.icount), P(pb.ibuf), P(pb.committed), P(pb.term_start),
-        P(pb.last_index), pb.R, P(pb.run_first), P(pb.run_term),
-        P(pb.run_count), P(pb.inc), P(pb.out), P(mtype), P(mindex), P(mhint), P(mlogterm),
-        P(send), P(bcast), P(stats), threads)
-    return send, bcast, stats
+    """One round of stepLeader message handling (oracle).  Returns StepOut."""
+    o = StepOut(pb)
+    m = OrcMsgs(P(mtype), P(mindex), P(mhint), P(mlogterm), P(o.sent), P(o.bcast), P(o.snap),
+                P(o.timeout_now), P(o.msg_count), P(o.msg_index))
+    s = pb.struct(goff)
+    lib().orc_progress_step_batch(C.byref(s), C.byref(m), P(o.stats), threads)
+    return o
 
 
 def progress_send(pb, want, send_if_empty, max_ents):
     sent = np.zeros(pb.G, mask_dtype(pb.S))
     snap = np.zeros(pb.G, mask_dtype(pb.S))
-    lib().orc_progress_send_batch(
-        pb.G, pb.S, pb.F, pb.stride, P(pb.match), P(pb.next), P(pb.pending), P(pb.flags),
-        P(pb.istart), P(pb.icount), P(pb.ibuf), P(pb.first_index), P(pb.last_index), P(want),
-        send_if_empty, max_ents, P(sent), P(snap))
+    s = pb.struct()
+    lib().orc_progress_send_batch(C.byref(s), P(want), send_if_empty, max_ents, P(sent), P(snap))
     return sent, snap

@@ -892,30 +892,122 @@ uint64_t orc_find_conflict_by_term(uint32_t nruns, const uint64_t *first, const 
   return index;
 }
 
-static void pr_load(orc_pr *p, uint64_t off, uint64_t stride, uint32_t F, uint64_t *match,
-                    uint64_t *next, uint64_t *pending, uint8_t *pflags, uint8_t *istart,
-                    uint8_t *icount, uint64_t *ibuf, uint32_t s, uint64_t g) {
-  p->match = match[off];
-  p->next = next[off];
-  p->pending = pending[off];
-  p->state = pflags[off] & PF_STATE;
-  p->probe_sent = (pflags[off] & PF_PROBE_SENT) != 0;
-  p->recent_active = (pflags[off] & PF_RECENT_ACTIVE) != 0;
-  p->start = istart[off];
-  p->count = icount[off];
-  p->size = F;
-  p->buf = ibuf + ((uint64_t)s * stride + g) * F; /* ring row [S][stride][F] */
+/* The leader-side state of G groups (mirrors qe_progress of
+ * include/etcd_quorum.h, ABI 2) and one round of peer messages (mirrors
+ * qe_peer_msgs).  Slot s of group g lives at [s*stride + g]; the Inflights
+ * ring of that peer is ibuf[(s*stride + g)*F .. +F). */
+typedef struct orc_prog {
+  uint64_t G, goff;
+  uint32_t S, F;
+  uint64_t stride;
+  uint64_t *match, *next, *pending;
+  uint8_t *flags, *istart, *icount;
+  uint64_t *ibuf;
+  uint64_t *committed;
+  const uint64_t *term_start, *first_index, *last_index;
+  uint32_t R, reserved;
+  const uint64_t *run_first, *run_term;
+  const uint8_t *run_count;
+  const void *inc, *out;
+  const void *tracked;            /* NULL: every slot holds a Progress      */
+  const uint8_t *self_slot;       /* NULL / >= S: the leader has no slot    */
+  const uint8_t *lead_transferee; /* NULL / >= S: no transfer in progress   */
+  const uint64_t *snap_index;     /* NULL: first_index - 1                  */
+  uint32_t max_ents, reserved2;   /* entries per MsgApp, 0 = noLimit        */
+} orc_prog;
+
+typedef struct orc_msgs {
+  const uint8_t *type;
+  const uint64_t *index, *hint, *logterm;
+  void *sent;          /* [G] slots sent >= 1 MsgApp/MsgSnap              */
+  uint8_t *bcast;      /* [G] bcastAppend calls (commit advances)         */
+  void *snap;          /* [G] slots sent a MsgSnap                        */
+  void *timeout_now;   /* [G] slots sent MsgTimeoutNow                    */
+  uint8_t *msg_count;  /* [S][stride] messages sent to the peer           */
+  uint64_t *msg_index; /* [S][stride] m.Index of the first of them        */
+} orc_msgs;
+
+/* message kinds (qe_peer_msgs.type) */
+enum { M_NONE = 0, M_APP_RESP, M_APP_RESP_REJECT, M_HEARTBEAT_RESP, M_SNAP_STATUS,
+       M_SNAP_STATUS_REJECT, M_UNREACHABLE };
+
+static void pr_load2(orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
+  uint64_t off = s * a->stride + g;
+  p->match = a->match[off];
+  p->next = a->next[off];
+  p->pending = a->pending[off];
+  p->state = a->flags[off] & PF_STATE;
+  p->probe_sent = (a->flags[off] & PF_PROBE_SENT) != 0;
+  p->recent_active = (a->flags[off] & PF_RECENT_ACTIVE) != 0;
+  p->start = a->istart[off];
+  p->count = a->icount[off];
+  p->size = a->F;
+  p->buf = a->ibuf + off * a->F;
   p->bstride = 1;
 }
-static void pr_store(const orc_pr *p, uint64_t off, uint64_t *match, uint64_t *next,
-                     uint64_t *pending, uint8_t *pflags, uint8_t *istart, uint8_t *icount) {
-  match[off] = p->match;
-  next[off] = p->next;
-  pending[off] = p->pending;
-  pflags[off] = (uint8_t)(p->state | (p->probe_sent ? PF_PROBE_SENT : 0) |
-                          (p->recent_active ? PF_RECENT_ACTIVE : 0));
-  istart[off] = (uint8_t)p->start;
-  icount[off] = (uint8_t)p->count;
+static void pr_store2(const orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
+  uint64_t off = s * a->stride + g;
+  a->match[off] = p->match;
+  a->next[off] = p->next;
+  a->pending[off] = p->pending;
+  a->flags[off] = (uint8_t)(p->state | (p->probe_sent ? PF_PROBE_SENT : 0) |
+                            (p->recent_active ? PF_RECENT_ACTIVE : 0));
+  a->istart[off] = (uint8_t)p->start;
+  a->icount[off] = (uint8_t)p->count;
+}
+
+/* Per-group context of one round: the log model and the message record. */
+typedef struct orc_gctx {
+  const orc_prog *a;
+  const orc_msgs *m;
+  uint64_t g, fi, li, snap;
+  uint32_t me, sent, snapm;
+} orc_gctx;
+
+static void rec_msg(orc_gctx *c, uint32_t s, uint64_t index) {
+  uint64_t off = s * c->a->stride + c->g;
+  if (c->m && c->m->msg_count) {
+    if (c->m->msg_count[off] == 0 && c->m->msg_index) c->m->msg_index[off] = index;
+    if (c->m->msg_count[off] < 255) c->m->msg_count[off]++;
+  }
+  c->sent |= 1u << s;
+}
+
+/* raft.maybeSendAppend (raft/raft.go:432-492) on the log model: entries
+ * exist in [first_index, last_index]; term(i) never fails (log.go:265-271
+ * returns 0, nil outside [dummy, last]), entries(Next) is (nil, nil) for
+ * Next > lastIndex (:287-291) and ErrCompacted for Next < firstIndex
+ * (:381-388).  The `len(ents) == 0 && !sendIfEmpty` return (:442-444) comes
+ * BEFORE the snapshot branch (:446-469).  max_ents models MaxSizePerMsg for
+ * equal-size entries (limitSize keeps at least one entry); 0 = noLimit. */
+static int send_append(orc_gctx *c, orc_pr *p, uint32_t s, int send_if_empty) {
+  if (pr_is_paused(p)) return 0;                       /* :434-436 */
+  if (p->next > c->li) {                               /* no entries */
+    if (!send_if_empty) return 0;
+    rec_msg(c, s, p->next - 1);                        /* empty MsgApp (commit) */
+    return 1;
+  }
+  if (p->next < c->fi) {                               /* ErrCompacted */
+    if (!send_if_empty) return 0;                      /* :442-444 */
+    if (!p->recent_active) return 0;                   /* :447-450 */
+    pr_become_snapshot(p, c->snap);                    /* :468 */
+    rec_msg(c, s, c->snap);
+    c->snapm |= 1u << s;
+    return 1;
+  }
+  uint64_t last = c->li;
+  if (c->me) {
+    uint64_t l = p->next + (c->me - 1);
+    if (l >= p->next && l < last) last = l;
+  }
+  rec_msg(c, s, p->next - 1);                          /* MsgApp Index = Next-1 */
+  if (p->state == PR_REPLICATE) {                      /* :478-482 */
+    p->next = last + 1;                                /* OptimisticUpdate */
+    infl_add(p, last);
+  } else if (p->state == PR_PROBE) {                   /* :483-484 */
+    p->probe_sent = 1;
+  }
+  return 1;
 }
 
 uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast) {
@@ -923,20 +1015,33 @@ uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint
   return orc_mix64((gid * PHI) ^ committed ^ tag);
 }
 
-/* One round of leader-side message handling per group (raft/raft.go:
- * 1106-1296), messages taken in slot order.  type: 0 none, 1 MsgAppResp,
- * 2 MsgAppResp reject, 3 MsgHeartbeatResp.  Accepts with index > lastIndex
- * are invalid input: counted as invariant violations and ignored. */
-void orc_progress_step_batch(uint64_t G, uint64_t goff, uint32_t S, uint32_t F, uint64_t stride,
-                             uint64_t *match, uint64_t *next, uint64_t *pending, uint8_t *pflags,
-                             uint8_t *istart, uint8_t *icount, uint64_t *ibuf, uint64_t *committed,
-                             const uint64_t *term_start, const uint64_t *last_index, uint32_t R,
-                             const uint64_t *run_first, const uint64_t *run_term,
-                             const uint8_t *run_count, const void *inc, const void *out,
-                             const uint8_t *mtype, const uint64_t *mindex, const uint64_t *mhint,
-                             const uint64_t *mlogterm, void *send_mask, uint8_t *bcast,
-                             uint64_t *stats, int threads) {
-  uint32_t mb = S <= 8 ? 1 : 2;
+/* One round of leader-side message handling per group, messages taken in
+ * slot order (stepLeader, raft/raft.go:1099-1338), sends executed inline
+ * exactly where the reference executes them:
+ *   MsgAppResp reject  RecentActive; findConflictByTerm (log.go:147-168)
+ *                      when LogTerm > 0; MaybeDecrTo -> (Replicate ->
+ *                      BecomeProbe), sendAppend                 :1107-1236
+ *   MsgAppResp accept  RecentActive; oldPaused; MaybeUpdate -> Probe ->
+ *                      BecomeReplicate / Snapshot caught up -> BecomeProbe
+ *                      + BecomeReplicate / Replicate -> FreeLE; maybeCommit
+ *                      -> bcastAppend (every other peer, sendIfEmpty), else
+ *                      sendAppend if oldPaused; then
+ *                      `for maybeSendAppend(from, false) {}`; MsgTimeoutNow
+ *                      to the lead transferee once Match == lastIndex
+ *                                                               :1237-1282
+ *   MsgHeartbeatResp   RecentActive, ProbeSent = false, FreeFirstOne when
+ *                      the inflights are full, sendAppend if Match <
+ *                      lastIndex                                :1284-1294
+ *   MsgSnapStatus      in StateSnapshot only: (reject -> PendingSnapshot =
+ *                      0), BecomeProbe, ProbeSent = true        :1310-1331
+ *   MsgUnreachable     Replicate -> BecomeProbe                 :1332-1338
+ * A message from a slot without a Progress is dropped (:1100-1104).  The
+ * commit gate is raftLog.maybeCommit on the log model (term(i) == Term <=>
+ * term_start <= i <= last_index, log.go:325-331).  An accept beyond
+ * lastIndex is processed as the reference does and also counted as an
+ * invariant violation (a follower cannot ack entries the leader lacks). */
+void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *stats, int threads) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
   uint32_t full = (1u << S) - 1u;
   uint64_t st[NSTAT];
   memset(st, 0, sizeof(st));
@@ -948,73 +1053,103 @@ void orc_progress_step_batch(uint64_t G, uint64_t goff, uint32_t S, uint32_t F, 
     uint64_t ls[NSTAT];
     memset(ls, 0, sizeof(ls));
 #pragma omp for schedule(static)
-    for (int64_t gi = 0; gi < (int64_t)G; gi++) {
+    for (int64_t gi = 0; gi < (int64_t)a->G; gi++) {
       uint64_t g = (uint64_t)gi;
-      uint32_t mi = inc ? ld_mask(inc, mb, g) & full : full;
-      uint32_t mo = out ? ld_mask(out, mb, g) & full : 0;
-      uint64_t li = last_index[g], ts = term_start[g], c = committed[g];
-      uint32_t nr = run_count[g] < R ? run_count[g] : R;
+      orc_gctx c;
+      c.a = a;
+      c.m = m;
+      c.g = g;
+      c.fi = a->first_index[g];
+      c.li = a->last_index[g];
+      c.snap = a->snap_index ? a->snap_index[g] : c.fi - 1;
+      c.me = a->max_ents;
+      c.sent = c.snapm = 0;
+      uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+      uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+      uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+      uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+      uint32_t lt = a->lead_transferee ? a->lead_transferee[g] : 0xFFu;
+      uint64_t ts = a->term_start[g], li = c.li, cm = a->committed[g], c0 = cm;
+      uint32_t nr = a->run_count[g] < a->R ? a->run_count[g] : a->R;
       uint64_t rf[16], rt[16];
       for (uint32_t r = 0; r < nr; r++) {
-        rf[r] = run_first[r * stride + g];
-        rt[r] = run_term[r * stride + g];
+        rf[r] = a->run_first[r * a->stride + g];
+        rt[r] = a->run_term[r * a->stride + g];
       }
+      orc_pr prs[16];
       uint64_t vals[16];
-      for (uint32_t s = 0; s < S; s++) vals[s] = match[s * stride + g];
-      uint32_t send = 0, bc = 0;
       for (uint32_t s = 0; s < S; s++) {
-        uint64_t off = s * stride + g;
-        uint32_t ty = mtype[off];
-        if (ty == 0 || ty > 3) continue; /* no message / unknown kind: ignored */
-        orc_pr p;
-        pr_load(&p, off, stride, F, match, next, pending, pflags, istart, icount, ibuf, s, g);
-        p.recent_active = 1;
-        if (ty == 2) { /* MsgAppResp reject, raft.go:1109-1236 */
-          uint64_t probe = mhint[off];
-          if (mlogterm[off] > 0)
-            probe = orc_find_conflict_by_term(nr, rf, rt, li, mhint[off], mlogterm[off]);
-          if (pr_maybe_decr_to(&p, mindex[off], probe)) {
-            if (p.state == PR_REPLICATE) pr_become_probe(&p);
-            send |= 1u << s; /* sendAppend(m.From) */
-          }
-        } else if (ty == 1) { /* MsgAppResp accept, raft.go:1237-1282 */
-          if (mindex[off] > li) {
-            ls[ST_VIOLATIONS] += 1;
-          } else {
-            int old_paused = pr_is_paused(&p);
-            if (pr_maybe_update(&p, mindex[off])) {
-              if (p.state == PR_PROBE) {
-                pr_become_replicate(&p);
-              } else if (p.state == PR_SNAPSHOT && p.match >= p.pending) {
-                pr_become_probe(&p);
-                pr_become_replicate(&p);
-              } else if (p.state == PR_REPLICATE) {
-                infl_free_le(&p, mindex[off]);
-              }
-              vals[s] = p.match;
-              uint64_t mci = orc_joint_committed(S, mi, mo, vals);
-              if (orc_maybe_commit(mci, &c, ts, li)) {
-                bc = 1; /* releasePendingReadIndexMessages + bcastAppend */
-              } else if (old_paused) {
-                send |= 1u << s;
-              }
-            }
-          }
-        } else if (ty == 3) { /* MsgHeartbeatResp, raft.go:1284-1296 */
-          p.probe_sent = 0;
-          if (p.state == PR_REPLICATE && infl_full(&p)) infl_free_le(&p, *ib(&p, p.start));
-          if (p.match < li) send |= 1u << s;
-        }
-        pr_store(&p, off, match, next, pending, pflags, istart, icount);
+        pr_load2(&prs[s], a, s, g);
+        if (m->msg_count) m->msg_count[s * a->stride + g] = 0;
       }
-      uint64_t c0 = committed[g];
-      committed[g] = c;
-      if (send_mask) st_mask(send_mask, mb, g, send);
-      if (bcast) bcast[g] = (uint8_t)bc;
+      uint32_t bc = 0, tnow = 0;
+      for (uint32_t s = 0; s < S; s++) {
+        if (!((trk >> s) & 1u)) continue; /* no Progress: dropped */
+        uint64_t off = s * a->stride + g;
+        uint32_t ty = m->type[off];
+        orc_pr *p = &prs[s];
+        if (ty == M_APP_RESP_REJECT) {
+          p->recent_active = 1;
+          uint64_t probe = m->hint[off];
+          if (m->logterm[off] > 0)
+            probe = orc_find_conflict_by_term(nr, rf, rt, li, m->hint[off], m->logterm[off]);
+          if (pr_maybe_decr_to(p, m->index[off], probe)) {
+            if (p->state == PR_REPLICATE) pr_become_probe(p);
+            send_append(&c, p, s, 1);
+          }
+        } else if (ty == M_APP_RESP) {
+          p->recent_active = 1;
+          uint64_t idx = m->index[off];
+          if (idx > li) ls[ST_VIOLATIONS] += 1;
+          int old_paused = pr_is_paused(p);
+          if (pr_maybe_update(p, idx)) {
+            if (p->state == PR_PROBE) {
+              pr_become_replicate(p);
+            } else if (p->state == PR_SNAPSHOT && p->match >= p->pending) {
+              pr_become_probe(p);
+              pr_become_replicate(p);
+            } else if (p->state == PR_REPLICATE) {
+              infl_free_le(p, idx);
+            }
+            for (uint32_t q = 0; q < S; q++) vals[q] = prs[q].match;
+            uint64_t mci = orc_joint_committed(S, mi, mo, vals);
+            if (orc_maybe_commit(mci, &cm, ts, li)) {
+              if (bc < 255) bc++;
+              /* bcastAppend: every Progress but the leader's own (:515-522) */
+              for (uint32_t q = 0; q < S; q++)
+                if (((trk >> q) & 1u) && q != self) send_append(&c, &prs[q], q, 1);
+            } else if (old_paused) {
+              send_append(&c, p, s, 1);
+            }
+            while (send_append(&c, p, s, 0)) {
+            }
+            if (s == lt && p->match == li) tnow |= 1u << s; /* sendTimeoutNow */
+          }
+        } else if (ty == M_HEARTBEAT_RESP) {
+          p->recent_active = 1;
+          p->probe_sent = 0;
+          if (p->state == PR_REPLICATE && infl_full(p)) infl_free_le(p, *ib(p, p->start));
+          if (p->match < li) send_append(&c, p, s, 1);
+        } else if (ty == M_SNAP_STATUS || ty == M_SNAP_STATUS_REJECT) {
+          if (p->state == PR_SNAPSHOT) {
+            if (ty == M_SNAP_STATUS_REJECT) p->pending = 0;
+            pr_become_probe(p);
+            p->probe_sent = 1;
+          }
+        } else if (ty == M_UNREACHABLE) {
+          if (p->state == PR_REPLICATE) pr_become_probe(p);
+        }
+      }
+      for (uint32_t s = 0; s < S; s++) pr_store2(&prs[s], a, s, g);
+      a->committed[g] = cm;
+      if (m->sent) st_mask(m->sent, mb, g, c.sent);
+      if (m->snap) st_mask(m->snap, mb, g, c.snapm);
+      if (m->timeout_now) st_mask(m->timeout_now, mb, g, tnow);
+      if (m->bcast) m->bcast[g] = (uint8_t)bc;
       ls[ST_GROUPS] += 1;
-      ls[ST_COMMIT_SUM] += c;
-      ls[ST_COMMIT_ADVANCED] += (c != c0);
-      ls[ST_CHECKSUM] += orc_checksum_step(goff + g, c, send, bc);
+      ls[ST_COMMIT_SUM] += cm;
+      ls[ST_COMMIT_ADVANCED] += (cm != c0);
+      ls[ST_CHECKSUM] += orc_checksum_step(a->goff + g, cm, c.sent, bc);
     }
 #pragma omp critical
     for (int k = 0; k < NSTAT; k++) st[k] += ls[k];
@@ -1023,48 +1158,33 @@ void orc_progress_step_batch(uint64_t G, uint64_t goff, uint32_t S, uint32_t F, 
     for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
 }
 
-/* raft.maybeSendAppend (raft/raft.go:432-492) for the slots in want[g]:
- * entries exist in [first_index, last_index] (first_index - 1 is the
- * snapshot index); at most max_ents entries per MsgApp. */
-void orc_progress_send_batch(uint64_t G, uint32_t S, uint32_t F, uint64_t stride, uint64_t *match,
-                             uint64_t *next, uint64_t *pending, uint8_t *pflags, uint8_t *istart,
-                             uint8_t *icount, uint64_t *ibuf, const uint64_t *first_index,
-                             const uint64_t *last_index, const void *want, uint32_t send_if_empty,
+/* raft.sendAppend / maybeSendAppend(to, send_if_empty) once for every slot
+ * of want[g] (bcastAppend after a proposal, raft.go:515-522, or a single
+ * sendAppend), see send_append above.  sent / snap report the outcome. */
+void orc_progress_send_batch(const orc_prog *a, const void *want, uint32_t send_if_empty,
                              uint32_t max_ents, void *sent, void *snap) {
-  uint32_t mb = S <= 8 ? 1 : 2;
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
   uint32_t full = (1u << S) - 1u;
-  for (uint64_t g = 0; g < G; g++) {
-    uint32_t w = ld_mask(want, mb, g) & full, sm = 0, sn = 0;
-    uint64_t fi = first_index[g], li = last_index[g];
+  for (uint64_t g = 0; g < a->G; g++) {
+    orc_gctx c;
+    c.a = a;
+    c.m = NULL;
+    c.g = g;
+    c.fi = a->first_index[g];
+    c.li = a->last_index[g];
+    c.snap = a->snap_index ? a->snap_index[g] : c.fi - 1;
+    c.me = max_ents;
+    c.sent = c.snapm = 0;
+    uint32_t w = ld_mask(want, mb, g) & full;
     for (uint32_t s = 0; s < S; s++) {
       if (!((w >> s) & 1u)) continue;
-      uint64_t off = s * stride + g;
       orc_pr p;
-      pr_load(&p, off, stride, F, match, next, pending, pflags, istart, icount, ibuf, s, g);
-      if (pr_is_paused(&p)) continue;
-      if (p.next > li) { /* no entries */
-        if (!send_if_empty) continue;
-        sm |= 1u << s;
-      } else if (p.next < fi) { /* entries compacted -> snapshot */
-        if (!p.recent_active) continue;
-        pr_become_snapshot(&p, fi - 1);
-        sm |= 1u << s;
-        sn |= 1u << s;
-      } else {
-        uint64_t last = p.next + (max_ents ? max_ents : 1) - 1;
-        if (last > li || last < p.next) last = li;
-        if (p.state == PR_REPLICATE) {
-          p.next = last + 1; /* OptimisticUpdate */
-          infl_add(&p, last);
-        } else if (p.state == PR_PROBE) {
-          p.probe_sent = 1;
-        }
-        sm |= 1u << s;
-      }
-      pr_store(&p, off, match, next, pending, pflags, istart, icount);
+      pr_load2(&p, a, s, g);
+      send_append(&c, &p, s, (int)send_if_empty);
+      pr_store2(&p, a, s, g);
     }
-    if (sent) st_mask(sent, mb, g, sm);
-    if (snap) st_mask(snap, mb, g, sn);
+    if (sent) st_mask(sent, mb, g, c.sent);
+    if (snap) st_mask(snap, mb, g, c.snapm);
   }
 }
 

@@ -33,6 +33,13 @@ Outputs (data only: inputs + expected outputs):
   tests/golden/raft_tables.json        the three tables
   tests/golden/confchange_testdata.json  9 files of confchange steps
   tests/golden/confchange_testdata.txt   the same, tab-separated (C++ test)
+  tests/golden/progress_scenarios.json  leader-side Progress scenarios:
+    TestLeaderAppResp (table), TestSendAppendForProgressProbe/Replicate/
+    Snapshot, TestLeaderIncreaseNext, TestRecvMsgUnreachable,
+    TestMsgAppRespWaitReset, TestProvideSnap, TestIgnoreProvidingSnap,
+    raft_snap_test.go's five tests, and the leader side of
+    TestLeaderTransferToSlowFollower -- state set up by the tests' code is
+    restated per scenario (see progress_scenarios()).
 """
 import json
 import os
@@ -282,6 +289,208 @@ def fast_log_rejection_table():
                       "-> rejection -> next MsgApp)", "rows": rows}
 
 
+# ---------------------------------------------------------------------------
+# Leader-side Progress scenarios (stepLeader + maybeSendAppend).  These tests
+# build their state with code (newTestRaft, becomeLeader, restore ...) rather
+# than tables, so each scenario below restates the state that code produces
+# (raft.go reset :590-619, becomeLeader :724-758, appendEntry :621-642,
+# restore) for a single group: slot s is node id s+1, slot 0 is the leader.
+# Inflights capacity: the tests use 256 (newTestConfig); the slot model caps it
+# at 255, and no scenario fills the ring.  max_ents 0 = noLimit (the tests'
+# MaxSizePerMsg).  Expectations are exactly what each test asserts, except
+# where a scenario says "derived" (then they follow the test's message flow).
+# ---------------------------------------------------------------------------
+def _peer(match, nxt, state, probe_sent=False, recent_active=False, pending=0, ring=()):
+    return {"match": match, "next": nxt, "state": STATES[state], "probe_sent": probe_sent,
+            "recent_active": recent_active, "pending": pending, "ring": list(ring)}
+
+
+def leader_app_resp_rows():
+    b = _body("raft_test.go", "TestLeaderAppResp")
+    rows = [(int(a), r == "true", int(wm), int(wn), int(k), int(wi), int(wc))
+            for a, r, wm, wn, k, wi, wc in re.findall(
+                r"\{(\d+), (true|false), (\d+), (\d+), (\d+), (\d+), (\d+)\},", b)]
+    assert len(rows) == 4, rows
+    return rows
+
+
+def progress_scenarios():
+    sc = []
+    # TestLeaderAppResp (raft_test.go:2426-2480): log [1:t0, 2:t1] in storage,
+    # becomeCandidate -> Term 1, becomeLeader appends 3:t1.  Peers reset to
+    # Match 0 / Next 3 (Probe); the leader's own Progress Match 3 (Replicate).
+    for i, (idx, rej, wm, wn, k, wi, wc) in enumerate(leader_app_resp_rows()):
+        exp = {"peers": {"1": {"match": wm, "next": wn}}, "messages": k, "committed": wc}
+        if k:
+            exp["msg_index_all"] = wi
+        sc.append({
+            "name": f"TestLeaderAppResp#{i}", "source": "raft/raft_test.go:2426-2480",
+            "S": 3, "self": 0, "max_ents": 0,
+            "log": {"first_index": 1, "last_index": 3, "term_start": 2, "committed": 0,
+                    "runs": [[0, 0], [2, 1]]},
+            "peers": [_peer(3, 4, "StateReplicate"), _peer(0, 3, "StateProbe"),
+                      _peer(0, 3, "StateProbe")],
+            "steps": [{"op": "step", "msgs": {"1": {"type": "reject" if rej else "accept",
+                                                    "index": idx, "hint": idx}},
+                       "expect": exp}]})
+    # TestSendAppendForProgressProbe (raft_test.go:2613-2678): fresh log,
+    # becomeLeader appends 1:t1; node 2 in StateProbe, Next 1.
+    steps = [{"op": "append"}, {"op": "send", "want": [1], "send_if_empty": 1,
+                                 "expect": {"sent": [1], "peers": {"1": {"probe_sent": True}}}}]
+    for _ in range(3):
+        for _ in range(10):
+            steps += [{"op": "append"}, {"op": "send", "want": [1], "send_if_empty": 1,
+                                          "expect": {"sent": []}}]
+        steps += [{"op": "check", "expect": {"peers": {"1": {"probe_sent": True}}}}]
+    steps += [{"op": "step", "msgs": {"1": {"type": "heartbeat"}},
+               "expect": {"messages": 1, "msg_index": {"1": 0},
+                          "peers": {"1": {"probe_sent": True}}}}]
+    base = {"S": 2, "self": 0, "max_ents": 0,
+            "log": {"first_index": 1, "last_index": 1, "term_start": 1, "committed": 0,
+                    "runs": [[0, 0], [1, 1]]}}
+    sc.append(dict(base, name="TestSendAppendForProgressProbe",
+                   source="raft/raft_test.go:2613-2678",
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateProbe")], steps=steps))
+    # TestSendAppendForProgressReplicate (:2680-2695): BecomeReplicate -> Next 1
+    steps = []
+    for _ in range(10):
+        steps += [{"op": "append"}, {"op": "send", "want": [1], "send_if_empty": 1,
+                                      "expect": {"sent": [1]}}]
+    sc.append(dict(base, name="TestSendAppendForProgressReplicate",
+                   source="raft/raft_test.go:2680-2695",
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateReplicate")],
+                   steps=steps))
+    # TestSendAppendForProgressSnapshot (:2697-2712): BecomeSnapshot(10)
+    steps = []
+    for _ in range(10):
+        steps += [{"op": "append"}, {"op": "send", "want": [1], "send_if_empty": 1,
+                                      "expect": {"sent": []}}]
+    sc.append(dict(base, name="TestSendAppendForProgressSnapshot",
+                   source="raft/raft_test.go:2697-2712",
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateSnapshot", pending=10)],
+                   steps=steps))
+    # TestLeaderIncreaseNext (:2581-2611): log 1..3:t1, Term 1, becomeLeader
+    # appends 4:t1; node 2 forced to (state, Next 2); MsgProp appends 5 ->
+    # bcastAppend.
+    b = _body("raft_test.go", "TestLeaderIncreaseNext")
+    rows = re.findall(r"\{tracker\.(State\w+), (\d+), ([^}]+)\}", b)
+    assert len(rows) == 2, rows
+    for st, nxt, want in rows:
+        want = eval(want.replace("uint64(len(previousEnts) + 1 + 1 + 1)", "3 + 1 + 1 + 1"))
+        sc.append({"name": f"TestLeaderIncreaseNext/{st}", "source": "raft/raft_test.go:2581-2611",
+                   "S": 2, "self": 0, "max_ents": 0,
+                   "log": {"first_index": 1, "last_index": 4, "term_start": 1, "committed": 0,
+                           "runs": [[0, 0], [1, 1]]},
+                   "peers": [_peer(4, 5, "StateReplicate"), _peer(0, int(nxt), st)],
+                   "steps": [{"op": "append"},
+                             {"op": "send", "want": [1], "send_if_empty": 1,
+                              "expect": {"peers": {"1": {"next": want}}}}]})
+    # TestRecvMsgUnreachable (:2714-2735): log 1..3:t1 + 4:t1; node 2 Match 3,
+    # BecomeReplicate (Next 4), OptimisticUpdate(5) (Next 6).
+    sc.append({"name": "TestRecvMsgUnreachable", "source": "raft/raft_test.go:2714-2735",
+               "S": 2, "self": 0, "max_ents": 0,
+               "log": {"first_index": 1, "last_index": 4, "term_start": 1, "committed": 0,
+                       "runs": [[0, 0], [1, 1]]},
+               "peers": [_peer(4, 5, "StateReplicate"), _peer(3, 6, "StateReplicate")],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "unreachable"}},
+                          "expect": {"peers": {"1": {"state": 0, "next": 4}}}}]})
+    # TestMsgAppRespWaitReset (:1407-1465): 3 peers, becomeLeader appends 1:t1;
+    # bcastAppend probes nodes 2 and 3; node 2 acks 1 (commit 1); MsgProp
+    # appends 2 and broadcasts (only node 2 is not paused); node 3 acks 1.
+    sc.append({"name": "TestMsgAppRespWaitReset", "source": "raft/raft_test.go:1407-1465",
+               "S": 3, "self": 0, "max_ents": 0,
+               "log": {"first_index": 1, "last_index": 1, "term_start": 1, "committed": 0,
+                       "runs": [[0, 0], [1, 1]]},
+               "peers": [_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateProbe"),
+                         _peer(0, 1, "StateProbe")],
+               "steps": [{"op": "send", "want": [1, 2], "send_if_empty": 1, "expect": {}},
+                         {"op": "step", "msgs": {"1": {"type": "accept", "index": 1}},
+                          "expect": {"committed": 1}},
+                         {"op": "append"},
+                         {"op": "send", "want": [1, 2], "send_if_empty": 1,
+                          "expect": {"sent": [1]}},
+                         {"op": "step", "msgs": {"2": {"type": "accept", "index": 1}},
+                          "expect": {"messages": 1, "msg_index": {"2": 1}}}]})
+    # Snapshot tests: restore(snapshot index 11, term 11) -> committed 11,
+    # firstIndex 12, lastIndex 11; becomeCandidate Term 1; becomeLeader appends
+    # 12:t1 (node 2: Match 0, Next 12, Probe).
+    snap_log = {"first_index": 12, "last_index": 12, "term_start": 12, "committed": 11,
+                "runs": [[11, 11], [12, 1]], "snap_index": 11}
+    lead = _peer(12, 13, "StateReplicate")
+    # TestProvideSnap (:2986-3014) / TestSendingSnapshotSetPendingSnapshot
+    # (raft_snap_test.go:33-49): Next forced to firstIndex; rejection of Index
+    # Next-1 (hint 0) -> MaybeDecrTo -> Next 1 -> sendAppend -> MsgSnap.
+    sc.append({"name": "TestProvideSnap", "source": "raft/raft_test.go:2986-3014",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log,
+               "peers": [lead, _peer(0, 12, "StateProbe")],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "reject", "index": 11}},
+                          "expect": {"messages": 1, "snap": [1]}}]})
+    sc.append({"name": "TestSendingSnapshotSetPendingSnapshot",
+               "source": "raft/raft_snap_test.go:33-49",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log,
+               "peers": [lead, _peer(0, 12, "StateProbe")],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "reject", "index": 11}},
+                          "expect": {"peers": {"1": {"pending": 11}}}}]})
+    # TestIgnoreProvidingSnap (:3016-3043): Next = firstIndex-1, not
+    # RecentActive; MsgProp -> bcastAppend sends nothing.
+    sc.append({"name": "TestIgnoreProvidingSnap", "source": "raft/raft_test.go:3016-3043",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log,
+               "peers": [lead, _peer(0, 11, "StateProbe")],
+               "steps": [{"op": "append"},
+                         {"op": "send", "want": [1], "send_if_empty": 1,
+                          "expect": {"sent": []}}]})
+    # TestPendingSnapshotPauseReplication (raft_snap_test.go:51-66)
+    sc.append({"name": "TestPendingSnapshotPauseReplication",
+               "source": "raft/raft_snap_test.go:51-66",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log,
+               "peers": [lead, _peer(0, 12, "StateSnapshot", pending=11)],
+               "steps": [{"op": "append"},
+                         {"op": "send", "want": [1], "send_if_empty": 1,
+                          "expect": {"sent": []}}]})
+    # TestSnapshotFailure / Succeed / Abort (raft_snap_test.go:68-141): node 2
+    # Next 1, BecomeSnapshot(11).
+    snap_peer = _peer(0, 1, "StateSnapshot", pending=11)
+    sc.append({"name": "TestSnapshotFailure", "source": "raft/raft_snap_test.go:68-89",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log, "peers": [lead, snap_peer],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "snap_status_reject"}},
+                          "expect": {"peers": {"1": {"pending": 0, "next": 1,
+                                                     "probe_sent": True}}}}]})
+    sc.append({"name": "TestSnapshotSucceed", "source": "raft/raft_snap_test.go:91-112",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log, "peers": [lead, snap_peer],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "snap_status"}},
+                          "expect": {"peers": {"1": {"pending": 0, "next": 12,
+                                                     "probe_sent": True}}}}]})
+    sc.append({"name": "TestSnapshotAbort", "source": "raft/raft_snap_test.go:114-141",
+               "S": 2, "self": 0, "max_ents": 0, "log": snap_log, "peers": [lead, snap_peer],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "accept", "index": 11}},
+                          "expect": {"peers": {"1": {"pending": 0, "next": 13,
+                                                     "inflights": 1}}}}]})
+    # TestLeaderTransferToSlowFollower (:3523-3541), leader side, derived from
+    # the test's message flow: entries 1, 2 (Term 1) committed; node 3 missed
+    # entry 2 (Match 1, Next 3, entry 2 in flight).  MsgTransferLeader ->
+    # sendAppend(3) (empty MsgApp at Index 2); node 3 rejects (hint 1, log term
+    # 1) -> Probe at Index 1; node 3 acks 2 -> Match == lastIndex ->
+    # MsgTimeoutNow (the test then finds the leader stepped down for node 3).
+    sc.append({"name": "TestLeaderTransferToSlowFollower (leader side, derived)",
+               "source": "raft/raft_test.go:3523-3541, raft.go:1275-1281",
+               "S": 3, "self": 0, "max_ents": 0, "transferee": 2,
+               "log": {"first_index": 1, "last_index": 2, "term_start": 1, "committed": 2,
+                       "runs": [[0, 0], [1, 1]]},
+               "peers": [_peer(2, 3, "StateReplicate"),
+                         _peer(2, 3, "StateReplicate", recent_active=True),
+                         _peer(1, 3, "StateReplicate", recent_active=True, ring=[2])],
+               "steps": [{"op": "send", "want": [2], "send_if_empty": 1, "expect": {"sent": [2]}},
+                         {"op": "step", "msgs": {"2": {"type": "reject", "index": 2, "hint": 1,
+                                                       "logterm": 1}},
+                          "expect": {"messages": 1, "msg_index": {"2": 1}, "timeout_now": [],
+                                     "peers": {"2": {"state": 0, "next": 2,
+                                                     "probe_sent": True}}}},
+                         {"op": "step", "msgs": {"2": {"type": "accept", "index": 2}},
+                          "expect": {"timeout_now": [2],
+                                     "peers": {"2": {"state": 1, "match": 2, "next": 3}}}}]})
+    return sc
+
+
 def confchange_files():
     """datadriven blocks: `cmd [args]`, input lines, `----`, output up to a
     blank line."""
@@ -339,6 +548,8 @@ def main():
     }
     with open(os.path.join(HERE, "raft_tables.json"), "w", encoding="utf-8") as f:
         json.dump(tables, f, indent=1)
+    with open(os.path.join(HERE, "progress_scenarios.json"), "w", encoding="utf-8") as f:
+        json.dump(progress_scenarios(), f, indent=1)
     # election table in a line format for the C++ test: <size> <state> id:0|1,..
     with open(os.path.join(HERE, "election_table.txt"), "w", encoding="utf-8") as f:
         for r in tables["TestLeaderElectionInOneRoundRPC"]["rows"]:

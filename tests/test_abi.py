@@ -56,7 +56,9 @@ int main(void) {
   Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
   Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
   Z(qe_progress) F(qe_progress, infl_buf) F(qe_progress, log_runs) F(qe_progress, out_mask)
-  Z(qe_peer_msgs) F(qe_peer_msgs, bcast)
+  F(qe_progress, tracked) F(qe_progress, snap_index) F(qe_progress, max_ents)
+  Z(qe_peer_msgs) F(qe_peer_msgs, bcast) F(qe_peer_msgs, timeout_now) F(qe_peer_msgs, msg_index)
+  F(qe_peer_msgs, bytes_requested)
   Z(qe_conf) F(qe_conf, slot_ids) F(qe_conf, tracked) F(qe_conf, auto_leave)
   Z(qe_conf_changes) F(qe_conf_changes, stride) F(qe_conf_changes, node_id)
   F(qe_conf_changes, new_progress)
@@ -89,7 +91,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == 1
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 2
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0

@@ -1,16 +1,20 @@
 """GPU parity of the Progress state machine (qe_progress_step /
 qe_progress_send) against the oracle, which
-tests/test_progress_oracle.py pins to the reference's tables."""
+tests/test_progress_oracle.py pins to the reference's tables and to the
+leader-side scenarios of tests/golden/progress_scenarios.json.  The same
+scenarios run here through the HIP kernels."""
 import numpy as np
 import pytest
 import torch
 
 from oracle import orc
 from tests.golden_util import raft_tables
+from tests.progress_scenarios import F_CAP, peer_view, run_scenario, scenarios
 from tests.test_progress_oracle import log_runs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
+EXTRAS = ("tracked", "self_slot", "lead_transferee", "snap_index")
 
 
 @pytest.fixture(scope="module")
@@ -20,8 +24,8 @@ def eng():
     return engine
 
 
-def random_state(rng, G, S, F, R, masks):
-    pb = orc.ProgressBatch(G, S, F, R)
+def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
+    pb = orc.ProgressBatch(G, S, F, R, max_ents=max_ents)
     # leader log: runs over [dummy, last]
     for g in range(G):
         nr = int(rng.integers(1, R + 1))
@@ -42,6 +46,9 @@ def random_state(rng, G, S, F, R, masks):
     pb.match[:] = (rng.random(n) * (li + 1)).astype(np.uint64)
     pb.next[:] = pb.match + rng.integers(1, 4, n).astype(np.uint64)
     pb.next[rng.random(n) < 0.05] = 0  # edge: Next = 0 (MaybeDecrTo wrap)
+    fi = np.tile(pb.first_index, S)
+    low = rng.random(n) < 0.08  # compacted: Next < firstIndex (snapshot path)
+    pb.next[low] = (rng.random(int(low.sum())) * fi[low]).astype(np.uint64)
     pb.pending[:] = rng.integers(0, 70, n).astype(np.uint64)
     pb.flags[:] = (rng.integers(0, 3, n) | (rng.integers(0, 2, n) * 4) |
                    (rng.integers(0, 2, n) * 8)).astype(np.uint8)
@@ -56,12 +63,23 @@ def random_state(rng, G, S, F, R, masks):
         pb.inc = rng.integers(0, 1 << S, G).astype(md)
     if "out" in masks:
         pb.out = rng.integers(0, 1 << S, G).astype(md)
+    if "tracked" in extras:
+        t = rng.integers(0, 1 << S, G)
+        t[rng.random(G) < 0.5] = (1 << S) - 1
+        pb.tracked = t.astype(md)
+    if "self_slot" in extras:
+        pb.self_slot = rng.integers(0, S + 2, G).astype(np.uint8)  # >= S: no self
+    if "lead_transferee" in extras:
+        pb.lead_transferee = np.where(rng.random(G) < 0.5, 0xFF,
+                                      rng.integers(0, S, G)).astype(np.uint8)
+    if "snap_index" in extras:
+        pb.snap_index = (pb.first_index - 1 + rng.integers(0, 3, G)).astype(np.uint64)
     return pb
 
 
 def random_msgs(rng, pb):
     n = pb.S * pb.G
-    mtype = rng.integers(0, 5, n).astype(np.uint8)  # 4 = unknown kind -> ignored
+    mtype = rng.integers(0, 8, n).astype(np.uint8)  # 7 = unknown kind -> ignored
     li = np.tile(pb.last_index, pb.S)
     mindex = np.where(rng.random(n) < 0.5, pb.next - 1,
                       (rng.random(n) * (li + 3)).astype(np.uint64)).astype(np.uint64)
@@ -70,13 +88,15 @@ def random_msgs(rng, pb):
     return mtype, mindex, mhint, mlogterm
 
 
-def to_device(eng, pb, masks):
-    ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride)
+def to_device(eng, pb, masks, extras=()):
+    ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride,
+                           extras=extras, max_ents=pb.max_ents)
     ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, flags=pb.flags,
                  istart=pb.istart, icount=pb.icount, ibuf=pb.ibuf, committed=pb.committed,
                  term_start=pb.term_start, first_index=pb.first_index, last_index=pb.last_index,
                  run_first=pb.run_first, run_term=pb.run_term, run_count=pb.run_count,
-                 inc=pb.inc, out=pb.out)
+                 inc=pb.inc, out=pb.out, tracked=pb.tracked, self_slot=pb.self_slot,
+                 lead_transferee=pb.lead_transferee, snap_index=pb.snap_index)
     return ps
 
 
@@ -84,38 +104,55 @@ def assert_same(ps, pb):
     h = ps.host()
     for k in ("match", "next", "pending", "flags", "istart", "icount", "committed"):
         np.testing.assert_array_equal(h[k], getattr(pb, k), err_msg=k)
-    # inflight buffers: compare the live ring entries only (freed slots keep
-    # stale values in both, but compare everything anyway: identical ops)
     np.testing.assert_array_equal(h["ibuf"], pb.ibuf, err_msg="ibuf")
 
 
-@pytest.mark.parametrize("S,masks", [(1, ()), (3, ()), (5, ()), (5, ("inc",)),
-                                     (7, ("inc", "out")), (10, ("inc", "out")), (16, ("inc",))])
-def test_progress_rounds_match_oracle(eng, S, masks):
-    rng = np.random.default_rng(100 + S)
+def load_msgs(eng, ps, mtype, mindex, mhint, mlogterm):
+    msgs = eng.PeerMsgs(ps)
+    for name, a in (("type", mtype), ("index", mindex), ("reject_hint", mhint),
+                    ("log_term", mlogterm)):
+        t = torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(DEV)
+        getattr(msgs, name)[: t.numel()].copy_(t)
+    return msgs
+
+
+def assert_outputs(msgs, o, S):
+    md = orc.mask_dtype(S)
+    for k in ("sent", "snap", "timeout_now"):
+        np.testing.assert_array_equal(getattr(msgs, k).cpu().numpy().view(md), getattr(o, k),
+                                      err_msg=k)
+    np.testing.assert_array_equal(msgs.bcast.cpu().numpy(), o.bcast, err_msg="bcast")
+    cnt = msgs.msg_count.cpu().numpy()
+    np.testing.assert_array_equal(cnt, o.msg_count, err_msg="msg_count")
+    got_ix = msgs.msg_index.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got_ix[cnt > 0], o.msg_index[cnt > 0], err_msg="msg_index")
+
+
+CASES = [(1, (), ()), (3, (), EXTRAS), (5, (), ()), (5, (), EXTRAS), (5, ("inc",), EXTRAS),
+         (7, ("inc", "out"), EXTRAS), (10, ("inc", "out"), ()), (16, ("inc",), EXTRAS)]
+
+
+@pytest.mark.parametrize("S,masks,extras", CASES)
+def test_progress_rounds_match_oracle(eng, S, masks, extras):
+    rng = np.random.default_rng(100 + S + 7 * len(extras))
     G, F, R = 3001, 8, 6
-    pb = random_state(rng, G, S, F, R, masks)
-    ps = to_device(eng, pb, masks)
+    pb = random_state(rng, G, S, F, R, masks, extras, max_ents=int(rng.integers(0, 4)))
+    ps = to_device(eng, pb, masks, extras)
     for rnd in range(6):
         mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
-        msgs = eng.PeerMsgs(ps)
-        for name, a in (("type", mtype), ("index", mindex), ("reject_hint", mhint),
-                        ("log_term", mlogterm)):
-            t = torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(DEV)
-            getattr(msgs, name).copy_(t)
+        msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
         stats = eng.stats_buffer(DEV)
         eng.progress_step(ps, msgs, stats)
         got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
-        send, bcast, ostats = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
         assert_same(ps, pb)
+        assert_outputs(msgs, o, S)
+        np.testing.assert_array_equal(got, o.stats)
+        # a sendAppend / bcastAppend round to random peers
         md = orc.mask_dtype(S)
-        np.testing.assert_array_equal(msgs.send_mask.cpu().numpy().view(md), send)
-        np.testing.assert_array_equal(msgs.bcast.cpu().numpy(), bcast)
-        np.testing.assert_array_equal(got, ostats)
-        # send appends to the peers the step asked for (plus random others)
-        want = (send | rng.integers(0, 1 << S, G).astype(md)).astype(md)
+        want = rng.integers(0, 1 << S, G).astype(md)
         tw = torch.from_numpy(want.view(np.int16) if S > 8 else want).to(DEV)
-        sei, me = int(rnd % 2), int(rng.integers(1, 5))
+        sei, me = int(rnd % 2), int(rng.integers(0, 5))
         sent, snap = eng.progress_send(ps, tw, sei, me)
         o_sent, o_snap = orc.progress_send(pb, want, sei, me)
         np.testing.assert_array_equal(sent.cpu().numpy().view(md), o_sent)
@@ -123,7 +160,94 @@ def test_progress_rounds_match_oracle(eng, S, masks):
         assert_same(ps, pb)
 
 
+def test_progress_long_rings_and_bcasts(eng):
+    """F = 32 > the 8-entry prefetch (FreeLE continues from memory), small
+    max_ents so the send loop fills rings, and every accept advancing the
+    commit (bcasts to every peer from several slots)."""
+    rng = np.random.default_rng(77)
+    G, S, F, R = 2000, 5, 32, 4
+    pb = random_state(rng, G, S, F, R, (), EXTRAS, max_ents=1)
+    pb.term_start[:] = 0
+    pb.flags[:] = 1 | 8  # Replicate, RecentActive
+    ps = to_device(eng, pb, (), EXTRAS)
+    for _ in range(4):
+        n = S * G
+        mtype = np.where(rng.random(n) < 0.8, 1, 3).astype(np.uint8)
+        li = np.tile(pb.last_index, S)
+        mindex = np.minimum(pb.match + rng.integers(0, 30, n).astype(np.uint64), li)
+        z = np.zeros(n, np.uint64)
+        msgs = load_msgs(eng, ps, mtype, mindex, z, z)
+        eng.progress_step(ps, msgs)
+        o = orc.progress_step(pb, mtype, mindex, z, z)
+        assert_same(ps, pb)
+        assert_outputs(msgs, o, S)
+        assert int(o.bcast.sum()) > G // 2  # bcasts in most groups
+        pb.last_index[:] += 40  # the leader appends
+        ps.last_index.copy_(torch.from_numpy(pb.last_index.view(np.int64)).to(DEV))
+
+
+class GpuBackend:
+    """tests/progress_scenarios.py backend over the HIP engine (one group)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+
+    def load(self, sc, a):
+        # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
+        ps = self.eng.ProgressState(1, sc["S"], F_CAP, len(sc["log"]["runs"]), DEV, stride=1,
+                                    extras=EXTRAS, max_ents=sc["max_ents"])
+        ps.tracked = None  # every slot holds a Progress (as the oracle backend)
+        if "snap_index" not in a:
+            ps.snap_index = None
+        ps.load_host(**a)
+        self.ps, self.sc = ps, sc
+
+    def step(self, t, idx, hint, lt):
+        msgs = load_msgs(self.eng, self.ps, t, idx, hint, lt)
+        self.eng.progress_step(self.ps, msgs)
+        return {"sent": int(msgs.sent[0]), "snap": int(msgs.snap[0]),
+                "timeout_now": int(msgs.timeout_now[0]),
+                "msg_count": msgs.msg_count.cpu().numpy()[: self.sc["S"] * self.ps.stride: self.ps.stride],
+                "msg_index": msgs.msg_index.cpu().numpy().view(np.uint64)[
+                    : self.sc["S"] * self.ps.stride: self.ps.stride],
+                "bcast": int(msgs.bcast[0])}
+
+    def send(self, want, sei, me):
+        dt = torch.uint8 if self.sc["S"] <= 8 else torch.int16
+        w = torch.tensor([want], dtype=dt, device=DEV)
+        sent, snap = self.eng.progress_send(self.ps, w, sei, me)
+        return {"sent": int(sent[0]), "snap": int(snap[0])}
+
+    def append(self):
+        ps, s = self.ps, self.sc["self"]
+        ps.last_index += 1
+        li = int(ps.last_index[0])
+        ps.match[s * ps.stride] = li
+        ps.next[s * ps.stride] = max(int(ps.next[s * ps.stride]), li + 1)
+
+    def peer(self, s):
+        h = self.ps.host()
+        st = self.ps.stride
+        sl = slice(0, self.sc["S"] * st, st)
+        return peer_view(h["match"][sl], h["next"][sl], h["pending"][sl], h["flags"][sl],
+                         h["icount"][sl], s)
+
+    def committed(self):
+        return int(self.ps.committed[0])
+
+
+def test_progress_scenarios_on_gpu(eng):
+    """The reference's leader-side tests (TestLeaderAppResp,
+    TestSendAppendForProgress*, TestMsgAppRespWaitReset, TestProvideSnap,
+    raft_snap_test.go, ...) through qe_progress_step / qe_progress_send."""
+    for sc in scenarios():
+        run_scenario(sc, GpuBackend(eng))
+
+
 def test_fast_log_rejection_on_gpu(eng):
+    """TestFastLogRejection leader side: heartbeat response -> probe MsgApp
+    (sent inside the step) -> rejection -> the next MsgApp's (Index,
+    LogTerm)."""
     L = orc.lib()
     for r in raft_tables()["TestFastLogRejection"]["rows"]:
         lead = [tuple(e) for e in r["leader_log"]]
@@ -140,18 +264,18 @@ def test_fast_log_rejection_on_gpu(eng):
                      term_start=np.array([l_last + 1], np.uint64),
                      next=np.array([l_last + 1], np.uint64), match=np.array([0], np.uint64))
         msgs = eng.PeerMsgs(ps)
-        msgs.type.fill_(3)  # MsgHeartbeatResp
+        msgs.type.fill_(3)  # MsgHeartbeatResp -> sendAppend (probe)
         eng.progress_step(ps, msgs)
-        assert int(msgs.send_mask[0]) == 1
-        sent, _ = eng.progress_send(ps, msgs.send_mask, False, 1 << 20)
-        assert int(sent[0]) == 1
+        assert int(msgs.sent[0]) == 1 and int(msgs.msg_index[0]) == l_last
         msgs = eng.PeerMsgs(ps)
         msgs.type.fill_(2)  # MsgAppResp reject of the probe at Index = l_last
         msgs.index.fill_(l_last)
         msgs.reject_hint.fill_(r["reject_hint_index"])
         msgs.log_term.fill_(r["reject_hint_term"])
         eng.progress_step(ps, msgs)
-        idx = int(ps.next[0]) - 1
+        assert int(msgs.msg_count[0]) == 1
+        idx = int(msgs.msg_index[0])
+        assert idx == int(ps.next[0]) - 1
         term = L.orc_log_term(R, orc.P(rf), orc.P(rt), last, idx)
         assert (idx, term) == (r["next_append_index"], r["next_append_term"]), r
 
@@ -173,6 +297,47 @@ def test_maybe_decr_table_on_gpu(eng):
     eng.progress_step(ps, msgs)
     h = ps.host()
     for i, r in enumerate(rows):
-        assert int(h["next"][i]) == r["want_next"], r
+        # the sendAppend after a decrease moves Next again only in Replicate
+        # (BecomeProbe first), so check MaybeDecrTo's result through the
+        # message it triggered: Index = Next - 1 after the decrease
         assert int(h["match"][i]) == r["match"], r
-        assert bool(int(msgs.send_mask[i]) & 1) == r["want"], r
+        sent = bool(int(msgs.sent[i]) & 1)
+        assert sent == r["want"], r
+        if r["want"] and r["state"] != 1:
+            assert int(msgs.msg_index[i]) + 1 == r["want_next"], r
+
+
+def test_send_if_empty_precedes_snapshot_on_gpu(eng):
+    """raft.go:440-469: maybeSendAppend(to, false) with Next < firstIndex
+    returns false before the snapshot branch (round-1 kernels sent a MsgSnap
+    here)."""
+    G = 64
+    ps = eng.ProgressState(G, 1, 8, 1, DEV)
+    ps.first_index.fill_(10)
+    ps.last_index.fill_(20)
+    ps.next.fill_(5)
+    ps.match.fill_(4)
+    ps.flags.fill_(8)  # Probe, RecentActive
+    want = torch.ones(G, dtype=torch.uint8, device=DEV)
+    sent, snap = eng.progress_send(ps, want, False, 0)
+    assert int(sent.sum()) == 0 and int(snap.sum()) == 0
+    assert int((ps.flags[:G] & 3).sum()) == 0 and int(ps.pending[:G].sum()) == 0
+    sent, snap = eng.progress_send(ps, want, True, 0)
+    assert int(sent.sum()) == G and int(snap.sum()) == G
+    assert bool(((ps.flags[:G] & 3) == 2).all()) and bool((ps.pending[:G] == 9).all())
+
+
+def test_bytes_requested_accounting(eng):
+    """The instrumented variant gives the same results and a byte count in
+    the expected range."""
+    rng = np.random.default_rng(5)
+    G, S, F, R = 4096, 5, 8, 4
+    pb = random_state(rng, G, S, F, R, ())
+    ps = to_device(eng, pb, ())
+    mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
+    msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+    b = eng.progress_bytes_requested(ps, msgs)
+    o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
+    assert_same(ps, pb)
+    assert_outputs(msgs, o, S)
+    assert 50 * G < b < 600 * G, b

@@ -63,11 +63,12 @@ def _one_group(F=16):
 
 def test_fast_log_rejection_leader_side(orc):
     """raft_test.go TestFastLogRejection, leader side, through the batch
-    runners: becomeLeader appends an empty entry at term 1 (the test's fresh
+    runner: becomeLeader appends an empty entry at term 1 (the test's fresh
     raft is at term 0 -> campaign -> term 1); the follower's heartbeat
-    response triggers a probe MsgApp at lastIndex-1; its rejection (hint
-    index / log term) goes through findConflictByTerm + MaybeDecrTo; the
-    next MsgApp's (Index, LogTerm) must match the test."""
+    response triggers a probe MsgApp at Index = lastIndex-1; its rejection
+    (hint index / log term) goes through findConflictByTerm + MaybeDecrTo and
+    the sendAppend inside the step emits the next MsgApp, whose (Index,
+    LogTerm) must match the test."""
     L = orc.lib()
     for r in T["TestFastLogRejection"]["rows"]:
         lead = [tuple(e) for e in r["leader_log"]]
@@ -81,19 +82,45 @@ def test_fast_log_rejection_leader_side(orc):
         pb.term_start[0] = l_last + 1
         pb.next[0], pb.match[0] = l_last + 1, 0  # reset(): Next = lastIndex+1 before the append
         z = lambda v: np.array([v], np.uint64)
-        # heartbeat response -> sendAppend
-        send, _, _ = orc.progress_step(pb, np.array([3], np.uint8), z(0), z(0), z(0))
-        assert send[0] == 1
-        sent, snap = orc.progress_send(pb, send, 0, 1 << 20)
-        assert sent[0] == 1 and pb.flags[0] & PF_PROBE_SENT
-        # rejection of the MsgApp at Index = Next-1 = l_last
-        send, _, _ = orc.progress_step(pb, np.array([2], np.uint8), z(l_last),
-                                       z(r["reject_hint_index"]), z(r["reject_hint_term"]))
-        assert send[0] == 1
-        nxt = int(pb.next[0])
-        idx = nxt - 1
+        # heartbeat response -> sendAppend: probe at Index = Next-1 = l_last
+        o = orc.progress_step(pb, np.array([3], np.uint8), z(0), z(0), z(0))
+        assert o.sent[0] == 1 and o.msg_count[0] == 1 and o.msg_index[0] == l_last
+        assert pb.flags[0] & PF_PROBE_SENT
+        # rejection of that probe -> next MsgApp
+        o = orc.progress_step(pb, np.array([2], np.uint8), z(l_last),
+                              z(r["reject_hint_index"]), z(r["reject_hint_term"]))
+        assert o.sent[0] == 1 and o.msg_count[0] == 1
+        idx = int(o.msg_index[0])
+        assert idx == int(pb.next[0]) - 1
         term = L.orc_log_term(len(rf), orc.P(rf), orc.P(rt), last, idx)
         assert (idx, term) == (r["next_append_index"], r["next_append_term"]), r
+
+
+def test_progress_scenarios_on_oracle(orc):
+    """Every leader-side scenario of tests/golden/progress_scenarios.json
+    (TestLeaderAppResp, TestSendAppendForProgress*, TestProvideSnap, the
+    raft_snap_test.go tests, ...) through the oracle."""
+    from tests.progress_scenarios import OracleBackend, run_scenario, scenarios
+    names = []
+    for sc in scenarios():
+        run_scenario(sc, OracleBackend(orc))
+        names.append(sc["name"])
+    assert len(names) == 19
+
+
+def test_send_if_empty_precedes_snapshot(orc):
+    """raft.go:440-469: with sendIfEmpty=false and Next < firstIndex there are
+    no entries, so maybeSendAppend returns false BEFORE the snapshot branch
+    (no MsgSnap, the Progress stays in its state)."""
+    pb = orc.ProgressBatch(1, 1, 8, 1)
+    pb.first_index[0], pb.last_index[0] = 10, 20
+    pb.next[0], pb.match[0] = 5, 4
+    pb.flags[0] = 0 | PF_RECENT_ACTIVE  # Probe, recently active
+    w = np.array([1], np.uint8)
+    sent, snap = orc.progress_send(pb, w, 0, 0)
+    assert sent[0] == 0 and snap[0] == 0 and pb.flags[0] & 3 == 0 and pb.pending[0] == 0
+    sent, snap = orc.progress_send(pb, w, 1, 0)
+    assert sent[0] == 1 and snap[0] == 1 and pb.flags[0] & 3 == 2 and pb.pending[0] == 9
 
 
 def test_find_conflict_by_term_jump_equals_walk(orc):
