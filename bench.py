@@ -19,6 +19,9 @@ import os
 import sys
 import time
 
+import socket
+import subprocess
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -26,7 +29,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from etcd_amd import engine  # noqa: E402
+engine = None  # etcd_amd.engine, imported once the process knows its rank
 
 METRIC = "quorum group-evals/sec at 1/2/4/8 MI355X; % HBM peak; speedup vs Go host"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
@@ -65,16 +68,46 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true", help="skip the secondary workloads")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = this process's CPU share: the affinity "
+                         "set, capped by OMP_NUM_THREADS when the box sets it)")
     ap.add_argument("--cpu-groups", type=int, default=1 << 21)
     return ap.parse_args()
 
 
+def cpu_share():
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def maybe_spawn(args):
+    """`bench.py --gpus N` outside a torch.distributed launch starts N ranks
+    (one process per GPU) with torch.distributed.run as a CHILD process --
+    this process has not touched the GPU -- and exits with its status.
+    Rank 0 of the children prints the JSON line."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return False
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 class Dist:
     """One process per GPU (torch.distributed.run env).  Collectives go over
-    RCCL (backend "nccl") by default.  QE_DIST_BACKEND=gloo with
-    QE_DEVICE_MOD=1 rehearses the multi-rank logic on a 1-GPU box (all ranks
-    on cuda:0, counters reduced on the host)."""
+    RCCL (backend "nccl") by default: barrier/max through torch, the stats
+    all-reduce through the engine's own C ABI (qe_allreduce_stats on an RCCL
+    communicator set up with qe_comm_init -- the path a Go host uses).
+    QE_DIST_BACKEND=gloo with QE_DEVICE_MOD=1 rehearses the multi-rank logic
+    on a 1-GPU box (all ranks on cuda:0, counters reduced on the host)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,6 +118,7 @@ class Dist:
         dev_idx = self.local % mod if mod > 0 else self.local
         torch.cuda.set_device(dev_idx)
         self.dev = torch.device("cuda", dev_idx)
+        self.comm = None
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.backend == "nccl":
@@ -109,15 +143,44 @@ class Dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def _rccl(self):
+        """The engine's RCCL communicator (qe_comm_init); the 128-byte id
+        travels from rank 0 over torch.distributed."""
+        if self.comm is None:
+            import ctypes as C
+            lib = engine._lib.lib()
+            idb = (C.c_uint8 * lib.qe_comm_id_bytes())()
+            if self.rank == 0:
+                engine.check("qe_comm_unique_id", lib.qe_comm_unique_id(idb))
+            obj = [bytes(idb)]
+            dist.broadcast_object_list(obj, src=0)
+            idb = (C.c_uint8 * len(obj[0])).from_buffer_copy(obj[0])
+            comm = C.c_void_p()
+            engine.check("qe_comm_init", lib.qe_comm_init(C.byref(comm), self.world, self.rank,
+                                                           idb, self.dev.index))
+            self.comm = comm
+        return self.comm
+
     def sum_stats(self, folded):
-        """All-reduce (sum) of the uint64 statistics vector; the int64
-        wraparound equals uint64 modular addition.  RCCL over xGMI: 128 B,
-        once per run, latency-bound and off the data path."""
+        """All-reduce (sum) of the uint64 statistics vector: RCCL over xGMI
+        through qe_allreduce_stats (128 B, once per run, latency-bound and
+        off the data path); gloo rehearsal: torch on the host."""
         if self.world > 1:
-            t = self._coll(folded)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            folded = t.to(self.dev)
+            if self.backend == "nccl":
+                engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
+                    engine._ptr(folded), folded.numel(), self._rccl(), engine._stream(self.dev)))
+            else:
+                t = self._coll(folded)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                folded = t.to(self.dev)
         return folded
+
+    def close(self):
+        if self.comm is not None:
+            engine._lib.lib().qe_comm_destroy(self.comm)
+            self.comm = None
+        if self.world > 1:
+            dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------------------
@@ -224,8 +287,10 @@ def setup(name, G, S, kind, d, stats):
         bpg = (8 + 1 + 1 + 1 + 1 + 1 + 8 + 1 + 1 + 1) / steps_per_launch
         return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
     if kind == "progress":
-        F, R = 8, 4
-        ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff)
+        # MaxInflightMsgs 8, MaxSizePerMsg = 16 entries, 4-term leader log
+        F, R, ME = 8, 4, 16
+        ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff, extras=("self_slot",),
+                                  max_ents=ME)
         n = S * ps.stride
         gen = torch.Generator(device=d.dev).manual_seed(0x5EED + d.rank)
         base = torch.randint(1 << 20, 1 << 40, (ps.stride,), device=d.dev, generator=gen)
@@ -239,6 +304,7 @@ def setup(name, G, S, kind, d, stats):
         ps.term_start.copy_(base[:G])
         ps.first_index.copy_(base[:G] - 64)
         ps.committed.copy_(base[:G])
+        ps.self_slot.fill_(0)  # the leader's own Progress is slot 0
         rf = ps.run_first.view(R, ps.stride)
         for r in range(R):
             rf[r].copy_(base - 65 + 40 * r)
@@ -246,8 +312,10 @@ def setup(name, G, S, kind, d, stats):
             torch.arange(1, R + 1, device=d.dev).repeat_interleave(ps.stride).view(R, ps.stride))
         ps.run_count.fill_(R)
         msgs = engine.PeerMsgs(ps)
+        msgs.snap = msgs.timeout_now = None  # no snapshots / transfers in this workload
         u = torch.rand(n, device=d.dev, generator=gen)
         ty = torch.where(u < 0.7, 1, torch.where(u < 0.8, 2, torch.where(u < 0.9, 3, 0)))
+        ty.view(S, ps.stride)[0] = 0  # no message from the leader itself
         msgs.type.copy_(ty.to(torch.uint8))
         # acks stay within the leader's log: match + [0, 64] <= base + 127 < lastIndex
         msgs.index.copy_(ps.match + torch.randint(0, 65, (n,), device=d.dev, generator=gen))
@@ -257,7 +325,9 @@ def setup(name, G, S, kind, d, stats):
         # Every timed launch steps the SAME fresh state with the same round
         # of messages: the mutable state is restored from a pristine copy
         # before each launch (outside the kernel's HIP events), so no launch
-        # sees stale, already-applied duplicates.
+        # sees stale, already-applied duplicates.  The Inflights buffer needs
+        # no restore: a round appends only into free ring entries, and the
+        # live entries it reads are the restored (start, count) window.
         mutable = ("match", "next", "pending", "flags", "istart", "icount", "committed")
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
@@ -265,35 +335,15 @@ def setup(name, G, S, kind, d, stats):
             for k in mutable:
                 getattr(ps, k).copy_(pristine[k])
 
-        # Exact algorithmic bytes of one round over these inputs (every byte
-        # the state machine must read or write, once):
-        #  per peer: message type (1); a processed message (types 1-3) reads
-        #  and writes the peer's Progress (match/next/pending 48 + flags/
-        #  start/count 6); accept/reject read the index (8); a reject reads
-        #  hint + logTerm (16); Inflights entries examined by FreeLE
-        #  (inflights.go:87-113): min(count, freed + 1) for an accept that
-        #  advances Match, 2 for a heartbeat on a full ring;
-        #  per group: committed rw (16), termStart/lastIndex (16), run_count
-        #  (1), send mask + bcast out (2), and the term-run table (16 R) when
-        #  findConflictByTerm runs (a reject with logTerm > 0).
-        with torch.no_grad():
-            m = ps.match.view(S, ps.stride)[:, :G]
-            idx = msgs.index.view(S, ps.stride)[:, :G]
-            t = ty.view(S, ps.stride)[:, :G]
-            cnt = ps.icount.view(S, ps.stride)[:, :G].to(torch.int64)
-            r = idx - m
-            freed = torch.clamp((r - 1) // 8 + 1, min=0)  # entries match+1+8k <= idx
-            freed = torch.minimum(freed, cnt)
-            acc_reads = torch.where((t == 1) & (r > 0) & (cnt > 0),
-                                    torch.minimum(cnt, freed + 1), torch.zeros_like(cnt))
-            hb_reads = torch.where((t == 3) & (cnt == F), 2, 0)
-            proc = (t >= 1) & (t <= 3)
-            peer_bytes = G * S \
-                + int(proc.sum()) * 54 + int(((t == 1) | (t == 2)).sum()) * 8 \
-                + int((t == 2).sum()) * 16 + 8 * int((acc_reads + hb_reads).sum())
-            ltv = lt.view(S, ps.stride)[:, :G]
-            runs = int(((t == 2) & (ltv > 0)).any(dim=0).sum()) * 16 * R
-            total = peer_bytes + G * (16 + 16 + 1 + 2) + runs
+        # Algorithmic bytes of this round: the instrumented kernel variant
+        # counts every field the state machine reads or writes (reads of the
+        # message, the Progress fields each event needs, PendingSnapshot only
+        # in StateSnapshot, the Inflights entries FreeLE examines, the
+        # term-run table when findConflictByTerm runs; writes of changed
+        # fields, appended Inflights entries and the outputs), once each.
+        prepare()
+        total = engine.progress_bytes_requested(ps, msgs)
+        prepare()
         bpg = total / G
         import ctypes as C
         p_, m_ = ps.struct(), msgs.struct()
@@ -380,49 +430,57 @@ def time_steps(step, d, steps, warmup, prepare=None):
     return wall, kern_ms
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def cpu_baseline(args, S=5):
     """Oracle port timed on this host's cores over a bounded sample."""
     from oracle import orc
     G = args.cpu_groups
+    threads = args.cpu_threads or cpu_share()
     hb = orc.Batch(G, S, masks=())
-    orc.gen_batch(hb, 0x5EED, threads=args.cpu_threads)
+    orc.gen_batch(hb, 0x5EED, threads=threads)
     commit = np.zeros(G, np.uint64)
     vote = np.zeros(G, np.uint8)
     L = orc.lib()
     w = L.orc_gf_build(G, S, G, orc.P(hb.match), None, None, None, orc.P(hb.voted),
                        orc.P(hb.granted))
     try:
-        L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, args.cpu_threads)  # warm-up
-        t1 = L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, args.cpu_threads)
-        reps = max(1, int(1.5 / max(t1, 1e-6)))
-        t = L.orc_gf_run(w, orc.P(commit), orc.P(vote), reps, args.cpu_threads)
+        L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, threads)  # warm-up
+        t1 = L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, threads)
+        reps = max(1, int(10.0 / max(t1, 1e-6)))
+        t = L.orc_gf_run(w, orc.P(commit), orc.P(vote), reps, threads)
         gf_rate = G * reps / t
     finally:
         L.orc_gf_free(w)
     # the SoA restatement (strongest CPU variant)
     L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
-                  orc.P(commit), orc.P(vote), 1, args.cpu_threads)
+                  orc.P(commit), orc.P(vote), 1, threads)
     t1 = L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
-                       orc.P(commit), orc.P(vote), 1, args.cpu_threads)
-    reps2 = max(1, int(1.5 / max(t1, 1e-6)))
+                       orc.P(commit), orc.P(vote), 1, threads)
+    reps2 = max(1, int(3.0 / max(t1, 1e-6)))
     t2 = L.orc_soa_run(G, S, G, orc.P(hb.match), None, None, orc.P(hb.voted), orc.P(hb.granted),
-                       orc.P(commit), orc.P(vote), reps2, args.cpu_threads)
+                       orc.P(commit), orc.P(vote), reps2, threads)
     soa_rate = G * reps2 / t2
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    host_cpus = os.cpu_count()
     return {
-        "value": gf_rate, "unit": "group-evals/s", "cores": args.cpu_threads, "kind": "port",
-        "sample": (f"{G} groups x 5 voters x {reps} passes: Go-faithful map/AckedIndexer loop "
-                   f"(oracle/quorum_oracle.c orc_gf_run, CommittedIndex+VoteResult per group), "
-                   f"OpenMP {args.cpu_threads} threads, {cpu_model}"),
+        "value": gf_rate, "unit": "group-evals/s", "cores": threads, "kind": "port",
+        "sample": (f"{G} groups x 5 voters x {reps} passes (~10 s): Go-faithful map/AckedIndexer "
+                   f"loop (oracle/quorum_oracle.c orc_gf_run, CommittedIndex+VoteResult per "
+                   f"group), OpenMP {threads} threads = this process's CPU share "
+                   f"(affinity {len(os.sched_getaffinity(0))} CPUs, OMP_NUM_THREADS "
+                   f"{os.environ.get('OMP_NUM_THREADS', 'unset')}) of a {host_cpus}-CPU "
+                   f"{cpu_model()} host"),
+        "cpu_model": cpu_model(), "host_cpus": host_cpus,
         "soa_value": soa_rate,
-        "soa_sample": f"{G} groups x {reps2} passes, SoA restatement (orc_soa_run)",
+        "soa_sample": f"{G} groups x {reps2} passes, SoA restatement (orc_soa_run), {threads} threads",
     }
 
 
@@ -509,8 +567,9 @@ def config1(args, d):
     res["hbm_frac"] = res["achieved_GBs"] / HBM_PEAK_GBS
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         from oracle import orc
+        threads = args.cpu_threads or cpu_share()
         hb = orc.Batch(G, S, masks=(), votes=False)
-        orc.gen_batch(hb, 0x5EED, dist=1, p_absent=0, threads=args.cpu_threads)
+        orc.gen_batch(hb, 0x5EED, dist=1, p_absent=0, threads=threads)
         # CPU result must equal the GPU's (parity at the reference's own shape)
         c_ref = orc.commit_vote(hb)[0]
         assert np.array_equal(commit.cpu().numpy().view(np.uint64), c_ref), "config1 mismatch"
@@ -520,15 +579,15 @@ def config1(args, d):
         zero = np.zeros(G, np.uint8)
         w = L.orc_gf_build(G, S, G, orc.P(hb.match), None, None, None, orc.P(zero), orc.P(zero))
         try:
-            L.orc_gf_run(w, orc.P(cc), orc.P(vv), 1, args.cpu_threads)
-            t1 = L.orc_gf_run(w, orc.P(cc), orc.P(vv), 1, args.cpu_threads)
+            L.orc_gf_run(w, orc.P(cc), orc.P(vv), 1, threads)
+            t1 = L.orc_gf_run(w, orc.P(cc), orc.P(vv), 1, threads)
             n = max(1, int(1.0 / max(t1, 1e-6)))
-            t = L.orc_gf_run(w, orc.P(cc), orc.P(vv), n, args.cpu_threads)
+            t = L.orc_gf_run(w, orc.P(cc), orc.P(vv), n, threads)
         finally:
             L.orc_gf_free(w)
         assert np.array_equal(cc, c_ref)
         res["cpu_port_value"] = G * n / t
-        res["cpu_port_cores"] = args.cpu_threads
+        res["cpu_port_cores"] = threads
         res["speedup_vs_cpu_port"] = res["value"] / res["cpu_port_value"]
     del b, commit, g
     torch.cuda.empty_cache()
@@ -536,8 +595,15 @@ def config1(args, d):
 
 
 def main():
+    global engine
     args = parse()
+    maybe_spawn(args)  # --gpus N > 1 outside torchrun: relaunch as N ranks (exits)
+    from etcd_amd import engine as _engine
+    engine = _engine
     d = Dist()
+    if d.world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={d.world}", file=sys.stderr)
+        sys.exit(2)
     main_res = run_workload(args.workload, args, d, args.steps, args.warmup)
     aux = {}
     if not args.no_aux:
@@ -548,23 +614,32 @@ def main():
             r = run_workload(name, args, d, max(5, args.steps // 2), max(2, args.warmup // 2))
             aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
                                            "achieved_GBs", "hbm_frac", "invariant_violations")}
+            if "roofline_valu" in r:
+                aux[name]["roofline_valu"] = r["roofline_valu"]
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
     if d.rank == 0:
         desc, G, S, kind = WORKLOADS[args.workload]
         traffic = load_traffic(args.workload)
+        majority_like = kind in ("majority", "joint", "joint_rot")
+        vs = None
+        if cpu is not None and majority_like:
+            vs = main_res["value"] / cpu["value"]
         line = {
             "metric": METRIC,
             "value": main_res["value"],
-            "unit": "group-evals/s" if kind in ("majority", "joint", "joint_rot") else main_res["unit"],
+            "unit": "group-evals/s" if majority_like else main_res["unit"],
             "n_gpus": d.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": vs,
+            "vs_baseline_basis": ("value / cpu_baseline.value: the metric's 'speedup vs Go host' "
+                                  "against the measured CPU port (BASELINE.md publishes no "
+                                  "number); null when no CPU baseline ran (N > 1)"),
             "dtype": "u64",
             "data": "synthetic: counter-based splitmix64 generator, inputs resident in HBM",
             "config": {
@@ -582,7 +657,7 @@ def main():
                 "unit": "GB/s",
                 "frac": main_res["hbm_frac"],
                 "traffic": traffic,
-                "kernel": "qe::k_cv_stream" if kind in ("majority", "joint", "joint_rot") else kind,
+                "kernel": "qe::k_cv_stream" if majority_like else kind,
                 "kernel_ms": main_res["kernel_ms"],
                 "bytes_per_unit": main_res["bytes_per_unit"],
             },
@@ -592,8 +667,7 @@ def main():
             "aux": aux,
         }
         print(json.dumps(line))
-    if d.world > 1:
-        dist.destroy_process_group()
+    d.close()
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@ QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
 QE_EHIP = -1000
+QE_ECOMM = -1001
 QE_INDEX_INF = (1 << 64) - 1
 QE_MAX_SLOTS = 16
 QE_VOTE_PENDING, QE_VOTE_LOST, QE_VOTE_WON = 1, 2, 3
@@ -171,6 +172,11 @@ PROTOTYPES = {
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, u32, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),
                                 C.POINTER(QeProgress), vp]),
+    "qe_comm_id_bytes": (C.c_size_t, []),
+    "qe_comm_unique_id": (C.c_int, [vp]),
+    "qe_comm_init": (C.c_int, [C.POINTER(vp), u32, u32, vp, C.c_int]),
+    "qe_comm_destroy": (C.c_int, [vp]),
+    "qe_allreduce_stats": (C.c_int, [vp, u32, vp, vp]),
 }
 
 

@@ -16,6 +16,8 @@ int g_repl_kernel = -1;  // qe_replication_round kernel: 0 pair, 1 stream, -1 de
 
 static thread_local char g_errbuf[256];
 
+void set_error(const char *msg) { snprintf(g_errbuf, sizeof(g_errbuf), "%s", msg); }
+
 int hip_status(hipError_t e) {
   if (e == hipSuccess) return QE_OK;
   snprintf(g_errbuf, sizeof(g_errbuf), "HIP error %d: %s", static_cast<int>(e),
@@ -120,6 +122,7 @@ const char *qe_strerror(int status) {
     case QE_EINVAL: return "invalid argument";
     case QE_ERANGE: return "out of range";
     case QE_EHIP: return g_errbuf[0] ? g_errbuf : "HIP error";
+    case QE_ECOMM: return g_errbuf[0] ? g_errbuf : "RCCL error";
     default: return "unknown status";
   }
 }

@@ -74,6 +74,7 @@ extern "C" {
 #define QE_EINVAL (-22)  /* null pointer / bad size / S out of range   */
 #define QE_ERANGE (-34)  /* value out of supported range                */
 #define QE_EHIP (-1000)  /* HIP launch / runtime error                  */
+#define QE_ECOMM (-1001) /* RCCL error (qe_comm_*, qe_allreduce_stats)    */
 
 /* Aggregate statistics.  A stats buffer is uint64[QE_STATS_WORDS]; kernels
  * add into QE_STATS_SHARDS shards of QE_STATS_COUNTERS counters (one 128-byte
@@ -515,6 +516,26 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
 
 /* out[QE_STATS_COUNTERS] (device) = sum over shards of stats (device). */
 int qe_stats_reduce(const uint64_t *stats, uint64_t *out, void *stream);
+
+/* ---- multi-GPU aggregation (RCCL over xGMI) ---------------------------- */
+
+/* Groups shard across GPUs with no data-path exchange; the one collective is
+ * the sum of the statistics vector (the batch form of etcd's per-member
+ * Prometheus counters, server/etcdserver/metrics.go:29-85).  Setup: rank 0
+ * calls qe_comm_unique_id, the host sends those qe_comm_id_bytes() bytes to
+ * every rank over its own transport, every rank calls qe_comm_init with its
+ * rank and device.  One communicator per process (one process per GPU). */
+size_t qe_comm_id_bytes(void);                 /* size of the id (128) */
+int qe_comm_unique_id(void *id);               /* rank 0: new id (host) */
+int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id,
+                 int device);
+int qe_comm_destroy(void *comm);
+
+/* stats[0..n) (DEVICE, n <= QE_STATS_WORDS; normally the QE_STATS_COUNTERS
+ * words qe_stats_reduce produced) = elementwise sum over all ranks of comm,
+ * in place, asynchronously on `stream`: ncclAllReduce(ncclUint64, ncclSum).
+ * uint64 addition wraps like the counters themselves. */
+int qe_allreduce_stats(uint64_t *stats, uint32_t n, void *comm, void *stream);
 
 /* ---- synthetic inputs (counter-based, bit-identical to oracle/) -------- */
 

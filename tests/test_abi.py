@@ -26,7 +26,8 @@ def test_header_declares_expected_surface():
     for f in ["qe_commit_vote", "qe_committed_index", "qe_vote_result", "qe_quorum_active",
               "qe_record_votes", "qe_replication_round", "qe_election_steps",
               "qe_stats_reduce", "qe_gen_groups", "qe_abi_version", "qe_strerror",
-              "qe_mask_bytes", "qe_tune"]:
+              "qe_mask_bytes", "qe_tune", "qe_allreduce_stats", "qe_comm_init",
+              "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes"]:
         assert f in fns
 
 
@@ -139,6 +140,24 @@ def test_argument_errors_without_gpu():
                               state=C.c_void_p(64), voted=C.c_void_p(64),
                               granted=C.c_void_p(64), self_slot=C.c_void_p(64))
     assert L.qe_election_steps(C.byref(st), C.byref(p), None, None) == _lib.QE_ERANGE
+
+
+def test_comm_argument_errors_without_gpu():
+    """qe_comm_* / qe_allreduce_stats validate before touching RCCL."""
+    L = _lib.lib()
+    assert L.qe_comm_id_bytes() == 128  # sizeof(ncclUniqueId)
+    assert L.qe_comm_unique_id(None) == _lib.QE_EINVAL
+    comm = C.c_void_p()
+    idb = (C.c_uint8 * 128)()
+    assert L.qe_comm_init(None, 1, 0, idb, 0) == _lib.QE_EINVAL
+    assert L.qe_comm_init(C.byref(comm), 0, 0, idb, 0) == _lib.QE_EINVAL
+    assert L.qe_comm_init(C.byref(comm), 2, 2, idb, 0) == _lib.QE_EINVAL  # rank >= nranks
+    assert L.qe_comm_init(C.byref(comm), 1, 0, None, 0) == _lib.QE_EINVAL
+    assert L.qe_comm_destroy(None) == _lib.QE_EINVAL
+    assert L.qe_allreduce_stats(None, 16, C.c_void_p(64), None) == _lib.QE_EINVAL
+    assert L.qe_allreduce_stats(C.c_void_p(64), 16, None, None) == _lib.QE_EINVAL
+    assert L.qe_allreduce_stats(C.c_void_p(64), 0, C.c_void_p(64), None) == _lib.QE_EINVAL
+    assert L.qe_allreduce_stats(C.c_void_p(64), 1025, C.c_void_p(64), None) == _lib.QE_EINVAL
 
 
 def test_missing_library_fails_loudly(tmp_path):
