@@ -89,7 +89,8 @@ class QeGenParams(C.Structure):
 class QeConfStateCSR(C.Structure):
     _fields_ = [("num_groups", u64), ("voters", vp), ("voters_off", vp),
                 ("voters_outgoing", vp), ("outgoing_off", vp), ("learners", vp),
-                ("learners_off", vp), ("learners_next", vp), ("learners_next_off", vp)]
+                ("learners_off", vp), ("learners_next", vp), ("learners_next_off", vp),
+                ("auto_leave", vp)]
 
 
 class QeProgress(C.Structure):
@@ -164,6 +165,7 @@ PROTOTYPES = {
     "qe_gen_groups": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeGenParams), vp]),
     "qe_apply_append_resps": (C.c_int, [u64, u32, u64, vp, vp, u64, vp, vp, vp, vp, vp]),
     "qe_pack_confstate": (C.c_int, [C.POINTER(QeConfStateCSR), u32, vp, vp, vp, vp, vp, vp]),
+    "qe_pack_conf": (C.c_int, [C.POINTER(QeConfStateCSR), C.POINTER(QeConf), vp, vp]),
     "qe_pack_match": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, u64, vp]),
     "qe_pack_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp]),
     "qe_slot_lookup": (C.c_int, [u64, u32, vp, u64, vp, vp, vp]),

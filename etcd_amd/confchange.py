@@ -75,6 +75,10 @@ def ChangeBatch(changers, ops, ccs, device=None):
     G = len(changers)
     if G == 0:
         return []
+    if any(len(x) > 255 for x in ccs):
+        # qe_conf_changes.count is a u8 per group (the reference Changer has
+        # no limit): refuse rather than apply a truncated change list
+        raise ValueError("ChangeBatch: more than 255 changes in one group")
     S = max(1, min(_lib.QE_MAX_SLOTS,
                    max(len(c.Tracker.Progress) + len(x) for c, x in zip(changers, ccs))))
     C = max(1, max(len(x) for x in ccs))

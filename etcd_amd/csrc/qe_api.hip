@@ -451,6 +451,7 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
       !c->learners_next_mask || !c->is_learner || !c->tracked || !c->auto_leave)
     return QE_EINVAL;
   if (!ch->op || !ch->count || !ch->last_index || !ch->result) return QE_EINVAL;
+  if (ch->max_changes > 255) return QE_EINVAL;  // count is a u8 per group
   if (ch->max_changes > 0 && (!ch->type || !ch->node_id || ch->stride < c->num_groups))
     return QE_EINVAL;
   CCArgs a{};

@@ -421,6 +421,11 @@ std::vector<Result> ChangeBatch(const std::vector<const Changer *> &changers,
   if (G == 0) return out;
   size_t need = 1, C = 0;
   for (uint64_t g = 0; g < G; g++) {
+    // qe_conf_changes.count is a u8 per group: a longer change list cannot be
+    // represented (the reference Changer has no such limit), so refuse it
+    // instead of silently applying a truncated list
+    if (ccs[g].size() > 255)
+      throw std::invalid_argument("ChangeBatch: more than 255 changes in one group");
     need = std::max(need, changers[g]->Tracker.Progress.size() + ccs[g].size());
     C = std::max(C, ccs[g].size());
   }

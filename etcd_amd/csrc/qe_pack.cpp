@@ -71,6 +71,88 @@ int qe_pack_threads(int n) {
   return QE_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// One group of a ConfState CSR batch in slot form: ids[S] (0 = unused), the
+// masks of Voters[0], Voters[1], Learners, LearnersNext, and QE_PACK_* flags.
+// A flagged group (too many peers, zero ID) is left empty.
+struct PackedGroup {
+  uint32_t mi, mo, ml, mlnx, flags;
+};
+
+PackedGroup pack_group(const List &voters, const List &outgoing, const List &learners,
+                       const List &lnext, uint64_t g, uint32_t S, uint64_t *ids) {
+  PackedGroup r{0, 0, 0, 0, 0};
+  uint64_t vbuf[2 * QE_MAX_SLOTS + 2], lbuf[QE_MAX_SLOTS + 1];
+  memset(ids, 0, sizeof(uint64_t) * S);
+  // voters of both halves, ascending + deduplicated (JointConfig.IDs)
+  uint32_t nv = 0;
+  auto add_voters = [&](const List &l) {
+    if (!l.has(g)) return;
+    for (const uint64_t *p = l.begin(g); p != l.end(g); ++p) {
+      if (nv >= 2 * QE_MAX_SLOTS + 1) { r.flags |= QE_PACK_TOO_MANY_PEERS; return; }
+      vbuf[nv++] = *p;
+    }
+  };
+  add_voters(voters);
+  add_voters(outgoing);
+  std::sort(vbuf, vbuf + nv);
+  nv = static_cast<uint32_t>(std::unique(vbuf, vbuf + nv) - vbuf);
+  uint32_t nl = 0;
+  if (learners.has(g)) {
+    for (const uint64_t *p = learners.begin(g); p != learners.end(g); ++p) {
+      if (std::binary_search(vbuf, vbuf + nv, *p)) {
+        r.flags |= QE_PACK_LEARNER_IS_VOTER;  // confchange.go:308-318 invariant
+        continue;
+      }
+      if (nl >= QE_MAX_SLOTS) { r.flags |= QE_PACK_TOO_MANY_PEERS; break; }
+      lbuf[nl++] = *p;
+    }
+  }
+  std::sort(lbuf, lbuf + nl);
+  nl = static_cast<uint32_t>(std::unique(lbuf, lbuf + nl) - lbuf);
+  if (nv + nl > S) r.flags |= QE_PACK_TOO_MANY_PEERS;
+  // LearnersNext must be outgoing voters (confchange.go:299-306)
+  if (lnext.has(g)) {
+    for (const uint64_t *p = lnext.begin(g); p != lnext.end(g); ++p) {
+      bool in_out = false;
+      if (outgoing.has(g))
+        for (const uint64_t *q = outgoing.begin(g); q != outgoing.end(g); ++q)
+          in_out |= (*q == *p);
+      if (!in_out) r.flags |= QE_PACK_LEARNER_NEXT_NOT_OUTGOING;
+    }
+  }
+  // ID 0 is raft.None, and slot id 0 marks an unused slot: a voter or a
+  // learner with ID 0 cannot be placed
+  for (uint32_t i = 0; i < nv; i++)
+    if (vbuf[i] == 0) r.flags |= QE_PACK_ZERO_ID;
+  for (uint32_t i = 0; i < nl; i++)
+    if (lbuf[i] == 0) r.flags |= QE_PACK_ZERO_ID;
+  if (!(r.flags & QE_PACK_TOO_MANY_PEERS) && !(r.flags & QE_PACK_ZERO_ID)) {
+    for (uint32_t i = 0; i < nv; i++) ids[i] = vbuf[i];
+    for (uint32_t i = 0; i < nl; i++) ids[nv + i] = lbuf[i];
+    auto mark = [&](const List &l, uint32_t &m) {
+      if (!l.has(g)) return;
+      for (const uint64_t *p = l.begin(g); p != l.end(g); ++p) {
+        const int s = slot_of(ids, S, *p);
+        if (s >= 0) m |= 1u << s;
+      }
+    };
+    mark(voters, r.mi);
+    mark(outgoing, r.mo);
+    mark(lnext, r.mlnx);
+    r.mlnx &= r.mo;  // only outgoing voters can be LearnersNext
+    for (uint32_t i = 0; i < nl; i++) r.ml |= 1u << (nv + i);
+  }
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
 int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_mask,
                       void *out_mask, void *learner_mask, uint64_t *slot_ids,
                       uint32_t *group_flags, uint64_t *num_flagged) {
@@ -87,70 +169,53 @@ int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_
   std::atomic<uint64_t> flagged{0};
   parallel_for(G, [&](uint64_t b, uint64_t e) {
     uint64_t local_flagged = 0;
-    uint64_t vbuf[2 * QE_MAX_SLOTS + 2], lbuf[QE_MAX_SLOTS + 1];
     for (uint64_t g = b; g < e; g++) {
-      uint32_t flags = 0;
-      uint64_t *ids = slot_ids + g * S;
-      memset(ids, 0, sizeof(uint64_t) * S);
-      // voters of both halves, ascending + deduplicated (JointConfig.IDs)
-      uint32_t nv = 0;
-      auto add_voters = [&](const List &l) {
-        if (!l.has(g)) return;
-        for (const uint64_t *p = l.begin(g); p != l.end(g); ++p) {
-          if (nv >= 2 * QE_MAX_SLOTS + 1) { flags |= QE_PACK_TOO_MANY_PEERS; return; }
-          vbuf[nv++] = *p;
-        }
-      };
-      add_voters(voters);
-      add_voters(outgoing);
-      std::sort(vbuf, vbuf + nv);
-      nv = static_cast<uint32_t>(std::unique(vbuf, vbuf + nv) - vbuf);
-      uint32_t nl = 0;
-      if (learners.has(g)) {
-        for (const uint64_t *p = learners.begin(g); p != learners.end(g); ++p) {
-          if (std::binary_search(vbuf, vbuf + nv, *p)) {
-            flags |= QE_PACK_LEARNER_IS_VOTER;  // confchange.go:308-318 invariant
-            continue;
-          }
-          if (nl >= QE_MAX_SLOTS) { flags |= QE_PACK_TOO_MANY_PEERS; break; }
-          lbuf[nl++] = *p;
-        }
-      }
-      std::sort(lbuf, lbuf + nl);
-      nl = static_cast<uint32_t>(std::unique(lbuf, lbuf + nl) - lbuf);
-      if (nv + nl > S) flags |= QE_PACK_TOO_MANY_PEERS;
-      // LearnersNext must be outgoing voters (confchange.go:299-306)
-      if (lnext.has(g)) {
-        for (const uint64_t *p = lnext.begin(g); p != lnext.end(g); ++p) {
-          bool in_out = false;
-          if (outgoing.has(g))
-            for (const uint64_t *q = outgoing.begin(g); q != outgoing.end(g); ++q)
-              in_out |= (*q == *p);
-          if (!in_out) flags |= QE_PACK_LEARNER_NEXT_NOT_OUTGOING;
-        }
-      }
-      for (uint32_t i = 0; i < nv; i++)
-        if (vbuf[i] == 0) flags |= QE_PACK_ZERO_ID;
-      uint32_t mi = 0, mo = 0, ml = 0;
-      if (!(flags & QE_PACK_TOO_MANY_PEERS) && !(flags & QE_PACK_ZERO_ID)) {
-        for (uint32_t i = 0; i < nv; i++) ids[i] = vbuf[i];
-        for (uint32_t i = 0; i < nl; i++) ids[nv + i] = lbuf[i];
-        auto mark = [&](const List &l, uint32_t &m) {
-          if (!l.has(g)) return;
-          for (const uint64_t *p = l.begin(g); p != l.end(g); ++p) {
-            const int s = slot_of(ids, S, *p);
-            if (s >= 0) m |= 1u << s;
-          }
-        };
-        mark(voters, mi);
-        mark(outgoing, mo);
-        for (uint32_t i = 0; i < nl; i++) ml |= 1u << (nv + i);
-      }
-      put_mask(inc_mask, mb, g, mi);
-      put_mask(out_mask, mb, g, mo);
-      put_mask(learner_mask, mb, g, ml);
-      if (group_flags) group_flags[g] = flags;
-      local_flagged += flags != 0;
+      const PackedGroup r = pack_group(voters, outgoing, learners, lnext, g, S, slot_ids + g * S);
+      put_mask(inc_mask, mb, g, r.mi);
+      put_mask(out_mask, mb, g, r.mo);
+      put_mask(learner_mask, mb, g, r.ml);
+      if (group_flags) group_flags[g] = r.flags;
+      local_flagged += r.flags != 0;
+    }
+    flagged += local_flagged;
+  });
+  if (num_flagged) *num_flagged = flagged.load();
+  return QE_OK;
+}
+
+int qe_pack_conf(const qe_confstate_csr *cs, const qe_conf *out, uint32_t *group_flags,
+                 uint64_t *num_flagged) {
+  if (!cs || !out) return QE_EINVAL;
+  if (out->num_slots == 0 || out->num_slots > QE_MAX_SLOTS || out->reserved) return QE_EINVAL;
+  if (out->num_groups != cs->num_groups) return QE_EINVAL;
+  const uint64_t G = cs->num_groups;
+  if (num_flagged) *num_flagged = 0;
+  if (G == 0) return QE_OK;
+  if (!cs->voters || !cs->voters_off) return QE_EINVAL;
+  if (!out->slot_ids || !out->inc_mask || !out->out_mask || !out->learner_mask ||
+      !out->learners_next_mask || !out->is_learner || !out->tracked || !out->auto_leave)
+    return QE_EINVAL;
+  const uint32_t S = out->num_slots, mb = S <= 8 ? 1 : 2;
+  const List voters{cs->voters, cs->voters_off}, outgoing{cs->voters_outgoing, cs->outgoing_off};
+  const List learners{cs->learners, cs->learners_off};
+  const List lnext{cs->learners_next, cs->learners_next_off};
+  std::atomic<uint64_t> flagged{0};
+  parallel_for(G, [&](uint64_t b, uint64_t e) {
+    uint64_t local_flagged = 0;
+    for (uint64_t g = b; g < e; g++) {
+      uint64_t *ids = out->slot_ids + g * S;
+      const PackedGroup r = pack_group(voters, outgoing, learners, lnext, g, S, ids);
+      uint32_t trk = 0;
+      for (uint32_t s = 0; s < S; s++) trk |= ids[s] ? (1u << s) : 0u;
+      put_mask(out->inc_mask, mb, g, r.mi);
+      put_mask(out->out_mask, mb, g, r.mo);
+      put_mask(out->learner_mask, mb, g, r.ml);
+      put_mask(out->learners_next_mask, mb, g, r.mlnx);
+      put_mask(out->is_learner, mb, g, r.ml);  // LearnersNext stay !IsLearner (confchange.go:299-306)
+      put_mask(out->tracked, mb, g, trk);
+      out->auto_leave[g] = (cs->auto_leave && r.flags == 0) ? (cs->auto_leave[g] != 0) : 0;
+      if (group_flags) group_flags[g] = r.flags;
+      local_flagged += r.flags != 0;
     }
     flagged += local_flagged;
   });

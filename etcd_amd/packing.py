@@ -105,12 +105,15 @@ class ConfStates:
     """G raftpb.ConfState messages (raft/raftpb/raft.proto:115-130) in CSR
     form: each field is (ids uint64, off uint64[G+1]) or None."""
 
-    def __init__(self, voters, voters_outgoing=None, learners=None, learners_next=None):
+    def __init__(self, voters, voters_outgoing=None, learners=None, learners_next=None,
+                 auto_leave=None):
         self.G = len(voters)
         self.voters = _csr(voters)
         self.voters_outgoing = _csr(voters_outgoing) if voters_outgoing is not None else None
         self.learners = _csr(learners) if learners is not None else None
         self.learners_next = _csr(learners_next) if learners_next is not None else None
+        self.auto_leave = (None if auto_leave is None else
+                           np.ascontiguousarray(np.asarray(auto_leave, dtype=np.uint8)))
 
     def struct(self):
         from ._lib import QeConfStateCSR
@@ -120,7 +123,8 @@ class ConfStates:
         return QeConfStateCSR(self.G, p(self.voters, 0), p(self.voters, 1),
                               p(self.voters_outgoing, 0), p(self.voters_outgoing, 1),
                               p(self.learners, 0), p(self.learners, 1),
-                              p(self.learners_next, 0), p(self.learners_next, 1))
+                              p(self.learners_next, 0), p(self.learners_next, 1),
+                              _np_ptr(self.auto_leave))
 
 
 def _np_ptr(a):
@@ -141,6 +145,29 @@ def pack_confstates(cs, num_slots):
     p.num_flagged = int(nflag.value)
     p.joint = cs.voters_outgoing is not None
     return p
+
+
+def pack_conf(cs, num_slots):
+    """Native qe_pack_conf: the full tracker.Config of every group (slot
+    ids, Voters[0], Voters[1], Learners, LearnersNext, IsLearner, tracked,
+    AutoLeave) as host arrays -- what qe_confchange consumes
+    (confchange/restore.go).  Returns (dict of numpy arrays, flags)."""
+    from . import _lib
+    G, S = cs.G, int(num_slots)
+    md = np.uint8 if S <= 8 else np.uint16
+    arr = {"slot_ids": np.zeros(G * S, np.uint64), "auto_leave": np.zeros(G, np.uint8)}
+    for k in ("inc", "out", "learner", "learners_next", "is_learner", "tracked"):
+        arr[k] = np.zeros(G, md)
+    st = cs.struct()
+    c = _lib.QeConf(G, S, 0, _np_ptr(arr["slot_ids"]), _np_ptr(arr["inc"]), _np_ptr(arr["out"]),
+                    _np_ptr(arr["learner"]), _np_ptr(arr["learners_next"]),
+                    _np_ptr(arr["is_learner"]), _np_ptr(arr["tracked"]),
+                    _np_ptr(arr["auto_leave"]))
+    flags = np.zeros(G, dtype=np.uint32)
+    nflag = ctypes.c_uint64(0)
+    _lib.check("qe_pack_conf", _lib.lib().qe_pack_conf(ctypes.byref(st), ctypes.byref(c),
+                                                       _np_ptr(flags), ctypes.byref(nflag)))
+    return arr, flags
 
 
 def pack_progress(p, progress, stride=None):

@@ -401,6 +401,7 @@ typedef struct qe_confstate_csr {
   const uint64_t *voters_outgoing, *outgoing_off;
   const uint64_t *learners, *learners_off;
   const uint64_t *learners_next, *learners_next_off;
+  const uint8_t *auto_leave;    /* [G] ConfState.auto_leave (ABI 2; NULL = false) */
 } qe_confstate_csr;
 
 /* group_flags bits reported by qe_pack_confstate */
@@ -484,6 +485,19 @@ typedef struct qe_conf {
   void *tracked;                /* slots holding a Progress                 */
   uint8_t *auto_leave;          /* [G] Config.AutoLeave                     */
 } qe_conf;
+
+/* The whole tracker.Config of each group from its ConfState, as
+ * ProgressTracker.ConfState / confchange.Restore see it (raft/tracker/
+ * tracker.go:146-154, raft/confchange/restore.go:1-155): slot_ids (voters of
+ * both halves ascending, then learners), Voters[0], Voters[1], Learners,
+ * LearnersNext (outgoing voters only), Progress.IsLearner (= Learners; a
+ * LearnersNext peer is still a voter), tracked (every placed peer) and
+ * AutoLeave -- the state qe_confchange consumes.  All pointers in `out` are
+ * HOST pointers here (copy them to the device for qe_confchange); its
+ * num_groups must equal cs->num_groups.  Flagged groups (QE_PACK_*) are left
+ * empty. */
+int qe_pack_conf(const qe_confstate_csr *cs, const qe_conf *out, uint32_t *group_flags,
+                 uint64_t *num_flagged);
 
 /* One operation per group with up to max_changes ConfChangeSingle entries:
  * change c of group g at [c*stride + g]. */

@@ -19,6 +19,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from etcd_amd import engine  # noqa: E402
 
+bench.engine = engine  # bench.py imports the engine lazily in its main()
+
 ROUNDS, LAUNCHES = 5, 15
 
 

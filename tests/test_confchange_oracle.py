@@ -22,3 +22,14 @@ def test_fixture_counts():
 def test_oracle_reproduces_testdata(name):
     for st, out in cc.replay(FILES[name]["steps"]):
         assert out == st["expect"], f"{name}:{st['line']} {st['cmd']} {st['input']}"
+
+
+def test_change_batch_refuses_more_than_255_changes():
+    """qe_conf_changes.count is a u8 per group: the Python mirror refuses a
+    longer list up front instead of truncating it."""
+    import pytest
+    from etcd_amd import confchange as C
+    from etcd_amd.tracker import ProgressTracker
+    ch = C.Changer(ProgressTracker(), LastIndex=1, device="cpu")
+    with pytest.raises(ValueError):
+        C.ChangeBatch([ch], [1], [[C.ConfChangeSingle(0, 1)] * 256], device="cpu")

@@ -295,3 +295,74 @@ def test_python_mirror_testdata():
             assert got == st["expect"], f"{name}:{st['line']}"
             n += 1
     assert n == 58
+
+
+def test_confstate_round_trip_seeds_confchange(eng):
+    """A ConfState (raft.proto:115-130) packed by qe_pack_conf seeds
+    qe_confchange: random configurations built by the oracle Changer are
+    exported as ConfState wire lists (voters, voters_outgoing, learners,
+    learners_next, auto_leave), packed, loaded, and then both sides run the
+    same random changes (confchange/restore.go semantics: every member holds
+    a Progress, LearnersNext are outgoing voters that are not IsLearner)."""
+    from etcd_amd.packing import ConfStates, pack_conf
+    rng = random.Random(4242)
+    G, S = 400, 8
+    pools = [rng.sample(range(1, 1 << 40), 6) for _ in range(G)]
+    changers = [cc.Changer() for _ in range(G)]
+    for k in range(6):  # build varied states (joint, learners, LearnersNext)
+        for g in range(G):
+            o = changers[g]
+            o.last_index = k
+            op = rng.choice([cc.OP_SIMPLE, cc.OP_ENTER_JOINT, cc.OP_ENTER_JOINT_AUTO,
+                             cc.OP_LEAVE_JOINT])
+            o.run(op, random_ccs(rng, pools[g], 3) if op != cc.OP_LEAVE_JOINT else [])
+    lists = {"voters": [], "voters_outgoing": [], "learners": [], "learners_next": []}
+    for o in changers:
+        lists["voters"].append(sorted(o.cfg.inc))
+        lists["voters_outgoing"].append(sorted(o.cfg.out))
+        lists["learners"].append(sorted(o.cfg.learners))
+        lists["learners_next"].append(sorted(o.cfg.lnext))
+    auto = [int(o.cfg.auto_leave) for o in changers]
+    assert any(lists["learners_next"]) and any(lists["voters_outgoing"]) and any(auto)
+    arr, flags = pack_conf(ConfStates(**lists, auto_leave=auto), S)
+    assert not flags.any()
+    cs = eng.ConfState(G, S, DEV)
+    cs.slot_ids.copy_(torch.from_numpy(arr["slot_ids"].view(np.int64)))
+    for k in eng.ConfState.MASKS:
+        cs_t = getattr(cs, k)
+        cs_t.copy_(torch.from_numpy(arr[k]))
+    cs.auto_leave.copy_(torch.from_numpy(arr["auto_leave"]))
+    ps = eng.ProgressState(G, S, 1, 1, DEV)
+    nxt = np.ones(S * ps.stride, np.uint64)
+    flg = np.zeros(S * ps.stride, np.uint8)
+    ids = arr["slot_ids"].reshape(G, S)
+    for g, o in enumerate(changers):
+        for s in range(S):
+            if ids[g, s]:
+                nxt[s * ps.stride + g] = o.prs[int(ids[g, s])].next
+                flg[s * ps.stride + g] = 8  # StateProbe, RecentActive (initProgress)
+    ps.load_host(next=nxt, flags=flg)
+    h = cs.host()
+    for g, o in enumerate(changers):  # the restored state reads back identically
+        cfg, prs = to_oracle(h, ps_host(ps), g, S)
+        assert cfg.string() == o.cfg.string()
+        assert cc.progress_string(prs) == cc.progress_string(o.prs)
+    ch = eng.ConfChanges(G, S, 3, DEV)
+    for k in range(6, 10):
+        ops, ccs = [], []
+        for g in range(G):
+            ops.append(rng.choice([cc.OP_SIMPLE, cc.OP_ENTER_JOINT, cc.OP_LEAVE_JOINT]))
+            ccs.append(random_ccs(rng, pools[g], 3) if ops[-1] != cc.OP_LEAVE_JOINT else [])
+        set_changes(ch, ops, ccs, [k] * G)
+        eng.confchange(cs, ch, ps)
+        torch.cuda.synchronize()
+        res = ch.result.cpu().numpy()
+        h, hp = cs.host(), ps_host(ps)
+        for g, o in enumerate(changers):
+            o.last_index = k
+            want = o.run(ops[g], ccs[g])
+            assert o.peak <= S
+            assert res[g] == want, (g, k)
+            cfg, prs = to_oracle(h, hp, g, S)
+            assert cfg.string() == o.cfg.string(), (g, k)
+            assert cc.progress_string(prs) == cc.progress_string(o.prs), (g, k)

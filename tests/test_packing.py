@@ -106,3 +106,42 @@ def test_pack_threads_knob_keeps_results():
     np.testing.assert_array_equal(a.slot_ids, b.slot_ids)
     np.testing.assert_array_equal(a.inc, b.inc)
     assert L.qe_pack_threads(-1) == _lib.QE_ERANGE
+
+
+def test_pack_conf_full_tracker_config():
+    """qe_pack_conf writes the whole tracker.Config of a ConfState
+    (confchange/restore.go): LearnersNext (outgoing voters only), IsLearner
+    (= Learners), tracked (every placed peer) and AutoLeave."""
+    from etcd_amd.packing import pack_conf
+    cs = ConfStates(
+        voters=[[1, 2, 3], [4, 5], [1], [7, 8]],
+        voters_outgoing=[[], [4, 6], [], [8, 9]],
+        learners=[[10], [7], [0], []],
+        learners_next=[[], [6], [], [9]],
+        auto_leave=[0, 1, 0, 1])
+    arr, flags = pack_conf(cs, 8)
+    ids = arr["slot_ids"].reshape(4, 8)
+    # group 0: voters 1,2,3 then learner 10
+    assert ids[0].tolist() == [1, 2, 3, 10, 0, 0, 0, 0]
+    assert int(arr["inc"][0]) == 0b0111 and int(arr["out"][0]) == 0
+    assert int(arr["learner"][0]) == 0b1000 and int(arr["is_learner"][0]) == 0b1000
+    assert int(arr["tracked"][0]) == 0b1111 and int(arr["learners_next"][0]) == 0
+    # group 1: joint (4,5 | 4,6), learner 7, LearnersNext 6, AutoLeave
+    assert ids[1].tolist()[:4] == [4, 5, 6, 7]
+    assert int(arr["inc"][1]) == 0b0011 and int(arr["out"][1]) == 0b0101
+    assert int(arr["learners_next"][1]) == 0b0100 and int(arr["is_learner"][1]) == 0b1000
+    assert int(arr["tracked"][1]) == 0b1111 and arr["auto_leave"][1] == 1
+    # group 2: a learner with ID 0 (raft.None) is flagged and the group left empty
+    assert flags[2] & _lib.QE_PACK_ZERO_ID
+    assert not ids[2].any() and int(arr["tracked"][2]) == 0 and arr["auto_leave"][2] == 0
+    # group 3
+    assert ids[3].tolist()[:3] == [7, 8, 9]
+    assert int(arr["learners_next"][3]) == 0b100 and int(arr["out"][3]) == 0b110
+    assert arr["auto_leave"][3] == 1 and flags[3] == 0
+
+
+def test_zero_id_learner_flagged_by_pack_confstate():
+    cs = ConfStates(voters=[[1, 2]], learners=[[0]])
+    p = pack_confstates(cs, 4)
+    assert p.flags[0] & _lib.QE_PACK_ZERO_ID
+    assert not p.slot_ids.any() and int(p.learner[0]) == 0
