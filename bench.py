@@ -50,6 +50,9 @@ WORKLOADS = {
                      "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
     "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
                      1 << 21, 5, "elec"),
+    "config5_prevote_cq": ("2M groups x 64 fused election steps with PreVote and CheckQuorum "
+                           "(5 voters, drop 0.2, grant 0.5, peer active 0.7)", 1 << 21, 5,
+                           "elec_pvcq"),
     "progress_step": ("16M groups x 5 peers: one round of MsgAppResp accept/reject + "
                       "MsgHeartbeatResp through the full Progress state machine "
                       "(inflights F=8, leader-log model R=4)", 1 << 24, 5, "progress"),
@@ -266,7 +269,12 @@ def setup(name, G, S, kind, d, stats):
         bpg = 40 * S + 26 + 1  # SURVEY.md §8(d) config 4 (+ ReadIndex out byte)
         return step, bpg, G, "group-rounds", {"b": b, "st": st, "resp": resp,
                                                "prepare": prepare}
-    if kind == "elec":
+    if kind in ("elec", "elec_pvcq"):
+        # config 5; elec_pvcq: raft.Config{PreVote, CheckQuorum} with each
+        # peer heard from within an election timeout with p = 0.7
+        flags = 0 if kind == "elec" else (engine._lib.QE_ELEC_PREVOTE |
+                                          engine._lib.QE_ELEC_CHECK_QUORUM)
+        p_active = 0 if kind == "elec" else 45875
         b = engine.SlotBatch(G, S, d.dev, masks=("inc",), votes=False, group_offset=goff)
         engine.gen_groups(b, 0x5EED)
         est = engine.ElectionState(b, engine.first_voter_slot(b))
@@ -279,7 +287,8 @@ def setup(name, G, S, kind, d, stats):
         sp = engine._ptr(stats)
 
         def step():
-            p = engine.QeElectionParams(0xE1EC, counter["step0"], steps_per_launch, 13107, 32768, 0)
+            p = engine.QeElectionParams(0xE1EC, counter["step0"], steps_per_launch, 13107, 32768,
+                                        flags, p_active, 0, None, None, None, 0)
             engine.check("qe_election_steps", lib.qe_election_steps(C.byref(s_), C.byref(p), sp, stream))
             counter["step0"] += steps_per_launch
 

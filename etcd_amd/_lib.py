@@ -25,7 +25,8 @@ QE_ECOMM = -1001
 QE_INDEX_INF = (1 << 64) - 1
 QE_MAX_SLOTS = 16
 QE_VOTE_PENDING, QE_VOTE_LOST, QE_VOTE_WON = 1, 2, 3
-QE_STATE_FOLLOWER, QE_STATE_CANDIDATE, QE_STATE_LEADER = 0, 1, 2
+QE_STATE_FOLLOWER, QE_STATE_CANDIDATE, QE_STATE_LEADER, QE_STATE_PRE_CANDIDATE = 0, 1, 2, 3
+QE_ELEC_PREVOTE, QE_ELEC_CHECK_QUORUM = 1, 2
 QE_STATS_COUNTERS = 16
 QE_STATS_SHARDS = 64
 QE_STATS_WORDS = QE_STATS_COUNTERS * QE_STATS_SHARDS
@@ -75,7 +76,9 @@ class QeElectionState(C.Structure):
 
 class QeElectionParams(C.Structure):
     _fields_ = [("seed", u64), ("step0", u64), ("steps", u32), ("p_drop_q16", u32),
-                ("p_grant_q16", u32), ("reserved", u32)]
+                ("p_grant_q16", u32), ("flags", u32), ("p_active_q16", u32), ("reserved", u32),
+                ("script_resp", vp), ("script_grant", vp), ("script_hup", vp),
+                ("script_stride", u64)]
 
 
 class QeGenParams(C.Structure):

@@ -319,7 +319,11 @@ int qe_election_steps(const qe_election_state *s, const qe_election_params *p, u
   if (s->num_groups == 0) return QE_OK;
   if (!s->term || !s->state || !s->voted || !s->granted || !s->self_slot) return QE_EINVAL;
   if (s->out_mask && !s->inc_mask) return QE_EINVAL;
-  if (p->p_drop_q16 > 65536 || p->p_grant_q16 > 65536) return QE_ERANGE;
+  if (p->p_drop_q16 > 65536 || p->p_grant_q16 > 65536 || p->p_active_q16 > 65536)
+    return QE_ERANGE;
+  if (p->flags & ~(QE_ELEC_PREVOTE | QE_ELEC_CHECK_QUORUM)) return QE_EINVAL;
+  if (p->reserved) return QE_EINVAL;
+  if (p->script_resp && (!p->script_grant || p->script_stride < s->num_groups)) return QE_EINVAL;
   EArgs a{};
   a.G = s->num_groups;
   a.goff = s->group_offset;
@@ -336,6 +340,12 @@ int qe_election_steps(const qe_election_state *s, const qe_election_params *p, u
   a.steps = p->steps;
   a.p_drop = p->p_drop_q16;
   a.p_grant = p->p_grant_q16;
+  a.flags = p->flags;
+  a.p_active = p->p_active_q16;
+  a.sresp = p->script_resp;
+  a.sgrant = p->script_grant;
+  a.shup = p->script_resp ? p->script_hup : nullptr;
+  a.sstride = p->script_stride;
   a.stats = stats;
   return dispatch_elec(s->num_slots, a, static_cast<hipStream_t>(stream));
 }

@@ -488,17 +488,20 @@ struct EArgs {
   const uint8_t *self_slot;
   const void *inc, *out, *learner;
   uint64_t seed, step0;
-  uint32_t steps, p_drop, p_grant;
+  uint32_t steps, p_drop, p_grant, flags, p_active;
+  const void *sresp, *sgrant;
+  const uint8_t *shup;
+  uint64_t sstride;
   uint64_t *stats;
 };
 
 enum { E_GROUPS, E_ELEC, E_LEAD, E_DOWN, E_WON, E_LOST, E_PEND, E_GR, E_RJ, E_VIOL, E_CSUM, E_N };
 
-// cnt: per-lane 32-bit step counters (flushed into 64-bit totals per chunk);
-// E_LEAD / E_DOWN equal E_WON / E_LOST and are filled in at the flush.
-__device__ __forceinline__ void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd,
-                                           uint32_t gr, uint32_t gbefore, uint32_t &sta,
-                                           uint32_t (&cnt)[E_N]) {
+// One TallyVotes with the invariant checks; counts into the
+// per-lane 32-bit step counters.
+__device__ __forceinline__ uint32_t elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd,
+                                               uint32_t gr, uint32_t gbefore,
+                                               uint32_t (&cnt)[E_N]) {
   const uint32_t voters = (mi | mo) & ~ml;
   const uint32_t gcn = popc(vd & gr & voters), rcn = popc(vd & ~gr & voters);
   const uint32_t res = joint_vote(mi, mo, vd, gr);
@@ -512,7 +515,33 @@ __device__ __forceinline__ void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml
   cnt[E_WON] += (res == kVoteWon);
   cnt[E_LOST] += (res == kVoteLost);
   cnt[E_PEND] += (res == kVotePending);
-  sta = res == kVoteWon ? QE_STATE_LEADER : (res == kVoteLost ? QE_STATE_FOLLOWER : sta);
+  return res;
+}
+
+// raft.campaign (raft/raft.go:785-803): PreVote -> becomePreCandidate (term
+// kept), else becomeCandidate (term+1); votes reset; self-vote; a won
+// (single-voter) tally moves on to the election / leadership.
+__device__ __forceinline__ void elec_campaign(bool pre, uint32_t mi, uint32_t mo, uint32_t ml,
+                                              uint32_t self, uint64_t &t, uint32_t &sta,
+                                              uint32_t &vd, uint32_t &gr, uint32_t (&cnt)[E_N]) {
+  bool go = true;
+  if (pre) {
+    sta = QE_STATE_PRE_CANDIDATE;
+    vd = self;
+    gr = self;
+    go = elec_tally(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon;
+  }
+  if (go) {
+    t += 1;
+    sta = QE_STATE_CANDIDATE;
+    vd = self;
+    gr = self;
+    cnt[E_ELEC] += 1;
+    if (elec_tally(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon) {
+      sta = QE_STATE_LEADER;
+      cnt[E_LEAD] += 1;
+    }
+  }
 }
 
 template <int S, typename MT>
@@ -526,6 +555,9 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
   const MT *incp = static_cast<const MT *>(a.inc), *outp = static_cast<const MT *>(a.out);
   const MT *lrnp = static_cast<const MT *>(a.learner);
   MT *vdp = static_cast<MT *>(a.voted), *grp = static_cast<MT *>(a.granted);
+  const MT *srp = static_cast<const MT *>(a.sresp), *sgp = static_cast<const MT *>(a.sgrant);
+  const bool pre = (a.flags & QE_ELEC_PREVOTE) != 0;
+  const bool cq = (a.flags & QE_ELEC_CHECK_QUORUM) != 0;
 
   for (uint64_t g = tid; g < a.G; g += nthreads) {
     const uint64_t gid = a.goff + g;
@@ -533,17 +565,18 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
     const uint32_t mo = outp ? (outp[g] & kFull) : 0u;
     const uint32_t ml = lrnp ? (lrnp[g] & kFull) : 0u;
     const uint32_t self = 1u << (a.self_slot[g] % S);
-    const uint32_t prog = mi | mo | ml;
-    const bool promotable = (self & (mi | mo)) != 0 && (self & ml) == 0;
+    const uint32_t voters = mi | mo;
+    const bool promotable = (self & voters) != 0 && (self & ml) == 0;
     uint64_t t = a.term[g];
     uint32_t sta = a.state[g];
     uint32_t vd = vdp[g] & kFull, gr = grp[g] & kFull;
-    const uint32_t others = prog & ~self;
+    // campaign sends (pre)vote requests to Voters.IDs() (raft.go:813-834)
+    const uint32_t peers = voters & ~self;
     // counter-based RNG key (oracle/quorum_oracle.c elec_gkey), once per group
     const uint64_t gk64 = mix64(a.seed + gid * kPhi) ^ 0x6A09E667F3BCC909ull;
     const uint32_t gkey = static_cast<uint32_t>(gk64) ^ static_cast<uint32_t>(gk64 >> 32);
     // 32-bit step counters per chunk of <= 2^24 steps (no overflow: at most
-    // 16 grants per step), flushed into the 64-bit totals
+    // 2 tallies x 16 grants per step), flushed into the 64-bit totals
     for (uint32_t k0 = 0; promotable && k0 < a.steps; k0 += (1u << 24)) {
       const uint32_t kend = a.steps - k0 < (1u << 24) ? a.steps : k0 + (1u << 24);
       uint32_t c32[E_N];
@@ -551,35 +584,65 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
       for (int i = 0; i < E_N; i++) c32[i] = 0;
       for (uint32_t k = k0; k < kend; k++) {
         const uint64_t step = a.step0 + k;
-        if (sta != QE_STATE_CANDIDATE) {
-          // hup -> campaign: becomeCandidate (term+1, ResetVotes), self-vote.
-          t += 1;
-          vd = self;
-          gr = self;
-          sta = QE_STATE_CANDIDATE;
-          c32[E_ELEC] += 1;
-          elec_tally(mi, mo, ml, vd, gr, 0u, sta, c32);
+        const uint32_t hb = gkey + static_cast<uint32_t>(step) * 0x9E3779B1u;
+        uint32_t resp = 0, val = 0;
+        bool hup = false;
+        if (srp) {
+          const uint64_t so = static_cast<uint64_t>(k) * a.sstride + g;
+          resp = srp[so] & peers;
+          val = sgp[so] & resp;
+          hup = a.shup && a.shup[so] != 0;
+        }
+        if (sta == QE_STATE_LEADER && cq) {
+          // CheckQuorum round (raft.go:997-1018)
+          if (!srp) {
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+              const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u + 0x27D4EB2Fu);
+              resp |= (((peers >> s) & 1u) && (d & 0xFFFFu) < a.p_active) ? (1u << s) : 0u;
+            }
+          }
+          const uint32_t recent = resp | self;
+          const uint32_t present = voters & ~ml;
+          const bool qa = joint_vote(mi, mo, present, recent & present) == kVoteWon;
+          const bool qb = joint_vote(mo, mi, present, recent & present) == kVoteWon;
+          c32[E_VIOL] += (qa != qb);
+          if (!qa) {
+            sta = QE_STATE_FOLLOWER;
+            c32[E_DOWN] += 1;
+          }
+        } else if (sta == QE_STATE_FOLLOWER || sta == QE_STATE_LEADER || hup) {
+          elec_campaign(pre, mi, mo, ml, self, t, sta, vd, gr, c32);
         } else {
           // d = fmix32(gkey + step*C1 + s*C2) per slot (oracle elec_draw)
-          const uint32_t hb = gkey + static_cast<uint32_t>(step) * 0x9E3779B1u;
-          uint32_t resp = 0, val = 0;
+          if (!srp) {
 #pragma unroll
-          for (int s = 0; s < S; s++) {
-            const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u);
-            const bool deliver = ((others >> s) & 1u) && (d & 0xFFFFu) >= a.p_drop;
-            resp |= deliver ? (1u << s) : 0u;
-            val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
+            for (int s = 0; s < S; s++) {
+              const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u);
+              const bool deliver = ((peers >> s) & 1u) && (d & 0xFFFFu) >= a.p_drop;
+              resp |= deliver ? (1u << s) : 0u;
+              val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
+            }
           }
-          const uint32_t gbefore = popc(gr & vd & ~ml & (mi | mo));
+          const uint32_t gbefore = popc(gr & vd & ~ml & voters);
           const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
           vd |= fresh;
           gr |= fresh & val;
-          elec_tally(mi, mo, ml, vd, gr, gbefore, sta, c32);
+          const uint32_t res = elec_tally(mi, mo, ml, vd, gr, gbefore, c32);
+          if (res == kVoteWon) {
+            if (sta == QE_STATE_PRE_CANDIDATE) {
+              elec_campaign(false, mi, mo, ml, self, t, sta, vd, gr, c32);
+            } else {
+              sta = QE_STATE_LEADER;
+              c32[E_LEAD] += 1;
+            }
+          } else if (res == kVoteLost) {
+            sta = QE_STATE_FOLLOWER;
+            c32[E_DOWN] += 1;
+          }
         }
       }
       c32[E_GROUPS] = kend - k0;
-      c32[E_LEAD] = c32[E_WON];
-      c32[E_DOWN] = c32[E_LOST];
 #pragma unroll
       for (int i = 0; i < E_N; i++) cnt[i] += c32[i];
     }

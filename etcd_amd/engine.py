@@ -244,8 +244,13 @@ def first_voter_slot(batch):
     return slot
 
 
-def election_steps(est, seed, step0, steps, p_drop=13107, p_grant=32768, stats=None):
-    p = QeElectionParams(seed, step0, steps, p_drop, p_grant, 0)
+def election_steps(est, seed, step0, steps, p_drop=13107, p_grant=32768, stats=None, flags=0,
+                   p_active=0, script=None):
+    """script: None or (resp, grant, hup, stride) device tensors [steps][stride]
+    (hup may be None) replacing the RNG (qe_election_params scripted mode)."""
+    sr, sg, sh, ss = script if script is not None else (None, None, None, 0)
+    p = QeElectionParams(seed, step0, steps, p_drop, p_grant, flags, p_active, 0, _ptr(sr),
+                         _ptr(sg), _ptr(sh), ss)
     s = est.struct()
     check("qe_election_steps", _lib.lib().qe_election_steps(C.byref(s), C.byref(p), _ptr(stats),
                                                              _stream(est.batch.device)))

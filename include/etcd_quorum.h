@@ -68,6 +68,7 @@ extern "C" {
 #define QE_STATE_FOLLOWER 0
 #define QE_STATE_CANDIDATE 1
 #define QE_STATE_LEADER 2
+#define QE_STATE_PRE_CANDIDATE 3
 
 /* Status codes */
 #define QE_OK 0
@@ -237,14 +238,39 @@ typedef struct qe_election_params {
   uint32_t steps;            /* fused steps per launch (state in registers)  */
   uint32_t p_drop_q16;       /* P(response dropped) * 65536                  */
   uint32_t p_grant_q16;      /* P(vote granted | delivered) * 65536          */
+  uint32_t flags;            /* QE_ELEC_* (ABI 1: reserved, 0)                */
+  uint32_t p_active_q16;     /* CheckQuorum: P(a leader heard from a peer
+                                within an election timeout) * 65536        */
   uint32_t reserved;
+  /* Scripted mode (replaying a recorded or test message flow): when
+   * script_resp is non-NULL, step k of group g takes its responses from
+   * [k*script_stride + g] of these arrays instead of the RNG. */
+  const void *script_resp;   /* mask-typed: peers whose (pre)vote response
+                                arrives / that were active (CheckQuorum)   */
+  const void *script_grant;  /* mask-typed: the responses that grant        */
+  const uint8_t *script_hup; /* 1: the election timeout fires this step
+                                (a (pre)candidate campaigns again); NULL
+                                = never                                     */
+  uint64_t script_stride;    /* >= num_groups                                */
 } qe_election_params;
 
-/* `steps` election steps per group: Leader/Follower campaign
- * (term+1, ResetVotes, self RecordVote; raft/raft.go:785-803), Candidate
- * receives one round of MsgVoteResp (drops/grants from a counter-based RNG)
- * -> RecordVote -> TallyVotes -> VoteWon: Leader, VoteLost: Follower
- * (raft/raft.go:837-845, :1399-1414).  Invariant checks go to stats. */
+#define QE_ELEC_PREVOTE 1u       /* raft.Config.PreVote                      */
+#define QE_ELEC_CHECK_QUORUM 2u  /* raft.Config.CheckQuorum                  */
+
+/* `steps` election steps per group:
+ *   Leader: CheckQuorum on -> one CheckQuorum round (raft/raft.go:997-1018):
+ *     the leader sees itself active, each other voter active with
+ *     p_active; !QuorumActive (tracker.go:215-225) -> becomeFollower (term
+ *     kept).  CheckQuorum off -> the leader is deposed and campaigns.
+ *   Follower (or a (pre)candidate whose timeout fires, script_hup): hup ->
+ *     campaign (raft.go:785-803): PreVote on -> becomePreCandidate (term
+ *     kept), else becomeCandidate (term+1); self-vote; a won tally moves on
+ *     (pre-vote -> election -> leader).
+ *   PreCandidate / Candidate: one round of responses from every other voter
+ *     (drops/grants from a counter-based RNG) -> RecordVote -> TallyVotes
+ *     (raft.go:837-845, :1399-1414): won -> campaign(campaignElection) /
+ *     becomeLeader; lost -> becomeFollower (term kept); pending -> stay.
+ * Invariant checks go to stats. */
 int qe_election_steps(const qe_election_state *st,
                       const qe_election_params *p, uint64_t *stats,
                       void *stream);

@@ -51,7 +51,8 @@ def _declare(L):
         "orc_replication_round_batch": (None, [u64, u64, u32, u64, vp, vp, vp, vp, vp, vp, vp, vp,
                                                vp, vp, vp, vp, vp, i32]),
         "orc_election_steps_batch": (None, [u64, u64, u32, vp, vp, vp, vp, vp, vp, vp, vp, u64,
-                                            u64, u32, u32, u32, vp, i32]),
+                                            u64, u32, u32, u32, u32, u32, vp, vp, vp, u64, vp,
+                                            i32]),
         "orc_gf_build": (vp, [u64, u32, u64, vp, vp, vp, vp, vp, vp]),
         "orc_gf_free": (None, [vp]),
         "orc_gf_run": (dbl, [vp, vp, vp, i32, i32]),
@@ -139,11 +140,14 @@ def replication_round(G, goff, S, stride, match, nxt, committed, term_start, las
 
 
 def election_steps(G, goff, S, term, state, voted, granted, self_slot, inc, out, learner, seed,
-                   step0, steps, p_drop, p_grant, threads=0):
+                   step0, steps, p_drop, p_grant, threads=0, flags=0, p_active=0, script=None):
+    """script: None or (resp, grant, hup, stride) arrays [steps][stride]."""
     stats = np.zeros(NSTAT, np.uint64)
+    sr, sg, sh, ss = script if script is not None else (None, None, None, 0)
     lib().orc_election_steps_batch(G, goff, S, P(term), P(state), P(voted), P(granted),
                                    P(self_slot), P(inc), P(out), P(learner), seed, step0, steps,
-                                   p_drop, p_grant, P(stats), threads)
+                                   p_drop, p_grant, flags, p_active, P(sr), P(sg), P(sh), ss,
+                                   P(stats), threads)
     return stats
 
 

@@ -472,12 +472,15 @@ uint64_t orc_checksum_elec(uint64_t gid, uint64_t term, uint32_t state, uint32_t
   return orc_mix64((gid * PHI) ^ term ^ tag);
 }
 
-/* One TallyVotes + transition with the invariant checks of DESIGN.md §5. */
-static void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd, uint32_t gr,
-                       uint32_t gbefore, uint32_t *sta, uint64_t *ls) {
+/* One TallyVotes (raft.go:837-845, tracker.go:267-288) with the invariant
+ * checks of DESIGN.md §5: the result is symmetric in the halves, VoteWon
+ * implies a granted quorum in both halves, and the granted count never
+ * falls within a term (gbefore). */
+static uint8_t elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd, uint32_t gr,
+                          uint32_t gbefore, uint64_t *ls) {
   int gcn, rcn;
-  uint8_t res = orc_tally(mi, mo, ml, vd, gr, &gcn, &rcn); /* raft.go:845 */
-  uint8_t sym = orc_joint_vote(mo, mi, vd, gr);           /* symmetry */
+  uint8_t res = orc_tally(mi, mo, ml, vd, gr, &gcn, &rcn);
+  uint8_t sym = orc_joint_vote(mo, mi, vd, gr);
   int n0 = popc(mi), n1 = popc(mo);
   int won_ok = (n0 == 0 || popc(gr & vd & mi) >= n0 / 2 + 1) &&
                (n1 == 0 || popc(gr & vd & mo) >= n1 / 2 + 1);
@@ -485,21 +488,17 @@ static void elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd, uint3
                        (uint64_t)((uint32_t)gcn < gbefore);
   ls[ST_GRANTED] += (uint64_t)gcn;
   ls[ST_REJECTED] += (uint64_t)rcn;
-  if (res == VOTE_WON) {            /* becomeLeader, raft.go:1402-1409 */
-    *sta = 2; ls[ST_LEADERS] += 1; ls[ST_WON] += 1;
-  } else if (res == VOTE_LOST) {    /* becomeFollower, raft.go:1410-1413 */
-    *sta = 0; ls[ST_STEPDOWNS] += 1; ls[ST_LOST] += 1;
-  } else {
-    ls[ST_PENDING] += 1;
-  }
+  ls[res == VOTE_WON ? ST_WON : (res == VOTE_LOST ? ST_LOST : ST_PENDING)] += 1;
+  return res;
 }
 
 /* Counter-based response RNG: per group gkey = mix64(seed +
  * gid*PHI) ^ IV folded to 32 bits (k = lo ^ hi); slot s at step t draws
  * d = fmix32(k + t*C1 + s*C2) (MurmurHash3's 32-bit finalizer), bits 0-15
- * the drop draw and bits 16-31 the grant draw. */
+ * the drop draw and bits 16-31 the grant draw; the CheckQuorum activity
+ * draw of a leader's peer is bits 0-15 of fmix32(k + t*C1 + s*C2 + C3). */
 static const uint64_t ELEC_IV = 0x6A09E667F3BCC909ULL;
-static const uint32_t ELEC_C1 = 0x9E3779B1u, ELEC_C2 = 0x85EBCA77u;
+static const uint32_t ELEC_C1 = 0x9E3779B1u, ELEC_C2 = 0x85EBCA77u, ELEC_C3 = 0x27D4EB2Fu;
 static inline uint32_t elec_gkey(uint64_t seed, uint64_t gid) {
   uint64_t k = orc_mix64(seed + gid * PHI) ^ ELEC_IV;
   return (uint32_t)k ^ (uint32_t)(k >> 32);
@@ -516,11 +515,55 @@ static inline uint32_t elec_draw(uint32_t gkey, uint64_t step, uint32_t s) {
   return orc_fmix32(gkey + (uint32_t)step * ELEC_C1 + s * ELEC_C2);
 }
 
+#define ELEC_PREVOTE 1u
+#define ELEC_CHECK_QUORUM 2u
+enum { SF = 0, SC = 1, SL = 2, SP = 3 }; /* StateFollower/Candidate/Leader/PreCandidate */
+
+/* raft.campaign (raft.go:785-803) of a promotable node: PreVote ->
+ * becomePreCandidate (votes reset, term kept), else becomeCandidate (term+1,
+ * votes reset); the self-vote poll; a won (single-voter) pre-vote goes on to
+ * campaign(campaignElection) and a won election to becomeLeader. */
+static void elec_campaign(int pre, uint32_t mi, uint32_t mo, uint32_t ml, uint32_t self,
+                          uint64_t *t, uint32_t *sta, uint32_t *vd, uint32_t *gr, uint64_t *ls) {
+  if (pre) {
+    *sta = SP;                                   /* becomePreCandidate (:708-722) */
+    *vd = 0; *gr = 0;
+    orc_record_votes(vd, gr, self, self);
+    if (elec_tally(mi, mo, ml, *vd, *gr, 0, ls) != VOTE_WON) return;
+  }
+  *t += 1;                                       /* becomeCandidate (:695-706) */
+  *sta = SC;
+  *vd = 0; *gr = 0;
+  orc_record_votes(vd, gr, self, self);
+  ls[ST_ELECTIONS] += 1;
+  if (elec_tally(mi, mo, ml, *vd, *gr, 0, ls) == VOTE_WON) {
+    *sta = SL;                                   /* becomeLeader */
+    ls[ST_LEADERS] += 1;
+  }
+}
+
+/* `steps` election steps per group.  Per step:
+ *   Leader     CheckQuorum on: one CheckQuorum round (raft.go:997-1018): its
+ *              peers' RecentActive from the activity draw (or the script),
+ *              self active; !QuorumActive -> becomeFollower (term kept).
+ *              CheckQuorum off: the leader is deposed and campaigns (the
+ *              simulation keeps elections going).
+ *   Follower, or a (pre)candidate whose election timeout fires (script_hup):
+ *              hup -> campaign (pre-vote first when PreVote is on).
+ *   PreCandidate / Candidate: one round of (pre)vote responses from every
+ *              other voter (campaign sends to Voters.IDs(), :813-834):
+ *              RecordVote + TallyVotes (stepCandidate, :1399-1414): won ->
+ *              campaign(campaignElection) / becomeLeader; lost ->
+ *              becomeFollower (term kept); pending -> stay.
+ * Non-promotable nodes (no Progress, or a learner, :1618-1623) never step.
+ * Script arrays ([steps][sstride]) replace the RNG when sresp != NULL. */
 void orc_election_steps_batch(uint64_t G, uint64_t goff, uint32_t S, uint64_t *term,
                               uint8_t *state, void *voted, void *granted, const uint8_t *self_slot,
                               const void *inc, const void *out, const void *learner,
                               uint64_t seed, uint64_t step0, uint32_t steps, uint32_t p_drop,
-                              uint32_t p_grant, uint64_t *stats, int threads) {
+                              uint32_t p_grant, uint32_t flags, uint32_t p_active,
+                              const void *sresp, const void *sgrant, const uint8_t *shup,
+                              uint64_t sstride, uint64_t *stats, int threads) {
   uint32_t mb = S <= 8 ? 1 : 2;
   uint32_t full = (1u << S) - 1u;
   uint64_t st[NSTAT];
@@ -539,36 +582,61 @@ void orc_election_steps_batch(uint64_t G, uint64_t goff, uint32_t S, uint64_t *t
       uint32_t mo = out ? ld_mask(out, mb, g) & full : 0;
       uint32_t ml = ld_mask(learner, mb, g) & full;
       uint32_t self = 1u << (self_slot[g] % S);
-      uint32_t prog = mi | mo | ml;
+      uint32_t voters = mi | mo;
       /* raft.promotable(): own Progress exists and is not a learner */
-      int promotable = (self & (mi | mo)) != 0 && (self & ml) == 0;
+      int promotable = (self & voters) != 0 && (self & ml) == 0;
       uint64_t t = term[g];
       uint32_t sta = state[g];
       uint32_t vd = ld_mask(voted, mb, g) & full, gr = ld_mask(granted, mb, g) & full;
       const uint32_t gkey = elec_gkey(seed, gid);
       for (uint32_t k = 0; k < steps && promotable; k++) {
         uint64_t step = step0 + k;
-        if (sta != 1) {
-          /* hup -> campaign(campaignElection), raft.go:785-803 */
-          t += 1;                                  /* becomeCandidate */
-          vd = 0; gr = 0;                          /* ResetVotes */
-          orc_record_votes(&vd, &gr, self, self);  /* poll(r.id, ..., true) */
-          sta = 1;
-          ls[ST_ELECTIONS] += 1;
-          elec_tally(mi, mo, ml, vd, gr, 0, &sta, ls);
-        } else {
-          /* one round of MsgVoteResp from every other Progress peer */
-          uint32_t resp = 0, val = 0;
-          for (uint32_t s = 0; s < S; s++) {
-            if (!((prog >> s) & 1u) || ((self >> s) & 1u)) continue;
-            uint32_t d = elec_draw(gkey, step, s);
-            if ((d & 0xFFFFu) < p_drop) continue; /* dropped */
-            resp |= 1u << s;
-            if ((d >> 16) < p_grant) val |= 1u << s;
+        uint32_t peers = voters & ~self;
+        uint32_t resp = 0, val = 0;
+        if (sresp) {
+          resp = ld_mask(sresp, mb, k * sstride + g) & peers;
+          val = ld_mask(sgrant, mb, k * sstride + g) & resp;
+        }
+        int hup = shup ? shup[k * sstride + g] != 0 : 0;
+        if (sta == SL && (flags & ELEC_CHECK_QUORUM)) {
+          if (!sresp)
+            for (uint32_t s = 0; s < S; s++) {
+              if (!((peers >> s) & 1u)) continue;
+              uint32_t d = orc_fmix32(gkey + (uint32_t)step * ELEC_C1 + s * ELEC_C2 + ELEC_C3);
+              if ((d & 0xFFFFu) < p_active) resp |= 1u << s;
+            }
+          uint32_t recent = resp | self;  /* the leader always sees itself active */
+          uint8_t qa = orc_quorum_active(mi, mo, ml, recent);
+          ls[ST_VIOLATIONS] += (uint64_t)(qa != orc_quorum_active(mo, mi, ml, recent));
+          if (!qa) {
+            sta = SF;                      /* becomeFollower(r.Term, None) */
+            ls[ST_STEPDOWNS] += 1;
           }
-          uint32_t gbefore = (uint32_t)popc(gr & vd & ~ml & (mi | mo));
-          orc_record_votes(&vd, &gr, resp, val);   /* RecordVote, :844 */
-          elec_tally(mi, mo, ml, vd, gr, gbefore, &sta, ls);
+        } else if (sta == SF || sta == SL || hup) {
+          elec_campaign((flags & ELEC_PREVOTE) != 0, mi, mo, ml, self, &t, &sta, &vd, &gr, ls);
+        } else {
+          if (!sresp)
+            for (uint32_t s = 0; s < S; s++) {
+              if (!((peers >> s) & 1u)) continue;
+              uint32_t d = elec_draw(gkey, step, s);
+              if ((d & 0xFFFFu) < p_drop) continue; /* dropped */
+              resp |= 1u << s;
+              if ((d >> 16) < p_grant) val |= 1u << s;
+            }
+          uint32_t gbefore = (uint32_t)popc(gr & vd & ~ml & voters);
+          orc_record_votes(&vd, &gr, resp, val); /* RecordVote, :844 */
+          uint8_t res = elec_tally(mi, mo, ml, vd, gr, gbefore, ls);
+          if (res == VOTE_WON) {
+            if (sta == SP) {
+              elec_campaign(0, mi, mo, ml, self, &t, &sta, &vd, &gr, ls);
+            } else {
+              sta = SL;
+              ls[ST_LEADERS] += 1;
+            }
+          } else if (res == VOTE_LOST) {
+            sta = SF;
+            ls[ST_STEPDOWNS] += 1;
+          }
         }
         ls[ST_GROUPS] += 1;
       }

@@ -40,6 +40,9 @@ Outputs (data only: inputs + expected outputs):
     raft_snap_test.go's five tests, and the leader side of
     TestLeaderTransferToSlowFollower -- state set up by the tests' code is
     restated per scenario (see progress_scenarios()).
+  tests/golden/election_scenarios.json  scripted election steps:
+    TestLeaderElectionInOneRoundRPC (table), TestLeaderStepdownWhenQuorumLost,
+    TestPreVoteWithSplitVote (node views derived from the test's flow).
 """
 import json
 import os
@@ -491,6 +494,63 @@ def progress_scenarios():
     return sc
 
 
+# ---------------------------------------------------------------------------
+# Election scenarios for qe_election_steps' scripted mode: one group per
+# node view, slot s = node id s+1.  Each step is one qe_election_steps step
+# with the responses the test's message flow delivers (resp = slots whose
+# response arrives, grant = those granting, hup = election timeout fires).
+# ---------------------------------------------------------------------------
+STATE_IDS = {"StateFollower": 0, "StateCandidate": 1, "StateLeader": 2, "StatePreCandidate": 3}
+
+
+def election_scenarios():
+    sc = []
+    # TestLeaderElectionInOneRoundRPC (raft_paper_test.go:192-232): MsgHup
+    # (campaign, Term 1), then one MsgVoteResp per entry of the votes map.
+    for i, r in enumerate(election_table()):
+        steps = [{}]
+        if r["size"] > 1:
+            steps.append({"resp": [vid - 1 for vid, _ in r["votes"]],
+                          "grant": [vid - 1 for vid, v in r["votes"] if v]})
+        steps[-1]["expect"] = {"state": STATE_IDS[r["state"]], "term": 1}
+        sc.append({"name": f"TestLeaderElectionInOneRoundRPC#{i}",
+                   "source": "raft/raft_paper_test.go:192-232", "S": r["size"], "self": 0,
+                   "flags": 0, "term": 0, "state": 0, "steps": steps})
+    # TestLeaderStepdownWhenQuorumLost (raft_test.go:1766-1781): a CheckQuorum
+    # leader of {1,2,3} at Term 1 hears from nobody for an election timeout.
+    sc.append({"name": "TestLeaderStepdownWhenQuorumLost", "source": "raft/raft_test.go:1766-1781",
+               "S": 3, "self": 0, "flags": 2, "term": 1, "state": 2,
+               "steps": [{"resp": [], "expect": {"state": 0, "term": 1}}]})
+    # ... and one that hears from a quorum stays leader (the converse, derived).
+    sc.append({"name": "CheckQuorum keeps a leader that hears from a quorum (derived)",
+               "source": "raft/raft.go:997-1018", "S": 3, "self": 0, "flags": 2, "term": 1,
+               "state": 2, "steps": [{"resp": [2], "expect": {"state": 2, "term": 1}}]})
+    # TestPreVoteWithSplitVote (raft_test.go:3925-3998), derived from the
+    # test's message flow: n1 won Term 2 and is isolated; n2 and n3 (both
+    # Term 2 followers) pre-vote for each other, both win the pre-vote, both
+    # campaign at Term 3 and reject each other (split vote: candidates at
+    # Term 3).  n2 times out first: pre-vote granted by n3, election at Term
+    # 4 granted by n3 -> n2 leads Term 4.  n3's view is followed up to the
+    # split (its step down to follower comes from n2's higher-term MsgVote,
+    # which is not a vote response).
+    n2 = [{"hup": 1},
+          {"resp": [2], "grant": [2]},
+          {"resp": [2], "grant": [], "expect": {"term": 3, "state": 1}},
+          {"hup": 1, "expect": {"term": 3, "state": 3}},
+          {"resp": [2], "grant": [2], "expect": {"term": 4, "state": 1}},
+          {"resp": [2], "grant": [2], "expect": {"term": 4, "state": 2}}]
+    sc.append({"name": "TestPreVoteWithSplitVote/n2 (derived)",
+               "source": "raft/raft_test.go:3925-3998", "S": 3, "self": 1, "flags": 1,
+               "term": 2, "state": 0, "steps": n2})
+    n3 = [{"hup": 1},
+          {"resp": [1], "grant": [1]},
+          {"resp": [1], "grant": [], "expect": {"term": 3, "state": 1}}]
+    sc.append({"name": "TestPreVoteWithSplitVote/n3 (derived)",
+               "source": "raft/raft_test.go:3925-3998", "S": 3, "self": 2, "flags": 1,
+               "term": 2, "state": 0, "steps": n3})
+    return sc
+
+
 def confchange_files():
     """datadriven blocks: `cmd [args]`, input lines, `----`, output up to a
     blank line."""
@@ -550,6 +610,8 @@ def main():
         json.dump(tables, f, indent=1)
     with open(os.path.join(HERE, "progress_scenarios.json"), "w", encoding="utf-8") as f:
         json.dump(progress_scenarios(), f, indent=1)
+    with open(os.path.join(HERE, "election_scenarios.json"), "w", encoding="utf-8") as f:
+        json.dump(election_scenarios(), f, indent=1)
     # election table in a line format for the C++ test: <size> <state> id:0|1,..
     with open(os.path.join(HERE, "election_table.txt"), "w", encoding="utf-8") as f:
         for r in tables["TestLeaderElectionInOneRoundRPC"]["rows"]:

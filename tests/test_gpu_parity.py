@@ -511,9 +511,13 @@ def test_test_commit_table_on_gpu(eng):
 # --------------------------------------------------------------------------
 # Election simulation (config 5)
 # --------------------------------------------------------------------------
-@pytest.mark.parametrize("S,joint", [(1, False), (3, False), (5, False), (7, False), (10, True),
-                                     (16, True)])
-def test_election_steps(eng, orc, S, joint):
+@pytest.mark.parametrize("S,joint,flags", [(1, False, 0), (3, False, 0), (5, False, 0),
+                                           (7, False, 0), (10, True, 0), (16, True, 0),
+                                           (1, False, 3), (3, False, 1), (5, False, 2),
+                                           (5, False, 3), (10, True, 3), (16, True, 1)])
+def test_election_steps(eng, orc, S, joint, flags):
+    """Random election steps (RNG drops/grants), optionally with PreVote (1)
+    and CheckQuorum (2), bit-exact against the oracle."""
     G = 30011
     masks = ("inc", "out", "learner")
     b = eng.SlotBatch(G, S, DEV, masks=masks, votes=False, group_offset=999)
@@ -528,12 +532,15 @@ def test_election_steps(eng, orc, S, joint):
     granted = np.zeros(G, eng.mask_np_dtype(S))
     ss = self_slot.cpu().numpy()
     step0 = 0
+    leaders = 0
     for launch, steps in enumerate((1, 7, 32)):
         stats = eng.stats_buffer(DEV)
-        eng.election_steps(est, 77, step0, steps, p_drop=13107, p_grant=32768, stats=stats)
+        eng.election_steps(est, 77, step0, steps, p_drop=13107, p_grant=32768, stats=stats,
+                           flags=flags, p_active=45875)
         got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
         want = orc.election_steps(G, 999, S, term, state, voted, granted, ss, h["inc"], h["out"],
-                                  h["learner"], 77, step0, steps, 13107, 32768)
+                                  h["learner"], 77, step0, steps, 13107, 32768, flags=flags,
+                                  p_active=45875)
         step0 += steps
         np.testing.assert_array_equal(est.term.cpu().numpy().view(np.uint64), term)
         np.testing.assert_array_equal(est.state.cpu().numpy(), state)
@@ -541,7 +548,31 @@ def test_election_steps(eng, orc, S, joint):
         np.testing.assert_array_equal(est.granted.cpu().numpy().view(granted.dtype), granted)
         np.testing.assert_array_equal(got, want)
         assert want[14] == 0  # invariant violations
-    assert int(want[12]) > 0  # some leaders elected
+        leaders += int(want[12])
+    assert leaders > 0  # some leaders elected
+
+
+def test_election_scenarios_on_gpu(eng):
+    """The scripted election scenarios (TestLeaderElectionInOneRoundRPC,
+    TestLeaderStepdownWhenQuorumLost, TestPreVoteWithSplitVote node views)
+    through k_election on the GPU."""
+    from tests.election_scenarios import run_scenario, scenarios, script_arrays
+    for sc in scenarios():
+        S = sc["S"]
+        b = eng.SlotBatch(1, S, DEV, masks=("inc", "learner"), votes=False)
+        b.inc.fill_((1 << S) - 1)
+        est = eng.ElectionState(b, torch.tensor([sc["self"]], dtype=torch.uint8, device=DEV))
+        est.term.fill_(sc["term"])
+        est.state.fill_(sc["state"])
+        resp, grant, hup = (torch.from_numpy(x).to(DEV) for x in script_arrays(sc))
+        if S > 8:
+            resp, grant = resp.view(torch.int16), grant.view(torch.int16)
+
+        def step(k, est=est, resp=resp, grant=grant, hup=hup, sc=sc):
+            eng.election_steps(est, 0, k, 1, p_drop=0, p_grant=0, flags=sc["flags"],
+                               script=(resp[k:], grant[k:], hup[k:], 1))
+            return int(est.term[0]), int(est.state[0])
+        run_scenario(sc, step)
 
 
 def test_leader_election_table_on_gpu(eng):

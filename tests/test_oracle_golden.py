@@ -146,3 +146,14 @@ def test_progress_update_table():
     for row in raft_tables()["TestProgressUpdate"]["rows"]:
         ok, m, n = Q.maybe_update(row["prev_match"], row["prev_next"], row["update"])
         assert (ok, m, n) == (row["want_ok"], row["want_match"], row["want_next"]), row
+
+
+def test_election_scenarios_on_oracle(orc):
+    """TestLeaderElectionInOneRoundRPC, TestLeaderStepdownWhenQuorumLost and
+    TestPreVoteWithSplitVote (node views) through the oracle's scripted
+    election steps (PreVote, CheckQuorum)."""
+    from tests.election_scenarios import oracle_runner, run_scenario, scenarios
+    scs = scenarios()
+    for sc in scs:
+        run_scenario(sc, oracle_runner(orc, sc))
+    assert len(scs) == 13 + 4
