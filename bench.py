@@ -33,6 +33,10 @@ engine = None  # etcd_amd.engine, imported once the process knows its rank
 
 METRIC = "quorum group-evals/sec at 1/2/4/8 MI355X; % HBM peak; speedup vs Go host"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+# VALU issue peak: 256 CUs x 4 SIMD32 x 2.4 GHz, one wave64 instruction per
+# 2 cycles per SIMD (MI355X_MICROARCH.md: v_fma_f32 wave64 = 2 cyc; the
+# 157.3 TFLOPS fp32 vector peak) = 1.2288e12 wave-instructions/s
+VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
 
 WORKLOADS = {
     # name: (description, groups per GPU, slots, kind)
@@ -266,7 +270,25 @@ def setup(name, G, S, kind, d, stats):
             st.next.copy_(pristine["next"])
             st.committed.copy_(pristine["committed"])
 
-        bpg = 40 * S + 26 + 1  # SURVEY.md §8(d) config 4 (+ ReadIndex out byte)
+        # Algorithmic bytes of this round (what the state machine must read
+        # and write, once): the responder and ReadIndex-ack masks (2 B),
+        # termStart / lastIndex / committed (24 B), every voter's Match (8S),
+        # a responder's m.Index and Next (16 B each); writes only where
+        # MaybeUpdate / commitTo change a word (as the reference assigns),
+        # plus the ReadIndex result byte.  SURVEY.md §8(d)'s 40n + 26 B
+        # counts every Next/resp read and every store; this round needs less.
+        with torch.no_grad():
+            nresp = bin(int(rm[0].item())).count("1")  # every group: same mask
+            step()
+            torch.cuda.synchronize(d.dev)
+            m1 = b.match.view(S, b.stride)[:, :G]
+            n1 = st.next.view(S, b.stride)[:, :G]
+            m0 = pristine["match"].view(S, b.stride)[:, :G]
+            n0 = pristine["next"].view(S, b.stride)[:, :G]
+            writes = 8 * (int((m1 != m0).sum()) + int((n1 != n0).sum()) +
+                          int((st.committed != pristine["committed"]).sum())) + G
+            prepare()
+        bpg = 2 + 24 + 8 * S + 16 * nresp + writes / G
         return step, bpg, G, "group-rounds", {"b": b, "st": st, "resp": resp,
                                                "prepare": prepare}
     if kind in ("elec", "elec_pvcq"):
@@ -493,15 +515,35 @@ def cpu_baseline(args, S=5):
     }
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary."""
+def load_pmc(workload):
+    """The committed rocprofv3 PMC record of a workload's dominant kernel
+    (profiles/pmc_traffic.json, scripts/summarize_workloads.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            data = json.load(f)
-        return data.get(workload, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(workload, {})
     except (OSError, ValueError):
+        return {}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary."""
+    return load_pmc(workload).get("hbm_bytes_per_launch")
+
+
+def valu_roofline(workload, kern_ms, units):
+    """VALU-issue roofline of a VALU-bound kernel: its VALU instructions per
+    launch (SQ_INSTS_VALU, committed PMC) over the live kernel time, against
+    VALU_PEAK_WIPS."""
+    v = load_pmc(workload).get("valu_insts_per_launch")
+    if not v:
         return None
+    ach = v / (kern_ms / 1000.0)
+    return {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_WIPS,
+            "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WIPS,
+            "valu_insts_per_launch": v, "valu_per_unit": v / units,
+            "lane_ops_per_unit": 64 * v / units,
+            "source": load_pmc(workload).get("profile")}
 
 
 def run_workload(name, args, d, steps, warmup):
@@ -526,7 +568,12 @@ def run_workload(name, args, d, steps, warmup):
     achieved = bpu * units / (kern_avg / 1000.0) / 1e9
     del keep
     torch.cuda.empty_cache()
-    return {
+    extra = {}
+    if kind in ("elec", "elec_pvcq", "progress"):
+        rv = valu_roofline(name, kern_avg, units)
+        if rv:
+            extra["roofline_valu"] = rv
+    return {**extra,
         "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
         "unit": f"{unit_name}/s", "value": value, "ms_per_step": ms_step,
         "kernel_ms": kern_avg, "bytes_per_unit": bpu,
