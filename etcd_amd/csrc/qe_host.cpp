@@ -4,6 +4,7 @@
 // the same order), copied to a grow-only device arena and evaluated by the
 // C ABI kernels; results are copied back.  Decisions never run on the CPU.
 #include <hip/hip_runtime_api.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -233,6 +234,43 @@ std::string MajorityConfig::String() const {
 
 std::vector<uint64_t> MajorityConfig::Slice() const { return {ids.begin(), ids.end()}; }
 
+// majority.go:45-101: sort by (index, id), the i-th gets bar i when its
+// index is above its predecessor's (else 0), print sorted by id.
+std::string MajorityConfig::Describe(const AckedIndexer &l) const {
+  if (ids.empty()) return "<empty majority quorum>";
+  struct Tup {
+    uint64_t id;
+    Index idx;
+    bool ok;
+    size_t bar;
+  };
+  const size_t n = ids.size();
+  std::vector<Tup> info;
+  info.reserve(n);
+  for (uint64_t id : ids) {
+    Index idx = 0;
+    const bool ok = l.AckedIndex(id, &idx);
+    info.push_back({id, ok ? idx : 0, ok, 0});
+  }
+  std::sort(info.begin(), info.end(), [](const Tup &a, const Tup &b) {
+    return a.idx == b.idx ? a.id < b.id : a.idx < b.idx;
+  });
+  for (size_t i = 1; i < n; i++)
+    if (info[i - 1].idx < info[i].idx) info[i].bar = i;
+  std::sort(info.begin(), info.end(), [](const Tup &a, const Tup &b) { return a.id < b.id; });
+  std::ostringstream os;
+  os << std::string(n, ' ') << "    idx\n";
+  for (const Tup &t : info) {
+    if (!t.ok) os << '?' << std::string(n, ' ');
+    else os << std::string(t.bar, 'x') << '>' << std::string(n - t.bar, ' ');
+    char buf[64];
+    snprintf(buf, sizeof(buf), " %5llu    (id=%llu)\n", static_cast<unsigned long long>(t.idx),
+             static_cast<unsigned long long>(t.id));
+    os << buf;
+  }
+  return os.str();
+}
+
 Index MajorityConfig::CommittedIndex(const AckedIndexer &l) const {
   return JointConfig(*this).CommittedIndex(l);
 }
@@ -250,6 +288,10 @@ std::set<uint64_t> JointConfig::IDs() const {
   std::set<uint64_t> s(c[0].ids);
   s.insert(c[1].ids.begin(), c[1].ids.end());
   return s;
+}
+
+std::string JointConfig::Describe(const AckedIndexer &l) const {
+  return MajorityConfig(IDs()).Describe(l);
 }
 
 Index JointConfig::CommittedIndex(const AckedIndexer &l) const {

@@ -151,12 +151,27 @@ int QE_CAT(dispatch_repl_, QE_S)(const RArgs &a, bool masked, bool joint, bool v
   return launch_repl<false, false, false>(a, st);
 }
 
-int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
-  auto kern = k_election<S, MT>;
+template <int OPT>
+static int launch_elec(const EArgs &a, hipStream_t st) {
+  auto kern = k_election<S, MT, OPT>;
   static int occ = occupancy(kern);
   const uint64_t waves = (a.G + 63) / 64;
   hipLaunchKernelGGL(kern, dim3(grid_for(waves, occ, 1)), dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
+}
+
+int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
+  const int opt = (a.flags & 3u) | (a.sresp ? 4 : 0);
+  switch (opt) {
+    case 0: return launch_elec<0>(a, st);
+    case 1: return launch_elec<1>(a, st);
+    case 2: return launch_elec<2>(a, st);
+    case 3: return launch_elec<3>(a, st);
+    case 4: return launch_elec<4>(a, st);
+    case 5: return launch_elec<5>(a, st);
+    case 6: return launch_elec<6>(a, st);
+    default: return launch_elec<7>(a, st);
+  }
 }
 
 }  // namespace qe

@@ -544,9 +544,12 @@ __device__ __forceinline__ void elec_campaign(bool pre, uint32_t mi, uint32_t mo
   }
 }
 
-template <int S, typename MT>
+// OPT: bit 0 PreVote, bit 1 CheckQuorum, bit 2 scripted responses
+// (compile-time, so the plain simulation carries none of their branches).
+template <int S, typename MT, int OPT>
 __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr bool pre = (OPT & 1) != 0, cq = (OPT & 2) != 0, scripted = (OPT & 4) != 0;
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * kBlock;
   uint64_t cnt[E_N];
@@ -556,8 +559,6 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
   const MT *lrnp = static_cast<const MT *>(a.learner);
   MT *vdp = static_cast<MT *>(a.voted), *grp = static_cast<MT *>(a.granted);
   const MT *srp = static_cast<const MT *>(a.sresp), *sgp = static_cast<const MT *>(a.sgrant);
-  const bool pre = (a.flags & QE_ELEC_PREVOTE) != 0;
-  const bool cq = (a.flags & QE_ELEC_CHECK_QUORUM) != 0;
 
   for (uint64_t g = tid; g < a.G; g += nthreads) {
     const uint64_t gid = a.goff + g;
@@ -587,15 +588,15 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
         const uint32_t hb = gkey + static_cast<uint32_t>(step) * 0x9E3779B1u;
         uint32_t resp = 0, val = 0;
         bool hup = false;
-        if (srp) {
+        if constexpr (scripted) {
           const uint64_t so = static_cast<uint64_t>(k) * a.sstride + g;
           resp = srp[so] & peers;
           val = sgp[so] & resp;
           hup = a.shup && a.shup[so] != 0;
         }
-        if (sta == QE_STATE_LEADER && cq) {
+        if (cq && sta == QE_STATE_LEADER) {
           // CheckQuorum round (raft.go:997-1018)
-          if (!srp) {
+          if constexpr (!scripted) {
 #pragma unroll
             for (int s = 0; s < S; s++) {
               const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u + 0x27D4EB2Fu);
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
           elec_campaign(pre, mi, mo, ml, self, t, sta, vd, gr, c32);
         } else {
           // d = fmix32(gkey + step*C1 + s*C2) per slot (oracle elec_draw)
-          if (!srp) {
+          if constexpr (!scripted) {
 #pragma unroll
             for (int s = 0; s < S; s++) {
               const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u);

@@ -73,6 +73,28 @@ class MajorityConfig(set):
     def Slice(self):
         return sorted(self)
 
+    def Describe(self, l):
+        """majority.go:45-101: the commit indexes of the voters as a bar
+        chart (text only, host side).  The voter of the i-th smallest index
+        gets a bar of i (0 when its index equals its predecessor's)."""
+        if len(self) == 0:
+            return "<empty majority quorum>"
+        n = len(self)
+        info = []
+        for vid in self:
+            idx, ok = l.AckedIndex(vid)
+            info.append([vid, int(idx), ok, 0])
+        info.sort(key=lambda t: (t[1], t[0]))
+        for i in range(1, n):
+            if info[i - 1][1] < info[i][1]:
+                info[i][3] = i
+        info.sort(key=lambda t: t[0])
+        out = [" " * n + "    idx\n"]
+        for vid, idx, ok, bar in info:
+            out.append("?" + " " * n if not ok else "x" * bar + ">" + " " * (n - bar))
+            out.append(f" {idx:5d}    (id={vid})\n")
+        return "".join(out)
+
     def CommittedIndex(self, l, device=None):
         """majority.go:126-172, evaluated on the GPU."""
         return CommittedIndexBatch([JointConfig(self, MajorityConfig())], [l], device)[0]
@@ -98,6 +120,10 @@ class JointConfig(tuple):
     def IDs(self):
         """joint.go:30-38."""
         return set(self[0]) | set(self[1])
+
+    def Describe(self, l):
+        """joint.go:40-44: Describe of the union of the halves."""
+        return MajorityConfig(self.IDs()).Describe(l)
 
     def CommittedIndex(self, l, device=None):
         """joint.go:49-56, evaluated on the GPU."""

@@ -65,6 +65,7 @@ class MajorityConfig {
   size_t size() const { return ids.size(); }
   std::string String() const;          // majority.go:27-43
   std::vector<uint64_t> Slice() const;  // majority.go:103-111
+  std::string Describe(const AckedIndexer &l) const;  // majority.go:45-101 (text)
   Index CommittedIndex(const AckedIndexer &l) const;  // majority.go:126-172
   quorum::VoteResult VoteResult(const Votes &votes) const;  // majority.go:178-210
   std::set<uint64_t> ids;
@@ -77,6 +78,7 @@ class JointConfig {
   JointConfig(MajorityConfig c0, MajorityConfig c1 = {}) : c{std::move(c0), std::move(c1)} {}
   std::string String() const;            // joint.go:21-26
   std::set<uint64_t> IDs() const;        // joint.go:30-38
+  std::string Describe(const AckedIndexer &l) const;  // joint.go:40-44 (text)
   Index CommittedIndex(const AckedIndexer &l) const;        // joint.go:49-56
   quorum::VoteResult VoteResult(const Votes &votes) const;  // joint.go:61-75
   MajorityConfig c[2];

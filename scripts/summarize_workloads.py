@@ -35,8 +35,8 @@ DOMINANT = {
     "config3_joint": ("void qe::k_cv_stream<10, 2,", 2),
     "config3_joint_rot": ("void qe::k_cv_stream<10, 2,", 2),
     "config4_repl": ("void qe::k_repl_stream<5,", 2),
-    "config5_elec": ("void qe::k_election<5,", 1),
-    "config5_prevote_cq": ("void qe::k_election<5,", 1),
+    "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 1),
+    "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
     "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false>", 1),
     "confchange": ("void qe::k_confchange<5>", 1),
 }

@@ -146,6 +146,13 @@ def datadriven_rows():
             }
             if cmd == "committed":
                 row["acked"] = sorted([k, v] for k, v in lookup.items())
+                # the harness prints c.Describe(l) and then the index
+                # (datadriven_test.go:172, :216): every line but the last
+                # is Describe's text (for the empty config the two share it)
+                if out[-1].startswith("<empty majority quorum>"):
+                    row["describe"] = "<empty majority quorum>"
+                else:
+                    row["describe"] = "\n".join(out[:-1]) + "\n"
             else:
                 row["votes"] = sorted([k, v == 2] for k, v in lookup.items())
             rows.append(row)
@@ -598,6 +605,14 @@ def main():
             f.write(f"{r['cmd']} {int(r['joint'])} {r['expect']} "
                     f"cfg={','.join(map(str, r['cfg']))} cfgj={','.join(map(str, r['cfgj']))} "
                     f"acked={acked} votes={votes} {r['source']}\n")
+    # Describe texts for the C++ test: cfg|cfgj|acked|text with newlines as \\n
+    with open(os.path.join(HERE, "describe_testdata.txt"), "w", encoding="utf-8") as f:
+        for r in rows:
+            if "describe" not in r:
+                continue
+            acked = ",".join(f"{k}:{v}" for k, v in r["acked"])
+            f.write(f"{','.join(map(str, r['cfg']))}|{','.join(map(str, r['cfgj']))}|{acked}|"
+                    + r["describe"].replace("\n", "\\n") + "\n")
     tables = {
         "TestCommit": {"source": "raft/raft_test.go:1127-1152", "rows": test_commit_table()},
         "TestLeaderElectionInOneRoundRPC": {"source": "raft/raft_paper_test.go:192-216", "rows": election_table()},

@@ -49,3 +49,16 @@ def test_cpp_confchange_datadriven_on_gpu():
     r = subprocess.run([exe, ROOT], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS: 58 confchange steps" in r.stdout
+
+
+def test_cpp_describe_matches_testdata():
+    """etcd_amd::quorum::{Majority,Joint}Config::Describe (host text
+    rendering, majority.go:45-101) against the 66 texts the reference's
+    datadriven harness printed (tests/golden/describe_testdata.txt)."""
+    if not os.path.exists(os.path.join(ROOT, "etcd_amd", "lib", "libetcd_quorum.so")):
+        pytest.skip("library not built")
+    _build()
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "describe_test")
+    r = subprocess.run([exe, ROOT], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS: 66 Describe cases" in r.stdout

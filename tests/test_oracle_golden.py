@@ -157,3 +157,23 @@ def test_election_scenarios_on_oracle(orc):
     for sc in scs:
         run_scenario(sc, oracle_runner(orc, sc))
     assert len(scs) == 13 + 4
+
+
+def test_describe_matches_testdata():
+    """MajorityConfig.Describe / JointConfig.Describe (majority.go:45-101,
+    joint.go:40-44) against the text the reference's datadriven harness
+    printed for every `committed` case (host-side rendering)."""
+    from etcd_amd.quorum import JointConfig, MajorityConfig, MapAckIndexer
+    from tests.golden_util import datadriven_cases
+    n = 0
+    for case in datadriven_cases():
+        if case["cmd"] != "committed":
+            continue
+        l = MapAckIndexer({int(k): int(v) for k, v in case["acked"]})
+        if case["joint"]:
+            got = JointConfig(case["cfg"], case["cfgj"]).Describe(l)
+        else:
+            got = MajorityConfig(case["cfg"]).Describe(l)
+        assert got == case["describe"], (case["source"], got, case["describe"])
+        n += 1
+    assert n == 66
