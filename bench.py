@@ -329,8 +329,8 @@ def setup(name, G, S, kind, d, stats):
         ps.next.copy_(ps.match + 1 + torch.randint(0, 4, (n,), device=d.dev, generator=gen))
         ps.flags.fill_(1 | 8)  # StateReplicate, RecentActive
         ps.icount.copy_(torch.randint(0, F + 1, (n,), device=d.dev, generator=gen).to(torch.uint8))
-        for k in range(F):
-            ps.ibuf.view(S, ps.stride, F)[:, :, k] = ps.match.view(S, ps.stride) + 1 + 8 * k
+        for k in range(F):  # entry-major rings: [S][F][stride]
+            ps.ibuf.view(S, F, ps.stride)[:, k, :] = ps.match.view(S, ps.stride) + 1 + 8 * k
         ps.last_index.copy_(base[:G] + 128)
         ps.term_start.copy_(base[:G])
         ps.first_index.copy_(base[:G] - 64)

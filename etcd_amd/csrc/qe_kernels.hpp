@@ -665,9 +665,9 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Progress state machine (qe_progress_step / qe_progress_send).  One group
-// per thread; per-peer state lives in slot-SoA rows, the Inflights ring in
-// [S][F][stride] rows (F = MaxInflightMsgs).
+// Progress state machine (qe_progress_step / qe_progress_send).  Per-peer
+// state lives in slot-SoA rows, the Inflights ring in [S][F][stride] rows
+// (F = MaxInflightMsgs, entry-major).
 // ---------------------------------------------------------------------------
 struct PArgs {
   uint64_t G, goff, stride;

@@ -1,15 +1,6 @@
 // qe_progress.hpp — qe_progress_step: the leader-side Progress state machine
 // (stepLeader, raft/raft.go:1099-1338) with the sends it triggers executed
-// where the reference executes them.  One group per lane, tiles of 64 groups.
-//
-// Every access goes through a per-tile buffer descriptor (wave-uniform base,
-// 32-bit lane offset, num_records clipping the ragged last tile), as in the
-// stream commit/vote kernel (qe_stream.hpp): a conditional access is an
-// unconditional load or store whose offset is pushed out of range when its
-// condition is false (no traffic, no branch, loads return 0).  Accesses that
-// are rare for a whole wave (PendingSnapshot of Snapshot-state peers, the
-// Inflights scan, the term-run table) sit behind real branches, so a wave
-// with no such peer skips them and waits for nothing.
+// where the reference executes them, and qe_progress_send.
 //
 // Decomposition (exact).  In the reference a message from
 // peer s can call bcastAppend, which sends to EVERY peer, so the order of
@@ -24,17 +15,32 @@
 //            message (with the bcast of its own accept, the oldPaused
 //            sendAppend, the `for maybeSendAppend(from, false)` loop and the
 //            MsgTimeoutNow check), then one sendAppend per later bcast.
-// The per-peer loads are software-pipelined: slot s+1's Progress loads are
-// issued before slot s's Inflights loads.
+// One lane per group, a wave per 64-group tile; the next slot's loads are
+// issued before this slot's work.  (A two-pass variant -- commit pass, then
+// one lane per peer -- was measured slower: DESIGN.md §6.)
+//
+// Sends have a closed form (send_burst): consecutive maybeSendAppend calls
+// on one peer append an arithmetic run of Inflights entries.  A peer's round
+// appends at most two runs (before and after its own message, whose handler
+// may reset the ring), so for F <= kRingChunk the ring is written once at
+// the end, entry row by entry row, from the two runs.
+//
+// Inflights rings are entry-major, [S][F][stride] (entry k of slot s of
+// group g at (s*F + k)*stride + g): entry k of a tile is one coalesced
+// 512-B access, where a peer-major row per lane touched 32-64 cache lines.
+//
+// Accesses go through per-tile buffer descriptors (wave-uniform base, 32-bit
+// lane offset, num_records clipping the ragged last tile), as in the stream
+// commit/vote kernel (qe_stream.hpp): a conditional access is an
+// unconditional load or store whose offset is pushed out of range when its
+// condition is false (no traffic, no branch, loads return 0).  Accesses that
+// are rare for a whole wave sit behind real (wave-uniform) branches.
 #pragma once
 #include "qe_stream.hpp"
 
 namespace qe {
 
-#ifndef QE_RING_CHUNK
-#define QE_RING_CHUNK 8
-#endif
-constexpr int kRingChunk = QE_RING_CHUNK;
+constexpr int kRingChunk = 8;  // F <= kRingChunk: closed-form ring writes
 
 __device__ __forceinline__ uint64_t bld64(rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -58,8 +64,9 @@ __device__ __forceinline__ void bst_mask(uint32_t v, rsrc_t r, uint32_t lane) {
 }
 
 // Byte accounting of the instrumented variant (ACCT): the bytes of every
-// access the kernel requests (offset in range), i.e. the algorithmic bytes
-// of the round at field granularity.
+// access the reference logic needs (field granularity, each once), i.e. the
+// algorithmic bytes of the round.  Re-reads (Match, m.Index in phase 2)
+// are not counted.
 template <bool ACCT>
 struct Acct {
   uint64_t b = 0;
@@ -67,84 +74,84 @@ struct Acct {
     if constexpr (ACCT) b += on ? bytes : 0u;
   }
 };
-
-struct PB {  // per-peer loads of one slot
-  uint64_t mt, ix, nx, hn, lt;  // mt, ix: re-read (L2-resident since round trips 1-2)
-  uint32_t fl, st, ct;
-  uint64_t rw[kRingChunk];  // the whole Inflights row when F <= kRingChunk
-};
-
-// Loads of slot row `row` (= s*stride + tile0): the Progress fields of a
-// touched peer, RejectHint/LogTerm of a reject, and (F <= kRingChunk) the
-// peer's whole Inflights row when FreeLE may run -- its position within the
-// row (start) is not needed to issue the loads, so they go out together.
 template <bool ACCT>
-__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, uint32_t n, uint32_t lane,
-                                        bool touched, bool rej, bool has_ix, bool ring, PB &b,
-                                        Acct<ACCT> &ac) {
-  constexpr int CH = kRingChunk;
-  const uint32_t o8 = touched ? lane * 8 : kOOB, o1 = touched ? lane : kOOB;
-  b.mt = bld64(mk_rsrc(a.match + row, n * 8), o8);
-  b.ix = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? lane * 8 : kOOB);
-  b.nx = bld64(mk_rsrc(a.next + row, n * 8), o8);
-  b.fl = bld8(mk_rsrc(a.flags + row, n), o1);
-  b.st = bld8(mk_rsrc(a.istart + row, n), o1);
-  b.ct = bld8(mk_rsrc(a.icount + row, n), o1);
-  b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
-  b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
-  ac.add(touched, 11);
-  ac.add(rej, 16);
-  const uint32_t F = a.F;
-  if (F <= CH) {
-    const rsrc_t r = mk_rsrc(a.ibuf + row * F, n * F * 8);
+__device__ __forceinline__ void acct_flush(const Acct<ACCT> &ac, uint64_t *acct) {
+  if constexpr (ACCT) {
+    uint64_t b = ac.b;
 #pragma unroll
-    for (int k = 0; k < CH; k++)
-      b.rw[k] = bld64(r, ring && static_cast<uint32_t>(k) < F ? (lane * F + k) * 8 : kOOB);
-  } else {
-#pragma unroll
-    for (int k = 0; k < CH; k++) b.rw[k] = 0;
+    for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
+    if ((threadIdx.x & 63) == 0 && acct)
+      atomicAdd(reinterpret_cast<unsigned long long *>(acct), static_cast<unsigned long long>(b));
   }
 }
 
-#ifndef QE_PSTEP_WAVES
-#define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
-#endif
+// Checksum of the round: a per-group part from the commit pass and a
+// per-group part from the peer pass (oracle/quorum_oracle.c orc_checksum_step).
+constexpr uint64_t kSentSalt = 0xD1B54A32D192ED03ull;
 
-// One peer's send side: raft.maybeSendAppend (raft/raft.go:432-492).
-struct PSend {
-  rsrc_t ring;
-  uint32_t ring0, F, me;
-  uint64_t fi, li, snap;
-  uint32_t count_msgs;  // messages sent to this peer this round (saturating)
-  uint64_t first_index; // m.Index of the first of them
-  bool snapped;
-  // Inflights entries this round appended: nadd of them, the first a0, each
-  // next one min(lastIndex, previous + me) (OptimisticUpdate moves Next to
-  // last+1 and the next MsgApp ends me-1 entries later)
-  uint64_t a0;
-  uint32_t nadd;
+// ---------------------------------------------------------------------------
+// Sends: raft.maybeSendAppend (raft/raft.go:432-492) in closed form.
+// ---------------------------------------------------------------------------
+// A run of Inflights entries appended by consecutive sends: n entries from
+// ring position p, the first MsgApp starting at Next = b; entry j is the
+// last index of MsgApp j: b + min(lastIndex - b, (j+1)*max_ents - 1)
+// (OptimisticUpdate moves Next past it, the next MsgApp starts there), or
+// lastIndex when max_ents = 0 (noLimit: one MsgApp carries every entry).
+struct PRun {
+  uint32_t p, n;
+  uint64_t b;
 };
 
-// `k` consecutive raft.maybeSendAppend(to, send_if_empty) calls on one peer
-// (raft/raft.go:432-492), k = kLoop: `for maybeSendAppend(to, false) {}`.
-// Consecutive calls have a closed form: a paused peer gets nothing; with no
-// entries (Next > lastIndex) every call sends an empty MsgApp if
-// sendIfEmpty, else none; Next < firstIndex: nothing unless sendIfEmpty,
-// then one MsgSnap to a recently active peer (BecomeSnapshot pauses it);
-// Probe: one MsgApp, ProbeSent pauses it; Replicate: one MsgApp per chunk
-// of max_ents entries (OptimisticUpdate + Inflights.Add) until the ring is
-// full or Next passes lastIndex, then empty MsgApps for the remaining calls
-// if sendIfEmpty.  Straight-line code per lane; the only loop is the
-// Inflights append loop (wave-uniform trip count).
+struct PSend {
+  uint64_t *rb;  // entry 0 of this slot's rings for the tile: entry k at rb[k*rs + lane]
+  uint64_t rs;   // stride
+  uint32_t lane;
+  bool row;      // F <= kRingChunk: the runs are written by ring_flush
+  uint32_t F, me;
+  uint64_t fi, li, snap;
+  uint32_t count_msgs;   // messages sent to this peer this round (saturating)
+  uint64_t first_index;  // m.Index of the first of them
+  bool snapped;
+};
+
+__device__ __forceinline__ uint64_t run_val(const PRun &r, uint32_t j, uint32_t me, uint64_t li) {
+  if (me == 0) return li;
+  const uint64_t step = static_cast<uint64_t>(j + 1) * me - 1;
+  const uint64_t d = li - r.b;
+  return r.b + (step < d ? step : d);
+}
+
+// Ring position of the next append (Inflights.Add, inflights.go:55-71); an
+// invalid Inflights.start (>= F) stays inside the ring.
+__device__ __forceinline__ uint32_t ring_pos(uint32_t start, uint32_t count, uint32_t F) {
+  uint32_t pos = start + count;
+  if (pos >= F) pos -= F;
+  if (pos >= F) pos = 0;
+  return pos;
+}
+
 constexpr uint32_t kLoop = 0xFFFFFFFFu;
 
+
+// `k` consecutive raft.maybeSendAppend(to, sei) calls on one peer, or with
+// k = kLoop one call with `sei` followed by `for maybeSendAppend(to, false)
+// {}`.  A paused peer gets nothing; with no entries (Next > lastIndex) every
+// call with sendIfEmpty sends an empty MsgApp; Next < firstIndex: nothing
+// unless sendIfEmpty (raft.go:442-444 come first), then one MsgSnap to a
+// recently active peer (BecomeSnapshot pauses it); Probe: one MsgApp,
+// ProbeSent pauses it; Replicate: one MsgApp per max_ents entries
+// (OptimisticUpdate + Inflights.Add) until the ring is full or Next passes
+// lastIndex, then empty MsgApps for the remaining calls with sendIfEmpty.
+// The appended entries extend `run`.
 template <bool ACCT>
-__device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x, Acct<ACCT> &ac) {
+__device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x, PRun &run,
+                                           Acct<ACCT> &ac) {
+  const bool loop = k == kLoop;
   const bool go = k > 0 && !pr_paused(p, x.F);
   const bool empty = p.next > x.li;
   const bool comp = !empty && p.next < x.fi;  // entries() fails with ErrCompacted
   uint64_t idx0 = p.next - 1;
-  uint32_t nmsg = (go && empty && sei) ? k : 0u;  // kLoop only comes with sei == false
+  uint32_t nmsg = (go && empty && sei) ? (loop ? 1u : k) : 0u;
   if (go && comp && sei && p.recent_active) {  // the sendIfEmpty check comes first (:442-444)
     pr_reset(p, QE_PR_SNAPSHOT);                // BecomeSnapshot(snapshot index) (:468)
     p.pending = x.snap;
@@ -159,29 +166,51 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
   }
   const bool repl = ents && p.state == QE_PR_REPLICATE;
   const uint32_t room = x.F > p.count ? x.F - p.count : 0u;
-  const uint32_t lim = repl ? (room < k ? room : k) : 0u;
+  const uint32_t lim = repl ? ((loop || room < k) ? room : k) : 0u;
+  const uint64_t d = x.li - p.next;  // valid when repl
   uint32_t added = 0;
-  while (__builtin_amdgcn_ballot_w64(added < lim && p.next <= x.li)) {
-    const bool on = added < lim && p.next <= x.li;
-    uint64_t last = x.li;
+  if (x.row) {  // lim <= F <= kRingChunk: count the appends directly
+    uint32_t fit = 1;  // MsgApps whose first entry is <= lastIndex
     if (x.me) {
-      const uint64_t l = p.next + (x.me - 1);
-      if (l >= p.next && l < last) last = l;
+#pragma unroll
+      for (int j = 1; j < kRingChunk; j++)
+        fit += (static_cast<uint64_t>(j) * x.me <= d) ? 1u : 0u;
     }
-    uint32_t pos = p.start + p.count;
-    if (pos >= x.F) pos -= x.F;
-    if (pos >= x.F) pos = 0;  // invalid Inflights.start: stay inside the row
-    bst64(last, x.ring, on ? (x.ring0 + pos) * 8 : kOOB);
-    ac.add(on, 8);
-    x.a0 = (on && x.nadd == 0) ? last : x.a0;
-    x.nadd += on ? 1u : 0u;
-    p.next = on ? last + 1 : p.next;
-    p.count += on ? 1u : 0u;
-    added += on ? 1u : 0u;
+    added = x.me ? (lim < fit ? lim : fit) : (lim ? 1u : 0u);
+    if (added) {
+      if (run.n == 0) {
+        run.p = ring_pos(p.start, p.count, x.F);
+        run.b = p.next;
+      }
+      run.n += added;
+      const PRun here{0, 0, p.next};
+      p.next = run_val(here, added - 1, x.me, x.li) + 1;
+      p.count += added;
+      ac.add(true, 8 * added);
+    }
+  } else {  // F > kRingChunk: append entry by entry, straight to memory
+    while (__builtin_amdgcn_ballot_w64(added < lim && p.next <= x.li)) {
+      const bool on = added < lim && p.next <= x.li;
+      const PRun here{0, 0, p.next};
+      const uint64_t last = run_val(here, 0, x.me, x.li);
+      const uint32_t pos = ring_pos(p.start, p.count, x.F);
+      if (on) {
+        x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] = last;
+        if (run.n == 0) {
+          run.p = pos;
+          run.b = p.next;
+        }
+        run.n += 1;
+        p.next = last + 1;
+        p.count += 1;
+        added += 1;
+      }
+      ac.add(on, 8);
+    }
   }
   if (repl) {
     nmsg = added;
-    if (sei && added < k && p.count < x.F && p.next > x.li) nmsg += k - added;  // empties
+    if (!loop && sei && added < k && p.count < x.F && p.next > x.li) nmsg += k - added;  // empties
   }
   if (nmsg) {
     if (x.count_msgs == 0) x.first_index = idx0;
@@ -190,23 +219,35 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
   }
 }
 
+// Row mode: entry row k is stored once, for the lanes whose runs cover
+// position k (the later run wins: it was appended after the earlier one).
+__device__ __forceinline__ void ring_flush(const PSend &x, const PRun &r1, const PRun &r2,
+                                           uint32_t n) {
+  if (!__builtin_amdgcn_ballot_w64((r1.n | r2.n) != 0)) return;
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) {
+    if (static_cast<uint32_t>(k) >= x.F) break;
+    const uint32_t j1 = static_cast<uint32_t>(k) >= r1.p ? k - r1.p : k + x.F - r1.p;
+    const uint32_t j2 = static_cast<uint32_t>(k) >= r2.p ? k - r2.p : k + x.F - r2.p;
+    const bool on1 = j1 < r1.n, on2 = j2 < r2.n;
+    if (__builtin_amdgcn_ballot_w64(on1 || on2)) {
+      const uint64_t v = on2 ? run_val(r2, j2, x.me, x.li) : run_val(r1, j1, x.me, x.li);
+      bst64(v, mk_rsrc(x.rb + k * x.rs, n * 8), (on1 || on2) ? x.lane * 8 : kOOB);
+    }
+  }
+}
+
 // Inflights.FreeLE(to) (raft/tracker/inflights.go:87-113) given fr_old, the
 // number of this round's c_old initial entries (from start) that are <= to,
-// stopping at the first that is not; the entries this round appended follow
-// them (closed form, PSend).  Exactly min(count, freed + 1) entries are
+// stopping at the first that is not; the entries this round appended before
+// it (run r1) follow them.  Exactly min(count, freed + 1) entries are
 // examined, as the reference's loop does.
 template <bool ACCT>
 __device__ __forceinline__ void free_le(PR &p, uint64_t to, uint32_t c_old, uint32_t fr_old,
-                                        const PSend &x, Acct<ACCT> &ac) {
+                                        const PRun &r1, const PSend &x, Acct<ACCT> &ac) {
   uint32_t fr = fr_old;
   if (fr == c_old) {
-    uint64_t v = x.a0;
-    for (uint32_t j = 0; j < x.nadd && v <= to; j++) {
-      fr++;
-      const uint64_t w = v + x.me;
-      v = (x.me == 0 || w < v || w > x.li) ? x.li : w;
-      if (x.me == 0) break;  // noLimit: one MsgApp carries every entry
-    }
+    for (uint32_t j = 0; j < r1.n && run_val(r1, j, x.me, x.li) <= to; j++) fr++;
   }
   ac.add(p.count > 0, 8 * (fr + 1 < p.count ? fr + 1 : p.count));
   if (fr > 0) {
@@ -240,8 +281,7 @@ __device__ __forceinline__ uint64_t row_at(const uint64_t (&rw)[kRingChunk], uin
   return v;
 }
 // The same from memory (F > kRingChunk): e[] holds the first min(CH, c_old)
-// entries from start, loaded after the peer's Progress arrived.
-template <bool ACCT>
+// entries from start.
 __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk], uint32_t npre,
                                                   uint32_t start, uint32_t c_old, uint64_t to,
                                                   const PSend &x) {
@@ -255,13 +295,58 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
   if (fr == npre && fr < c_old) {
     uint32_t pos = start + fr;
     while (pos >= x.F) pos -= x.F;
-    while (fr < c_old && bld64(x.ring, (x.ring0 + pos) * 8) <= to) {
+    while (fr < c_old && x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] <= to) {
       fr++;
       if (++pos >= x.F) pos -= x.F;
     }
   }
   return fr;
 }
+
+// ---------------------------------------------------------------------------
+// k_progress_step: one lane per group, a wave per 64-group tile.  Phase 1
+// (MaybeUpdate + maybeCommit over the slots in message order -> the bcast
+// set) runs in registers; phase 2 walks the slots, each peer's whole event
+// sequence at once, with the next slot's loads issued before this slot's
+// work.
+// ---------------------------------------------------------------------------
+struct PB {  // per-peer loads of one slot
+  uint64_t mt, ix, nx, hn, lt;  // mt, ix: re-read (L2-resident since phase 1)
+  uint32_t fl, st, ct;
+  uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring
+};
+
+// Loads of slot row `row` (= s*stride + tile0): the Progress fields of a
+// touched peer, RejectHint/LogTerm of a reject, and (F <= kRingChunk) the
+// peer's ring entries when FreeLE may run -- one coalesced entry row each
+// (rb: entry 0 of this slot's rings for the tile).
+template <bool ACCT>
+__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *rb,
+                                        uint32_t n, uint32_t lane, bool touched, bool rej,
+                                        bool has_ix, bool ring, PB &b, Acct<ACCT> &ac) {
+  const uint32_t o8 = touched ? lane * 8 : kOOB, o1 = touched ? lane : kOOB;
+  b.mt = bld64(mk_rsrc(a.match + row, n * 8), o8);
+  b.ix = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? lane * 8 : kOOB);
+  b.nx = bld64(mk_rsrc(a.next + row, n * 8), o8);
+  b.fl = bld8(mk_rsrc(a.flags + row, n), o1);
+  b.st = bld8(mk_rsrc(a.istart + row, n), o1);
+  b.ct = bld8(mk_rsrc(a.icount + row, n), o1);
+  b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
+  b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
+  ac.add(touched, 11);
+  ac.add(rej, 16);
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) b.rw[k] = 0;
+  if (a.F <= static_cast<uint32_t>(kRingChunk) && ring) {  // lanes < n only
+#pragma unroll
+    for (int k = 0; k < kRingChunk; k++)
+      if (static_cast<uint32_t>(k) < a.F) b.rw[k] = rb[k * a.stride + lane];
+  }
+}
+
+#ifndef QE_PSTEP_WAVES
+#define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
+#endif
 
 template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
@@ -305,10 +390,9 @@ k_progress_step(PArgs a) {
     const rsrc_t r_commit = mk_rsrc(a.committed + g0, n * 8);
     const uint64_t c0 = bld64(r_commit, o8);
     const uint64_t snap_ld = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), o8) : 0;
-    const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), lane);
     ac.add(live, (MASKED ? sizeof(MT) : 0) + (JOINT ? sizeof(MT) : 0) +
                      (a.tracked ? sizeof(MT) : 0) + (a.self_slot ? 1 : 0) +
-                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0) + 1);
+                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0));
     uint64_t m0[S];
     uint32_t ty[S];
 #pragma unroll
@@ -320,34 +404,22 @@ k_progress_step(PArgs a) {
       ac.add(live, 8);
       ac.add(live && tr, 1);
     }
-    const uint32_t nr = rc < a.R ? rc : a.R;
     // message kinds, 4 bits per slot, for the rolled phase-2 loop (kinds
     // above QE_MSG_UNREACHABLE are "no message")
     uint64_t tys = 0;
 #pragma unroll
     for (int s = 0; s < S; s++)
       tys |= static_cast<uint64_t>(ty[s] <= QE_MSG_UNREACHABLE ? ty[s] : 15u) << (4 * s);
-    // ---- round trip 2: m.Index of every MsgAppResp, the term-run table of
-    // a group with a reject, and slot 0's peer loads ----
+    // ---- round trip 2: m.Index of every MsgAppResp and slot 0's peer loads ----
     uint64_t ix[S];
-    uint32_t rej_any = 0;
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const bool has_ix = ty[s] == QE_MSG_APP_RESP || ty[s] == QE_MSG_APP_RESP_REJECT;
       ix[s] = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? o8 : kOOB);
       ac.add(has_ix, 8);
-      rej_any |= ty[s] == QE_MSG_APP_RESP_REJECT ? 1u : 0u;
     }
-    uint64_t rf[RM], rt[RM];
-#pragma unroll
-    for (int r = 0; r < RM; r++) {
-      const uint32_t off = (rej_any && static_cast<uint32_t>(r) < nr) ? o8 : kOOB;
-      const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
-      rf[r] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
-      rt[r] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
-    }
-    bool runs_counted = false;  // ACCT: the table counts once, when first used
+    bool runs_counted = false;  // ACCT: the run table counts once, when first used
     auto ty_of = [&](uint32_t s) -> uint32_t { return static_cast<uint32_t>(tys >> (4 * s)) & 15u; };
     auto has_ix_of = [&](uint32_t s) -> bool {
       const uint32_t t = ty_of(s);
@@ -358,12 +430,12 @@ k_progress_step(PArgs a) {
       const uint32_t t0 = ty_of(0);
       const bool msg = t0 >= QE_MSG_APP_RESP && t0 <= QE_MSG_UNREACHABLE;
       const bool ld = (trk & 1u) && (msg || self != 0u);
-      pb_load<ACCT>(a, g0, n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT, has_ix_of(0),
+      pb_load<ACCT>(a, g0, a.ibuf + g0, n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT, has_ix_of(0),
                     ld && (t0 == QE_MSG_APP_RESP || t0 == QE_MSG_HEARTBEAT_RESP), cur, ac);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
-    uint32_t bset = 0, upd = 0, nbc = 0;
+    uint32_t bset = 0, upd = 0;
     {
       uint64_t vals[S];
 #pragma unroll
@@ -377,7 +449,6 @@ k_progress_step(PArgs a) {
           if (mci > c && mci >= ts && mci <= li) {
             c = mci;
             bset |= 1u << s;
-            nbc++;
           }
         }
       }
@@ -389,6 +460,9 @@ k_progress_step(PArgs a) {
     x.fi = fi;
     x.li = li;
     x.snap = a.snap_index ? snap_ld : fi - 1;
+    x.rs = a.stride;
+    x.lane = lane;
+    x.row = row_ring;
     uint32_t sent = 0, snapm = 0, tnow = 0;
     auto touched_of = [&](uint32_t s) -> bool {
       const bool tr = (trk >> s) & 1u;
@@ -410,9 +484,9 @@ k_progress_step(PArgs a) {
       const bool touched = touched_of(s);
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
-        pb_load<ACCT>(a, row + a.stride, n, lane, touched_of(s + 1),
-                      ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), ring_of(s + 1), nxt,
-                      ac);
+        pb_load<ACCT>(a, row + a.stride, a.ibuf + static_cast<uint64_t>(s + 1) * F * a.stride + g0,
+                      n, lane, touched_of(s + 1), ty_of(s + 1) == QE_MSG_APP_RESP_REJECT,
+                      has_ix_of(s + 1), ring_of(s + 1), nxt, ac);
       PR p;
       p.match = cur.mt;
       p.next = cur.nx;
@@ -421,7 +495,6 @@ k_progress_step(PArgs a) {
       p.recent_active = (cur.fl & QE_PF_RECENT_ACTIVE) != 0;
       p.start = cur.st;
       p.count = cur.ct;
-      p.pending = 0;
       p.reset = 0;
       // PendingSnapshot is read only in StateSnapshot (every other state only
       // ever overwrites it)
@@ -432,15 +505,11 @@ k_progress_step(PArgs a) {
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
-      x.ring = mk_rsrc(a.ibuf + row * F, n * F * 8);
-      x.ring0 = lane * F;
+      x.rb = a.ibuf + static_cast<uint64_t>(s) * F * a.stride + g0;
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
-      // F > kRingChunk: cur.rw (unused by that path) takes the first
-      // entries from start, loaded after the Progress arrived
-      uint64_t e[CH];
-#pragma unroll
-      for (int k = 0; k < CH; k++) e[k] = 0;
+      // F > kRingChunk: cur.rw (zero on that path) takes the first entries
+      // from start, loaded after the Progress arrived
       uint32_t npre = 0;
       if (!row_ring) {
         const bool scan = ring_of(s) && p.state == QE_PR_REPLICATE;
@@ -450,16 +519,15 @@ k_progress_step(PArgs a) {
           for (int k = 0; k < CH; k++) {
             uint32_t pos = p.start + k;
             if (pos >= F) pos -= F;
-            if (pos >= F) pos = 0;  // invalid Inflights.start: stay inside the row
-            e[k] = bld64(x.ring, static_cast<uint32_t>(k) < npre ? (x.ring0 + pos) * 8 : kOOB);
+            if (pos >= F) pos = 0;  // invalid Inflights.start: stay inside the ring
+            if (static_cast<uint32_t>(k) < npre) cur.rw[k] = x.rb[static_cast<uint64_t>(pos) * x.rs + lane];
           }
         }
       }
       x.count_msgs = 0;
       x.first_index = 0;
       x.snapped = false;
-      x.nadd = 0;
-      x.a0 = 0;
+      PRun r1{0, 0, 0}, r2{0, 0, 0};
       // The peer's events in order: k1 bcast sends (from accepts of earlier
       // slots), its own message, that message's sendAppend (k2), the
       // `for maybeSendAppend(from, false) {}` loop (lp), k3 bcast sends (from
@@ -469,15 +537,25 @@ k_progress_step(PArgs a) {
       const uint32_t k1 = bcast_target ? popc(bset & below) : 0u;
       const uint32_t k3 = bcast_target ? popc(bset & ~below & ~(1u << s)) : 0u;
       uint32_t k2 = 0;
-      bool lp = false, updated = false;
-      send_burst<ACCT>(p, true, k1, x, ac);
+      bool lp = false;
+      if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
           uint64_t probe = cur.hn;
-          if (cur.lt > 0) {
+          if (cur.lt > 0) {  // the group's term runs, read here only (rejections are rare)
+            const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), lane);
+            const uint32_t nr = rc < a.R ? rc : a.R;
+            uint64_t rf[RM], rt[RM];
+#pragma unroll
+            for (int r = 0; r < RM; r++) {
+              const uint32_t off = static_cast<uint32_t>(r) < nr ? o8 : kOOB;
+              const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
+              rf[r] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
+              rt[r] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
+            }
             probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, cur.lt);
-            ac.add(!runs_counted, 16 * nr);
+            ac.add(!runs_counted, 1 + 16 * nr);
             runs_counted = true;
           }
           bool decr;  // MaybeDecrTo(m.Index, probe), progress.go:170-193
@@ -501,7 +579,6 @@ k_progress_step(PArgs a) {
           const bool old_paused = pr_paused(p, F);
           if (up) {  // MaybeUpdate (progress.go:144-153)
             p.match = idx;
-            updated = true;
             p.probe_sent = 0;
           }
           if (p.next < idx + 1) p.next = idx + 1;
@@ -513,8 +590,8 @@ k_progress_step(PArgs a) {
               pr_become_replicate(p);
             } else if (p.state == QE_PR_REPLICATE) {
               const uint32_t fo = row_ring ? row_prefix_le(cur.rw, F, p.start, c_old, idx)
-                                           : mem_prefix_le<ACCT>(e, npre, p.start, c_old, idx, x);
-              free_le<ACCT>(p, idx, c_old, fo, x, ac);
+                                           : mem_prefix_le(cur.rw, npre, p.start, c_old, idx, x);
+              free_le<ACCT>(p, idx, c_old, fo, r1, x, ac);
             }
             // bcastAppend of this accept (skips the leader) / sendAppend if
             // it was paused; then the send loop
@@ -528,12 +605,12 @@ k_progress_step(PArgs a) {
           if (p.state == QE_PR_REPLICATE && p.count == F) {
             // FreeFirstOne = FreeLE(buffer[start])
             uint64_t first;
-            if (c_old == 0) first = x.a0;
+            if (c_old == 0) first = run_val(r1, 0, x.me, li);
             else if (row_ring) first = row_at(cur.rw, p.start < F ? p.start : 0u);
-            else first = e[0];
+            else first = cur.rw[0];
             const uint32_t fo = row_ring ? row_prefix_le(cur.rw, F, p.start, c_old, first)
-                                         : mem_prefix_le<ACCT>(e, npre, p.start, c_old, first, x);
-            free_le<ACCT>(p, first, c_old, fo, x, ac);
+                                         : mem_prefix_le(cur.rw, npre, p.start, c_old, first, x);
+            free_le<ACCT>(p, first, c_old, fo, r1, x, ac);
           }
           k2 = p.match < li ? 1u : 0u;
         } else if (tt == QE_MSG_SNAP_STATUS || tt == QE_MSG_SNAP_STATUS_REJECT) {  // :1310-1331
@@ -546,14 +623,18 @@ k_progress_step(PArgs a) {
           if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
         }
       }
-      send_burst<ACCT>(p, true, k2, x, ac);
-      send_burst<ACCT>(p, false, lp ? kLoop : 0u, x, ac);
-      send_burst<ACCT>(p, true, k3, x, ac);
+      // After an accept: its sendAppend (sendIfEmpty), then the loop; the
+      // later bcasts follow the loop.  Otherwise the message's sendAppend
+      // and the later bcasts are consecutive sendIfEmpty sends: one burst.
+      const uint32_t km = lp ? kLoop : k2 + k3;
+      if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
+      if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
+      if (row_ring) ring_flush(x, r1, r2, n);
       // ---- stores: the peer's new Progress (unchanged words and bytes skipped) ----
       const uint32_t w8 = touched ? o8 : kOOB, w1 = touched ? lane : kOOB;
       const uint32_t fl = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
                           (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u);
-      const bool wm = updated, wn = touched && p.next != cur.nx;
+      const bool wm = touched && up, wn = touched && p.next != cur.nx;
       const bool wp = touched && (p.pending != pd0 || p.reset);
       const bool wf = touched && fl != cur.fl, ws = touched && p.start != cur.st;
       const bool wc = touched && p.count != cur.ct;
@@ -577,8 +658,8 @@ k_progress_step(PArgs a) {
       snapm |= x.snapped ? (1u << s) : 0u;
       if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
     }
+    const uint32_t bc = popc(bset);
     bst64(c, r_commit, c != c0 ? o8 : kOOB);
-    const uint32_t bc = nbc;
     bst_mask<MT>(sent, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
     bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
     bst_mask<MT>(tnow, opt_rsrc(static_cast<const MT *>(a.tnow), g0, n), lane);
@@ -589,12 +670,12 @@ k_progress_step(PArgs a) {
     ac.add(live && a.tnow, sizeof(MT));
     ac.add(live && a.bcast, 1);
     if (live) {
+      const uint64_t gh = (a.goff + g0 + lane) * kPhi;
       cnt[P_GROUPS] += 1;
       cnt[P_SUM] += c;
       cnt[P_ADV] += (c != c0);
-      const uint64_t tag =
-          (static_cast<uint64_t>(sent) << 40) | (static_cast<uint64_t>(bc) << 62);
-      cnt[P_CSUM] += mix64(((a.goff + g0 + lane) * kPhi) ^ c ^ tag);
+      cnt[P_CSUM] += mix64(gh ^ c ^ (static_cast<uint64_t>(bc) << 62)) +
+                     mix64(gh ^ (static_cast<uint64_t>(sent) << 40) ^ kSentSalt);
     }
   }
   if (a.stats) {
@@ -602,13 +683,7 @@ k_progress_step(PArgs a) {
                           QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
     block_stats_add<P_N, kBlock>(cnt, idx, a.stats);
   }
-  if constexpr (ACCT) {
-    uint64_t b = ac.b;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
-    if (lane == 0 && a.acct) atomicAdd(reinterpret_cast<unsigned long long *>(a.acct),
-                                       static_cast<unsigned long long>(b));
-  }
+  acct_flush<ACCT>(ac, a.acct);
 }
 
 // qe_progress_send: raft.sendAppend / maybeSendAppend(to, send_if_empty)
@@ -656,13 +731,17 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
       p.reset = 0;
       const uint64_t nx0 = p.next;
       const uint32_t st0 = p.start, ct0 = p.count;
-      x.ring = mk_rsrc(a.ibuf + row * a.F, n * a.F * 8);
-      x.ring0 = lane * a.F;
+      x.rb = a.ibuf + static_cast<uint64_t>(s) * a.F * a.stride + g0;
+      x.rs = a.stride;
+      x.lane = lane;
+      x.row = a.F <= static_cast<uint32_t>(kRingChunk);
       x.count_msgs = 0;
+      x.first_index = 0;
       x.snapped = false;
-      x.nadd = 0;
-      x.a0 = 0;
-      send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, x, ac);
+      PRun run{0, 0, 0};
+      const PRun none{0, 0, 0};
+      send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, x, run, ac);
+      if (x.row) ring_flush(x, none, run, n);
       const uint32_t f2 = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
                           (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u);
       bst64(p.next, mk_rsrc(a.next + row, n * 8), on && p.next != nx0 ? o8 : kOOB);

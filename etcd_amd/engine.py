@@ -262,7 +262,7 @@ def tune(key, value):
 
 class ProgressState:
     """Device-resident leader-side Progress of G groups (qe_progress):
-    match/next/pending [S][stride], flags, Inflights rings [S][stride][F],
+    match/next/pending [S][stride], flags, Inflights rings [S][F][stride] (entry-major),
     committed, and the leader-log model (term runs).  `extras` allocates the
     optional per-group arrays of ABI 2: "tracked" (slot mask), "self_slot",
     "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""

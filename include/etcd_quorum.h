@@ -316,8 +316,9 @@ typedef struct qe_progress {
   uint8_t *flags;               /* [S][stride] QE_PF_* bits                  */
   uint8_t *infl_start;          /* [S][stride] Inflights.start               */
   uint8_t *infl_count;          /* [S][stride] Inflights.count               */
-  uint64_t *infl_buf;           /* [S][stride][F] Inflights.buffer (a peer's
-                                   ring is one contiguous row of F entries)  */
+  uint64_t *infl_buf;           /* [S][F][stride] Inflights.buffer, entry-
+                                   major: entry k of slot s of group g at
+                                   (s*F + k)*stride + g                      */
   uint64_t *committed;          /* [G] raftLog.committed (rw)                */
   const uint64_t *term_start;   /* [G]                                       */
   const uint64_t *first_index;  /* [G] raftLog.firstIndex()                  */

@@ -962,8 +962,8 @@ uint64_t orc_find_conflict_by_term(uint32_t nruns, const uint64_t *first, const 
 
 /* The leader-side state of G groups (mirrors qe_progress of
  * include/etcd_quorum.h, ABI 2) and one round of peer messages (mirrors
- * qe_peer_msgs).  Slot s of group g lives at [s*stride + g]; the Inflights
- * ring of that peer is ibuf[(s*stride + g)*F .. +F). */
+ * qe_peer_msgs).  Slot s of group g lives at [s*stride + g]; entry k of
+ * that peer's Inflights ring at ibuf[(s*F + k)*stride + g] (entry-major). */
 typedef struct orc_prog {
   uint64_t G, goff;
   uint32_t S, F;
@@ -1010,8 +1010,8 @@ static void pr_load2(orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   p->start = a->istart[off];
   p->count = a->icount[off];
   p->size = a->F;
-  p->buf = a->ibuf + off * a->F;
-  p->bstride = 1;
+  p->buf = a->ibuf + (uint64_t)s * a->F * a->stride + g; /* entry k at buf[k*stride] */
+  p->bstride = a->stride;
 }
 static void pr_store2(const orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   uint64_t off = s * a->stride + g;
@@ -1078,9 +1078,11 @@ static int send_append(orc_gctx *c, orc_pr *p, uint32_t s, int send_if_empty) {
   return 1;
 }
 
+/* Two per-group parts: (commit, bcast count) and the sent mask (the GPU
+ * adds them in its commit pass and its peer pass). */
 uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast) {
-  uint64_t tag = ((uint64_t)send << 40) | ((uint64_t)bcast << 62);
-  return orc_mix64((gid * PHI) ^ committed ^ tag);
+  return orc_mix64((gid * PHI) ^ committed ^ ((uint64_t)bcast << 62)) +
+         orc_mix64((gid * PHI) ^ ((uint64_t)send << 40) ^ 0xD1B54A32D192ED03ull);
 }
 
 /* One round of leader-side message handling per group, messages taken in

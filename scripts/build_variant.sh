@@ -2,7 +2,7 @@
 # Build a variant of libetcd_quorum.so with extra compile flags, reusing the
 # main build's objects that the flags do not touch (copied with their
 # timestamps, so make only rebuilds what depends on the changed sources).
-#   scripts/build_variant.sh NAME "-DQE_PSTEP_WAVES=2" [prog|all]
+#   scripts/build_variant.sh NAME "-DQE_PSTEP_TPB=4" [prog|all]
 # -> etcd_amd/lib/variants/libetcd_quorum_NAME.so
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)

@@ -55,8 +55,8 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
     pb.icount[:] = rng.integers(0, F + 1, n).astype(np.uint8)
     pb.istart[:] = rng.integers(0, F, n).astype(np.uint8)
     base = pb.match.copy()
-    for k in range(F):
-        pb.ibuf[(np.arange(S)[:, None] * G + np.arange(G)[None, :]) * F + k] = \
+    for k in range(F):  # entry-major rings: entry k of slot s at (s*F + k)*stride + g
+        pb.ibuf[(np.arange(S)[:, None] * F + k) * pb.stride + np.arange(G)[None, :]] = \
             (base.reshape(S, G) + 1 + 2 * ((k - pb.istart.reshape(S, G).astype(int)) % F)).astype(np.uint64)
     md = orc.mask_dtype(S)
     if "inc" in masks:
