@@ -311,7 +311,7 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
 // work.
 // ---------------------------------------------------------------------------
 struct PB {  // per-peer loads of one slot
-  uint64_t mt, ix, nx, hn, lt;  // mt, ix: re-read (L2-resident since phase 1)
+  uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t fl, st, ct;
   uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring
 };
@@ -320,19 +320,30 @@ struct PB {  // per-peer loads of one slot
 // touched peer, RejectHint/LogTerm of a reject, and (F <= kRingChunk) the
 // peer's ring entries when FreeLE may run -- one coalesced entry row each
 // (rb: entry 0 of this slot's rings for the tile).
+// A wave-level branch skips each group of loads no lane needs (an issued
+// vector memory instruction costs the CU's memory path about the same
+// whether or not its lanes are masked off).
 template <bool ACCT>
 __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *rb,
-                                        uint32_t n, uint32_t lane, bool touched, bool rej,
-                                        bool has_ix, bool ring, PB &b, Acct<ACCT> &ac) {
-  const uint32_t o8 = touched ? lane * 8 : kOOB, o1 = touched ? lane : kOOB;
-  b.mt = bld64(mk_rsrc(a.match + row, n * 8), o8);
-  b.ix = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? lane * 8 : kOOB);
-  b.nx = bld64(mk_rsrc(a.next + row, n * 8), o8);
-  b.fl = bld8(mk_rsrc(a.flags + row, n), o1);
-  b.st = bld8(mk_rsrc(a.istart + row, n), o1);
-  b.ct = bld8(mk_rsrc(a.icount + row, n), o1);
-  b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
-  b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
+                                        const uint64_t *l_mix, uint32_t n, uint32_t lane,
+                                        bool touched, bool rej, bool has_ix, bool ring, PB &b,
+                                        Acct<ACCT> &ac) {
+  b.mt = l_mix[lane];
+  b.ix = has_ix ? l_mix[64 + lane] : 0;
+  b.nx = 0;
+  b.fl = b.st = b.ct = 0;
+  if (__builtin_amdgcn_ballot_w64(touched)) {
+    const uint32_t o8 = touched ? lane * 8 : kOOB, o1 = touched ? lane : kOOB;
+    b.nx = bld64(mk_rsrc(a.next + row, n * 8), o8);
+    b.fl = bld8(mk_rsrc(a.flags + row, n), o1);
+    b.st = bld8(mk_rsrc(a.istart + row, n), o1);
+    b.ct = bld8(mk_rsrc(a.icount + row, n), o1);
+  }
+  b.hn = b.lt = 0;
+  if (__builtin_amdgcn_ballot_w64(rej)) {
+    b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
+    b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
+  }
   ac.add(touched, 11);
   ac.add(rej, 16);
 #pragma unroll
@@ -365,10 +376,17 @@ k_progress_step(PArgs a) {
   const uint32_t F = a.F;
   const bool row_ring = F <= CH;  // wave-uniform
   const uint32_t o8 = lane * 8;
+  // per wave: Match and m.Index of every slot (phase 1's rows, read again in
+  // phase 2) and the group's term runs once a slot needs them
+  __shared__ uint64_t l_mix[kBlock / 64][S][2][64];
+  __shared__ uint64_t l_run[kBlock / 64][RM][2][64];
+  const uint32_t wv = threadIdx.x >> 6;
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
     const bool live = lane < n;
+    bool runs_staged = false;  // wave-uniform
+    uint32_t nr = 0;
     // ---- round trip 1: per group; message type and Match per slot ----
     const uint32_t mi =
         MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * sizeof(MT)), lane) &
@@ -418,6 +436,8 @@ k_progress_step(PArgs a) {
       const bool has_ix = ty[s] == QE_MSG_APP_RESP || ty[s] == QE_MSG_APP_RESP_REJECT;
       ix[s] = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? o8 : kOOB);
       ac.add(has_ix, 8);
+      l_mix[wv][s][0][lane] = m0[s];
+      l_mix[wv][s][1][lane] = ix[s];
     }
     bool runs_counted = false;  // ACCT: the run table counts once, when first used
     auto ty_of = [&](uint32_t s) -> uint32_t { return static_cast<uint32_t>(tys >> (4 * s)) & 15u; };
@@ -430,7 +450,8 @@ k_progress_step(PArgs a) {
       const uint32_t t0 = ty_of(0);
       const bool msg = t0 >= QE_MSG_APP_RESP && t0 <= QE_MSG_UNREACHABLE;
       const bool ld = (trk & 1u) && (msg || self != 0u);
-      pb_load<ACCT>(a, g0, a.ibuf + g0, n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT, has_ix_of(0),
+      pb_load<ACCT>(a, g0, a.ibuf + g0, &l_mix[wv][0][0][0], n, lane, ld,
+                    t0 == QE_MSG_APP_RESP_REJECT, has_ix_of(0),
                     ld && (t0 == QE_MSG_APP_RESP || t0 == QE_MSG_HEARTBEAT_RESP), cur, ac);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
@@ -485,8 +506,9 @@ k_progress_step(PArgs a) {
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
         pb_load<ACCT>(a, row + a.stride, a.ibuf + static_cast<uint64_t>(s + 1) * F * a.stride + g0,
-                      n, lane, touched_of(s + 1), ty_of(s + 1) == QE_MSG_APP_RESP_REJECT,
-                      has_ix_of(s + 1), ring_of(s + 1), nxt, ac);
+                      &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
+                      ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), ring_of(s + 1),
+                      nxt, ac);
       PR p;
       p.match = cur.mt;
       p.next = cur.nx;
@@ -538,21 +560,37 @@ k_progress_step(PArgs a) {
       const uint32_t k3 = bcast_target ? popc(bset & ~below & ~(1u << s)) : 0u;
       uint32_t k2 = 0;
       bool lp = false;
+      if (!runs_staged &&
+          __builtin_amdgcn_ballot_w64(touched && tt == QE_MSG_APP_RESP_REJECT && cur.lt > 0)) {
+        // the first slot of the tile that needs findConflictByTerm loads the
+        // run table for every group of the tile
+        runs_staged = true;
+        const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), lane);
+        nr = rc < a.R ? rc : a.R;
+#pragma unroll
+        for (int r = 0; r < RM; r++) {
+          const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
+          if (static_cast<uint32_t>(r) < a.R) {
+            const uint32_t off = static_cast<uint32_t>(r) < nr ? o8 : kOOB;
+            l_run[wv][r][0][lane] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
+            l_run[wv][r][1][lane] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
+          } else {
+            l_run[wv][r][0][lane] = 0;
+            l_run[wv][r][1][lane] = 0;
+          }
+        }
+      }
       if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
           uint64_t probe = cur.hn;
-          if (cur.lt > 0) {  // the group's term runs, read here only (rejections are rare)
-            const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), lane);
-            const uint32_t nr = rc < a.R ? rc : a.R;
+          if (cur.lt > 0) {  // the group's term runs (read at most once per tile)
             uint64_t rf[RM], rt[RM];
 #pragma unroll
             for (int r = 0; r < RM; r++) {
-              const uint32_t off = static_cast<uint32_t>(r) < nr ? o8 : kOOB;
-              const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
-              rf[r] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
-              rt[r] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
+              rf[r] = l_run[wv][r][0][lane];
+              rt[r] = l_run[wv][r][1][lane];
             }
             probe = find_conflict_by_term<RM>(rf, rt, nr, li, probe, cur.lt);
             ac.add(!runs_counted, 1 + 16 * nr);
@@ -638,14 +676,16 @@ k_progress_step(PArgs a) {
       const bool wp = touched && (p.pending != pd0 || p.reset);
       const bool wf = touched && fl != cur.fl, ws = touched && p.start != cur.st;
       const bool wc = touched && p.count != cur.ct;
-      bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
-      bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? w8 : kOOB);
-      bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? w8 : kOOB);
-      bst8(fl, mk_rsrc(a.flags + row, n), wf ? w1 : kOOB);
-      bst8(p.start, mk_rsrc(a.istart + row, n), ws ? w1 : kOOB);
-      bst8(p.count, mk_rsrc(a.icount + row, n), wc ? w1 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? w8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wp))
+        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? w8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wf)) bst8(fl, mk_rsrc(a.flags + row, n), wf ? w1 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(ws)) bst8(p.start, mk_rsrc(a.istart + row, n), ws ? w1 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wc)) bst8(p.count, mk_rsrc(a.icount + row, n), wc ? w1 : kOOB);
       bst8(x.count_msgs, opt_rsrc(a.msg_count, row, n), lane);
-      bst64(x.first_index, opt_rsrc(a.msg_index, row, n), x.count_msgs ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(x.count_msgs != 0))
+        bst64(x.first_index, opt_rsrc(a.msg_index, row, n), x.count_msgs ? o8 : kOOB);
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);
