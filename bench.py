@@ -52,6 +52,9 @@ WORKLOADS = {
                           1 << 27, 10, "joint_rot"),
     "config4_repl": ("32M groups x 5 voters lockstep replication round (MaybeUpdate, "
                      "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
+    "config4_repl_joint": ("32M groups x joint 5+5 over 6 slots (replacing one voter: "
+                           "C_old {0,1,2,3,4}, C_new {0,1,2,3,5}) lockstep replication round",
+                           1 << 25, 6, "repl_joint"),
     "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
                      1 << 21, 5, "elec"),
     "config5_prevote_cq": ("2M groups x 64 fused election steps with PreVote and CheckQuorum "
@@ -230,9 +233,14 @@ def setup(name, G, S, kind, d, stats):
             mean_u = float(u.double().mean().item())
             bpg = 3 * 2 + 2 * 2 + 8 * mean_u + 9
         return step, bpg, G, "group-evals", {"batch": b, "out": out}
-    if kind == "repl":
-        b = engine.SlotBatch(G, S, d.dev, masks=(), votes=False, group_offset=goff)
+    if kind in ("repl", "repl_joint"):
+        joint = kind == "repl_joint"
+        b = engine.SlotBatch(G, S, d.dev, masks=("inc", "out") if joint else (), votes=False,
+                             group_offset=goff)
         engine.gen_groups(b, 0x5EED, p_absent=0)
+        if joint:  # the joint configuration of a one-voter replacement (EnterJoint)
+            b.inc.fill_(0b101111)
+            b.out.fill_(0b011111)
         rows = b.match_rows()
         lo = rows.min(dim=0).values
         hi = rows.max(dim=0).values
@@ -247,7 +255,7 @@ def setup(name, G, S, kind, d, stats):
         resp = b.match.clone() + (rb.match & 1023)
         del rb
         full = (1 << S) - 1
-        rm = torch.full((G,), full & 0b11110, dtype=torch.uint8, device=d.dev)
+        rm = torch.full((G,), full & ~1, dtype=torch.uint8, device=d.dev)  # every follower
         acks = torch.full((G,), 0b00111, dtype=torch.uint8, device=d.dev)
         read_ok = torch.empty(G, dtype=torch.uint8, device=d.dev)
         import ctypes as C
@@ -288,7 +296,7 @@ def setup(name, G, S, kind, d, stats):
             writes = 8 * (int((m1 != m0).sum()) + int((n1 != n0).sum()) +
                           int((st.committed != pristine["committed"]).sum())) + G
             prepare()
-        bpg = 2 + 24 + 8 * S + 16 * nresp + writes / G
+        bpg = 2 + 24 + 8 * S + 16 * nresp + writes / G + (2 if joint else 0)  # + inc/out masks
         return step, bpg, G, "group-rounds", {"b": b, "st": st, "resp": resp,
                                                "prepare": prepare}
     if kind in ("elec", "elec_pvcq"):
@@ -531,6 +539,29 @@ def load_traffic(workload):
     return load_pmc(workload).get("hbm_bytes_per_launch")
 
 
+# Vector-memory instruction cost on MI355X, streaming probe (scripts/
+# vmem_probe.hip, tlb_probe.hip; profiles/r02d_vmem_probe.txt): cycles per
+# wave instruction per CU at 2.4 GHz -- a u64 row (dwordx2, 64 lanes) ~57
+# (HBM-bound when full; >= 42 however few lanes are active), a byte row ~22.5.
+VMEM_PROBE_CYC = {"u64_row": 57.0, "u64_row_floor": 42.0, "u8_row": 22.5,
+                  "source": "profiles/r02d_vmem_probe.txt"}
+
+
+def vmem_issue(workload, kern_ms, units):
+    """Vector-memory instructions per launch (SQ_INSTS_VMEM_RD + _WR,
+    committed PMC) and the cycles each costs a CU at the measured kernel time,
+    for comparison with the streaming probe's per-instruction cost."""
+    t = load_pmc(workload)
+    rd, wr = t.get("vmem_rd_per_launch"), t.get("vmem_wr_per_launch")
+    if not rd or wr is None:
+        return None
+    n = rd + wr
+    return {"vmem_insts_per_launch": n, "vmem_rd": rd, "vmem_wr": wr,
+            "vmem_per_tile": n / (units / 64.0),
+            "cycles_per_vmem_inst_per_cu": kern_ms / 1000.0 * 2.4e9 * 256 / n,
+            "probe_cycles": VMEM_PROBE_CYC, "source": t.get("profile")}
+
+
 def valu_roofline(workload, kern_ms, units):
     """VALU-issue roofline of a VALU-bound kernel: its VALU instructions per
     launch (SQ_INSTS_VALU, committed PMC) over the live kernel time, against
@@ -573,6 +604,9 @@ def run_workload(name, args, d, steps, warmup):
         rv = valu_roofline(name, kern_avg, units)
         if rv:
             extra["roofline_valu"] = rv
+    vi = vmem_issue(name, kern_avg, G if kind in ("elec", "elec_pvcq") else units)  # per group
+    if vi:
+        extra["vmem_issue"] = vi
     return {**extra,
         "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
         "unit": f"{unit_name}/s", "value": value, "ms_per_step": ms_step,

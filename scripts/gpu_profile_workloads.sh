@@ -6,6 +6,9 @@
 #   write  --pmc WRITE_SIZE
 #   sq     --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 #                SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+#   vmem   --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM
+#                SQ_INSTS_VALU_INT64 (vector-memory instruction counts)
+# PASSES selects the passes (default: all).
 # Output: gpurun_out/profw/<workload>/<pass>/...; fold with
 #   python scripts/summarize_workloads.py <tag>
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
@@ -13,10 +16,12 @@ WLS=${WLS:-"config2_n5 config2_n7 config3_joint config3_joint_rot config4_repl c
 O="$R/gpurun_out/profw"; mkdir -p "$O"
 for W in $WLS; do
   mkdir -p "$O/$W"
+  P=" ${PASSES:-kt fetch write sq vmem} "
   BA="--workload $W --no-aux --no-cpu-baseline"
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$W/kt" -o kt -- python3 "$R/bench.py" $BA --steps 20 --warmup 5 > "$O/$W/kt.log" 2>&1 || { echo "$W kt failed"; tail -5 "$O/$W/kt.log"; exit 3; }
-  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/$W/fetch" -o fetch -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/fetch.log" 2>&1 || { echo "$W fetch failed"; tail -5 "$O/$W/fetch.log"; exit 4; }
-  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/$W/write" -o write -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/write.log" 2>&1 || { echo "$W write failed"; tail -5 "$O/$W/write.log"; exit 5; }
-  timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/$W/sq" -o sq -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/sq.log" 2>&1 || { echo "$W sq failed"; tail -5 "$O/$W/sq.log"; exit 6; }
+  [[ $P == *" kt "* ]] && { timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$W/kt" -o kt -- python3 "$R/bench.py" $BA --steps 20 --warmup 5 > "$O/$W/kt.log" 2>&1 || { echo "$W kt failed"; tail -5 "$O/$W/kt.log"; exit 3; }; }
+  [[ $P == *" fetch "* ]] && { timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/$W/fetch" -o fetch -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/fetch.log" 2>&1 || { echo "$W fetch failed"; tail -5 "$O/$W/fetch.log"; exit 4; }; }
+  [[ $P == *" write "* ]] && { timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/$W/write" -o write -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/write.log" 2>&1 || { echo "$W write failed"; tail -5 "$O/$W/write.log"; exit 5; }; }
+  [[ $P == *" sq "* ]] && { timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$O/$W/sq" -o sq -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/sq.log" 2>&1 || { echo "$W sq failed"; tail -5 "$O/$W/sq.log"; exit 6; }; }
+  [[ $P == *" vmem "* ]] && { timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VALU_INT64 --output-format csv -d "$O/$W/vmem" -o vmem -- python3 "$R/bench.py" $BA --steps 5 --warmup 1 > "$O/$W/vmem.log" 2>&1 || { echo "$W vmem failed"; tail -5 "$O/$W/vmem.log"; exit 7; }; }
   echo "$W done"
 done

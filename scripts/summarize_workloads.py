@@ -39,6 +39,7 @@ DOMINANT = {
     "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
     "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false>", 1),
     "confchange": ("void qe::k_confchange<5>", 1),
+    "config4_repl_joint": ("void qe::k_repl_stream<6, true, true,", 2),
 }
 
 
@@ -64,7 +65,7 @@ def main():
         shutil.copy(kts[0], os.path.join(outd, f"{wl}_kernel_stats.csv"))
         stats = {r["Name"]: r for r in csv.DictReader(open(kts[0]))}
         c = {}
-        for p in ("fetch", "write", "sq"):
+        for p in ("fetch", "write", "sq", "vmem"):
             c.update(counters(os.path.join(d, p, "**", "*counter_collection.csv")))
         names = [k for k in stats if k.startswith(prefix)]
         if not names:
@@ -84,6 +85,9 @@ def main():
                 t["valu_insts_per_launch"] = row["SQ_INSTS_VALU"]
                 t["salu_insts_per_launch"] = row.get("SQ_INSTS_SALU")
                 t["waves_per_launch"] = row.get("SQ_WAVES")
+            if "SQ_INSTS_VMEM_RD" in row:
+                t["vmem_rd_per_launch"] = row["SQ_INSTS_VMEM_RD"]
+                t["vmem_wr_per_launch"] = row.get("SQ_INSTS_VMEM_WR")
             traffic[wl] = t
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)

@@ -351,20 +351,30 @@ def test_commit_vote_low_slot_chunks(eng, orc, S, joint):
     check_commit_vote(eng, orc, b)
 
 
-def test_full_size_config3_properties(eng, orc):
-    """BASELINE config 3 at full size (128M joint 5+5 groups): the order-free
-    stats vector (incl. checksum) matches the oracle, and the result is
-    symmetric in the halves (swap inc/out)."""
+@pytest.mark.parametrize("layout", ["rotated", "bucketed"])
+def test_full_size_config3_properties(eng, orc, layout):
+    """BASELINE config 3 at full size (128M joint 5+5 groups), in both bench
+    layouts (per-group rotated slots; shape-bucketed): every group's commit
+    and vote compared with the OpenMP oracle, the order-free stats vector
+    (incl. checksum) matches, and the result is symmetric in the halves
+    (swap inc/out)."""
     G, S = 1 << 27, 10
-    b = gpu_batch(eng, G, S, 0xC0FFEE, n_inc=5, n_out=5)
+    gen = {"mask_mode": 2} if layout == "bucketed" else {}
+    b = gpu_batch(eng, G, S, 0xC0FFEE, n_inc=5, n_out=5, **gen)
     out = eng.Outputs(G, DEV, tally=False)
-    got = {}
+    got, per_group = {}, {}
     try:
         for k in CV_KERNELS:
             eng.tune("cv_kernel", k)
             stats = eng.stats_buffer(DEV)
             eng.commit_vote(b, out, stats=stats)
             got[k] = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+            if not per_group:
+                per_group["commit"] = out.commit.cpu().numpy().view(np.uint64)
+                per_group["vote"] = out.vote.cpu().numpy()
+            else:
+                assert torch.equal(torch.from_numpy(per_group["commit"].view(np.int64)).to(DEV),
+                                   out.commit), f"cv_kernel {k}"
             c1 = out.commit.clone()
             b.inc, b.out = b.out, b.inc
             eng.commit_vote(b, out)
@@ -377,7 +387,9 @@ def test_full_size_config3_properties(eng, orc):
     hb = host_batch(orc, b)
     del b
     torch.cuda.empty_cache()
-    _, _, _, _, ostats = orc.commit_vote(hb)
+    c_ref, v_ref, _, _, ostats = orc.commit_vote(hb)
+    np.testing.assert_array_equal(per_group["commit"], c_ref)
+    np.testing.assert_array_equal(per_group["vote"], v_ref)
     for k in CV_KERNELS:
         np.testing.assert_array_equal(got[k], ostats, err_msg=f"cv_kernel {k}")
 
