@@ -161,16 +161,14 @@ static int launch_elec(const EArgs &a, hipStream_t st) {
 }
 
 int QE_CAT(dispatch_elec_, QE_S)(const EArgs &a, hipStream_t st) {
-  const int opt = (a.flags & 3u) | (a.sresp ? 4 : 0);
+  const int opt = (a.flags & 3u) | (a.sresp ? 4 : 0) | (a.out ? 8 : 0);
   switch (opt) {
-    case 0: return launch_elec<0>(a, st);
-    case 1: return launch_elec<1>(a, st);
-    case 2: return launch_elec<2>(a, st);
-    case 3: return launch_elec<3>(a, st);
-    case 4: return launch_elec<4>(a, st);
-    case 5: return launch_elec<5>(a, st);
-    case 6: return launch_elec<6>(a, st);
-    default: return launch_elec<7>(a, st);
+#define QE_E(o) \
+  case o: return launch_elec<o>(a, st);
+    QE_E(0) QE_E(1) QE_E(2) QE_E(3) QE_E(4) QE_E(5) QE_E(6) QE_E(7)
+    QE_E(8) QE_E(9) QE_E(10) QE_E(11) QE_E(12) QE_E(13) QE_E(14)
+#undef QE_E
+    default: return launch_elec<15>(a, st);
   }
 }
 

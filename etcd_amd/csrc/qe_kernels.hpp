@@ -498,15 +498,19 @@ struct EArgs {
 enum { E_GROUPS, E_ELEC, E_LEAD, E_DOWN, E_WON, E_LOST, E_PEND, E_GR, E_RJ, E_VIOL, E_CSUM, E_N };
 
 // One TallyVotes with the invariant checks; counts into the
-// per-lane 32-bit step counters.
+// per-lane 32-bit step counters.  JOINT = false: Voters[1] is empty for every
+// group (no out mask), so JointConfig.VoteResult is the incoming half's
+// MajorityConfig.VoteResult and the half-swap symmetry holds by construction.
+template <bool JOINT>
 __device__ __forceinline__ uint32_t elec_tally(uint32_t mi, uint32_t mo, uint32_t ml, uint32_t vd,
                                                uint32_t gr, uint32_t gbefore,
                                                uint32_t (&cnt)[E_N]) {
+  if constexpr (!JOINT) mo = 0;
   const uint32_t voters = (mi | mo) & ~ml;
   const uint32_t gcn = popc(vd & gr & voters), rcn = popc(vd & ~gr & voters);
-  const uint32_t res = joint_vote(mi, mo, vd, gr);
-  const uint32_t sym = joint_vote(mo, mi, vd, gr);
-  const uint32_t n0 = popc(mi), n1 = popc(mo);
+  const uint32_t res = JOINT ? joint_vote(mi, mo, vd, gr) : majority_vote(mi, vd, gr);
+  const uint32_t sym = JOINT ? joint_vote(mo, mi, vd, gr) : res;
+  const uint32_t n0 = popc(mi), n1 = JOINT ? popc(mo) : 0u;
   const bool won_ok = (n0 == 0 || popc(gr & vd & mi) >= n0 / 2 + 1) &&
                       (n1 == 0 || popc(gr & vd & mo) >= n1 / 2 + 1);
   cnt[E_VIOL] += (sym != res) + (res == kVoteWon && !won_ok) + (gcn < gbefore);
@@ -521,6 +525,7 @@ __device__ __forceinline__ uint32_t elec_tally(uint32_t mi, uint32_t mo, uint32_
 // raft.campaign (raft/raft.go:785-803): PreVote -> becomePreCandidate (term
 // kept), else becomeCandidate (term+1); votes reset; self-vote; a won
 // (single-voter) tally moves on to the election / leadership.
+template <bool JOINT>
 __device__ __forceinline__ void elec_campaign(bool pre, uint32_t mi, uint32_t mo, uint32_t ml,
                                               uint32_t self, uint64_t &t, uint32_t &sta,
                                               uint32_t &vd, uint32_t &gr, uint32_t (&cnt)[E_N]) {
@@ -529,7 +534,7 @@ __device__ __forceinline__ void elec_campaign(bool pre, uint32_t mi, uint32_t mo
     sta = QE_STATE_PRE_CANDIDATE;
     vd = self;
     gr = self;
-    go = elec_tally(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon;
+    go = elec_tally<JOINT>(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon;
   }
   if (go) {
     t += 1;
@@ -537,19 +542,21 @@ __device__ __forceinline__ void elec_campaign(bool pre, uint32_t mi, uint32_t mo
     vd = self;
     gr = self;
     cnt[E_ELEC] += 1;
-    if (elec_tally(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon) {
+    if (elec_tally<JOINT>(mi, mo, ml, vd, gr, 0u, cnt) == kVoteWon) {
       sta = QE_STATE_LEADER;
       cnt[E_LEAD] += 1;
     }
   }
 }
 
-// OPT: bit 0 PreVote, bit 1 CheckQuorum, bit 2 scripted responses
-// (compile-time, so the plain simulation carries none of their branches).
+// OPT: bit 0 PreVote, bit 1 CheckQuorum, bit 2 scripted responses, bit 3
+// joint (an out mask is given) -- compile-time, so the plain simulation
+// carries none of their branches.
 template <int S, typename MT, int OPT>
 __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr bool pre = (OPT & 1) != 0, cq = (OPT & 2) != 0, scripted = (OPT & 4) != 0;
+  constexpr bool joint = (OPT & 8) != 0;
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * kBlock;
   uint64_t cnt[E_N];
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
   for (uint64_t g = tid; g < a.G; g += nthreads) {
     const uint64_t gid = a.goff + g;
     const uint32_t mi = incp ? (incp[g] & kFull) : kFull;
-    const uint32_t mo = outp ? (outp[g] & kFull) : 0u;
+    const uint32_t mo = (joint && outp) ? (outp[g] & kFull) : 0u;
     const uint32_t ml = lrnp ? (lrnp[g] & kFull) : 0u;
     const uint32_t self = 1u << (a.self_slot[g] % S);
     const uint32_t voters = mi | mo;
@@ -605,15 +612,16 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
           }
           const uint32_t recent = resp | self;
           const uint32_t present = voters & ~ml;
-          const bool qa = joint_vote(mi, mo, present, recent & present) == kVoteWon;
-          const bool qb = joint_vote(mo, mi, present, recent & present) == kVoteWon;
+          const bool qa = (joint ? joint_vote(mi, mo, present, recent & present)
+                                 : majority_vote(mi, present, recent & present)) == kVoteWon;
+          const bool qb = joint ? joint_vote(mo, mi, present, recent & present) == kVoteWon : qa;
           c32[E_VIOL] += (qa != qb);
           if (!qa) {
             sta = QE_STATE_FOLLOWER;
             c32[E_DOWN] += 1;
           }
         } else if (sta == QE_STATE_FOLLOWER || sta == QE_STATE_LEADER || hup) {
-          elec_campaign(pre, mi, mo, ml, self, t, sta, vd, gr, c32);
+          elec_campaign<joint>(pre, mi, mo, ml, self, t, sta, vd, gr, c32);
         } else {
           // d = fmix32(gkey + step*C1 + s*C2) per slot (oracle elec_draw)
           if constexpr (!scripted) {
@@ -629,10 +637,10 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
           const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
           vd |= fresh;
           gr |= fresh & val;
-          const uint32_t res = elec_tally(mi, mo, ml, vd, gr, gbefore, c32);
+          const uint32_t res = elec_tally<joint>(mi, mo, ml, vd, gr, gbefore, c32);
           if (res == kVoteWon) {
             if (sta == QE_STATE_PRE_CANDIDATE) {
-              elec_campaign(false, mi, mo, ml, self, t, sta, vd, gr, c32);
+              elec_campaign<joint>(false, mi, mo, ml, self, t, sta, vd, gr, c32);
             } else {
               sta = QE_STATE_LEADER;
               c32[E_LEAD] += 1;
