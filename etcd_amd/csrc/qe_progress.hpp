@@ -683,9 +683,9 @@ k_progress_step(PArgs a) {
       if (__builtin_amdgcn_ballot_w64(wf)) bst8(fl, mk_rsrc(a.flags + row, n), wf ? w1 : kOOB);
       if (__builtin_amdgcn_ballot_w64(ws)) bst8(p.start, mk_rsrc(a.istart + row, n), ws ? w1 : kOOB);
       if (__builtin_amdgcn_ballot_w64(wc)) bst8(p.count, mk_rsrc(a.icount + row, n), wc ? w1 : kOOB);
-      bst8(x.count_msgs, opt_rsrc(a.msg_count, row, n), lane);
-      if (__builtin_amdgcn_ballot_w64(x.count_msgs != 0))
-        bst64(x.first_index, opt_rsrc(a.msg_index, row, n), x.count_msgs ? o8 : kOOB);
+      if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
+      if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
+        bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);
@@ -700,10 +700,11 @@ k_progress_step(PArgs a) {
     }
     const uint32_t bc = popc(bset);
     bst64(c, r_commit, c != c0 ? o8 : kOOB);
-    bst_mask<MT>(sent, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
-    bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
-    bst_mask<MT>(tnow, opt_rsrc(static_cast<const MT *>(a.tnow), g0, n), lane);
-    bst8(bc, opt_rsrc(static_cast<const uint8_t *>(a.bcast), g0, n), lane);
+    // optional outputs: no instruction at all for a NULL one
+    if (a.sent) bst_mask<MT>(sent, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+    if (a.snap) bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+    if (a.tnow) bst_mask<MT>(tnow, opt_rsrc(static_cast<const MT *>(a.tnow), g0, n), lane);
+    if (a.bcast) bst8(bc, opt_rsrc(static_cast<const uint8_t *>(a.bcast), g0, n), lane);
     ac.add(live && c != c0, 8);
     ac.add(live && a.sent, sizeof(MT));
     ac.add(live && a.snap, sizeof(MT));
