@@ -704,8 +704,10 @@ def main():
             r = run_workload(name, args, d, max(5, args.steps // 2), max(2, args.warmup // 2))
             aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
                                            "achieved_GBs", "hbm_frac", "invariant_violations")}
-            if "roofline_valu" in r:
-                aux[name]["roofline_valu"] = r["roofline_valu"]
+            for k in ("roofline_valu", "vmem_issue"):
+                if k in r:
+                    aux[name][k] = r[k]
+
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)

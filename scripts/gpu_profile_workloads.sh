@@ -12,7 +12,7 @@
 # Output: gpurun_out/profw/<workload>/<pass>/...; fold with
 #   python scripts/summarize_workloads.py <tag>
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
-WLS=${WLS:-"config2_n5 config2_n7 config3_joint config3_joint_rot config4_repl config5_elec config5_prevote_cq progress_step confchange"}
+WLS=${WLS:-"config2_n5 config2_n7 config3_joint config3_joint_rot config4_repl config4_repl_joint config5_elec config5_prevote_cq progress_step confchange"}
 O="$R/gpurun_out/profw"; mkdir -p "$O"
 for W in $WLS; do
   mkdir -p "$O/$W"
