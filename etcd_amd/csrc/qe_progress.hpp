@@ -313,21 +313,18 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
 struct PB {  // per-peer loads of one slot
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t fl, st, ct;
-  uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring
+  uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring (pb_ring)
 };
 
 // Loads of slot row `row` (= s*stride + tile0): the Progress fields of a
-// touched peer, RejectHint/LogTerm of a reject, and (F <= kRingChunk) the
-// peer's ring entries when FreeLE may run -- one coalesced entry row each
-// (rb: entry 0 of this slot's rings for the tile).
+// touched peer and RejectHint/LogTerm of a reject.
 // A wave-level branch skips each group of loads no lane needs (an issued
 // vector memory instruction costs the CU's memory path about the same
 // whether or not its lanes are masked off).
 template <bool ACCT>
-__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *rb,
-                                        const uint64_t *l_mix, uint32_t n, uint32_t lane,
-                                        bool touched, bool rej, bool has_ix, bool ring, PB &b,
-                                        Acct<ACCT> &ac) {
+__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *l_mix,
+                                        uint32_t n, uint32_t lane, bool touched, bool rej,
+                                        bool has_ix, PB &b, Acct<ACCT> &ac) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
   b.nx = 0;
@@ -348,7 +345,17 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
   ac.add(rej, 16);
 #pragma unroll
   for (int k = 0; k < kRingChunk; k++) b.rw[k] = 0;
-  if (a.F <= static_cast<uint32_t>(kRingChunk) && ring) {  // lanes < n only
+}
+
+// (F <= kRingChunk) the peer's ring entries when FreeLE may run (`ring`:
+// lanes < n only), one coalesced entry row each (rb: entry 0 of this slot's
+// rings for the tile).  Loaded when the slot's turn comes, after the next
+// slot's Progress loads are issued, not with that prefetch: one ring in
+// registers instead of two keeps the kernel at 3 waves/SIMD without scratch
+// (A/B: 3.51 vs 3.56 ms, 4 waves/SIMD spills and is slower).
+__device__ __forceinline__ void pb_ring(const PArgs &a, const uint64_t *rb, uint32_t lane,
+                                        bool ring, PB &b) {
+  if (ring) {
 #pragma unroll
     for (int k = 0; k < kRingChunk; k++)
       if (static_cast<uint32_t>(k) < a.F) b.rw[k] = rb[k * a.stride + lane];
@@ -450,9 +457,8 @@ k_progress_step(PArgs a) {
       const uint32_t t0 = ty_of(0);
       const bool msg = t0 >= QE_MSG_APP_RESP && t0 <= QE_MSG_UNREACHABLE;
       const bool ld = (trk & 1u) && (msg || self != 0u);
-      pb_load<ACCT>(a, g0, a.ibuf + g0, &l_mix[wv][0][0][0], n, lane, ld,
-                    t0 == QE_MSG_APP_RESP_REJECT, has_ix_of(0),
-                    ld && (t0 == QE_MSG_APP_RESP || t0 == QE_MSG_HEARTBEAT_RESP), cur, ac);
+      pb_load<ACCT>(a, g0, &l_mix[wv][0][0][0], n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT,
+                    has_ix_of(0), cur, ac);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
@@ -505,10 +511,9 @@ k_progress_step(PArgs a) {
       const bool touched = touched_of(s);
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
-        pb_load<ACCT>(a, row + a.stride, a.ibuf + static_cast<uint64_t>(s + 1) * F * a.stride + g0,
-                      &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
-                      ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), ring_of(s + 1),
-                      nxt, ac);
+        pb_load<ACCT>(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
+                      ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt, ac);
+      if (row_ring) pb_ring(a, a.ibuf + static_cast<uint64_t>(s) * F * a.stride + g0, lane, ring_of(s), cur);
       PR p;
       p.match = cur.mt;
       p.next = cur.nx;
