@@ -55,6 +55,9 @@ WORKLOADS = {
     "config4_repl_joint": ("32M groups x joint 5+5 over 6 slots (replacing one voter: "
                            "C_old {0,1,2,3,4}, C_new {0,1,2,3,5}) lockstep replication round",
                            1 << 25, 6, "repl_joint"),
+    "ready_collect": ("64M groups: qe_collect of a Ready-style commit delta (half the groups "
+                      "flagged): ascending group ids + their committed index", 1 << 26, 1,
+                      "collect"),
     "config5_elec": ("2M groups x 64 fused election steps (5 voters, drop 0.2, grant 0.5)",
                      1 << 21, 5, "elec"),
     "config5_prevote_cq": ("2M groups x 64 fused election steps with PreVote and CheckQuorum "
@@ -395,6 +398,30 @@ def setup(name, G, S, kind, d, stats):
                          lib.qe_progress_step(C.byref(p_), C.byref(m_), sp, stream))
 
         return step, bpg, G, "group-rounds", {"ps": ps, "msgs": msgs, "prepare": prepare}
+    if kind == "collect":
+        gen = torch.Generator(device=d.dev).manual_seed(0xC011 + d.rank)
+        flags = (torch.rand(G, device=d.dev, generator=gen) < 0.5).to(torch.uint8)
+        values = torch.randint(0, 1 << 40, (G,), device=d.dev, generator=gen)
+        import ctypes as C
+        lib = engine._lib.lib()
+        scratch = torch.empty((lib.qe_collect_scratch_bytes(G) + 7) // 8, dtype=torch.int64,
+                              device=d.dev)
+        groups = torch.empty(G, dtype=torch.int64, device=d.dev)
+        vals = torch.empty(G, dtype=torch.int64, device=d.dev)
+        count = torch.empty(1, dtype=torch.int64, device=d.dev)
+        stream = engine._stream(d.dev)
+        args_ = [G, goff] + [engine._ptr(t) for t in (flags, values, groups, vals, count, scratch)]
+
+        def step():
+            engine.check("qe_collect", lib.qe_collect(*args_, stream))
+
+        step()
+        torch.cuda.synchronize(d.dev)
+        sel = int(count.item())
+        # every flag read once; per selected group its value read and the id
+        # and value written (8 + 16 B)
+        bpg = 1 + 24 * sel / G
+        return step, bpg, G, "groups", {"t": (flags, values, scratch, groups, vals, count)}
     if kind == "confchange":
         cs = engine.ConfState(G, S, d.dev)
         ps = engine.ProgressState(G, S, 1, 1, d.dev)

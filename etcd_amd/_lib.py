@@ -165,6 +165,8 @@ PROTOTYPES = {
     "qe_election_steps": (C.c_int, [C.POINTER(QeElectionState), C.POINTER(QeElectionParams),
                                     vp, vp]),
     "qe_stats_reduce": (C.c_int, [vp, vp, vp]),
+    "qe_collect_scratch_bytes": (C.c_size_t, [u64]),
+    "qe_collect": (C.c_int, [u64, u64, vp, vp, vp, vp, vp, vp, vp]),
     "qe_gen_groups": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeGenParams), vp]),
     "qe_apply_append_resps": (C.c_int, [u64, u32, u64, vp, vp, u64, vp, vp, vp, vp, vp]),
     "qe_pack_confstate": (C.c_int, [C.POINTER(QeConfStateCSR), u32, vp, vp, vp, vp, vp, vp]),

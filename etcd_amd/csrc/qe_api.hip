@@ -5,6 +5,7 @@
 
 #include "qe_dispatch.hpp"
 #include "qe_conf.hpp"
+#include "qe_collect.hpp"
 
 namespace qe {
 
@@ -508,6 +509,34 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
     QE_CC_CASE(13) QE_CC_CASE(14) QE_CC_CASE(15) QE_CC_CASE(16)
 #undef QE_CC_CASE
   }
+  return hip_status(hipGetLastError());
+}
+
+size_t qe_collect_scratch_bytes(uint64_t num_groups) {
+  const uint64_t nb = (num_groups + kCollectChunk - 1) / kCollectChunk;
+  return static_cast<size_t>(nb * (sizeof(uint32_t) + sizeof(uint64_t)) + 64);
+}
+
+int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint8_t *flags,
+               const uint64_t *values, uint64_t *out_groups, uint64_t *out_values,
+               uint64_t *out_count, void *scratch, void *stream) {
+  if (!out_count || (num_groups && (!flags || !scratch))) return QE_EINVAL;
+  if (out_values && !values) return QE_EINVAL;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (num_groups == 0)
+    return hip_status(hipMemsetAsync(out_count, 0, sizeof(uint64_t), st));
+  const uint64_t nb = (num_groups + kCollectChunk - 1) / kCollectChunk;
+  if (nb > 0x7FFFFFFFull) return QE_ERANGE;
+  // scratch: offsets (u64, 8-B aligned at the start), then counts (u32)
+  if (reinterpret_cast<uintptr_t>(scratch) % 8) return QE_EINVAL;
+  uint64_t *offsets = static_cast<uint64_t *>(scratch);
+  uint32_t *counts = reinterpret_cast<uint32_t *>(offsets + nb);
+  const bool vec = (reinterpret_cast<uintptr_t>(flags) % 16) == 0;
+  hipLaunchKernelGGL(k_collect_count, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, st, flags,
+                     num_groups, vec, counts);
+  hipLaunchKernelGGL(k_collect_scan, dim3(1), dim3(1024), 0, st, counts, nb, offsets, out_count);
+  hipLaunchKernelGGL(k_collect_scatter, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, st, flags,
+                     num_groups, vec, group_offset, values, offsets, out_groups, out_values);
   return hip_status(hipGetLastError());
 }
 

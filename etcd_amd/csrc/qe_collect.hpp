@@ -1,0 +1,149 @@
+// qe_collect.hpp — qe_collect: the groups a batch step changed, as a dense
+// list in ascending group order.
+//
+// The consumer is the host's Ready loop: raft only reports a HardState when
+// it differs from the previous one (raft/node.go:571-573, newReady; the
+// RawNode keeps prevHardSt, raft/rawnode.go:152-176), so after a batched
+// round the host needs the groups whose commit advanced (the `adv` flags of
+// qe_replication_round) and their new index -- not all G words over PCIe.
+//
+// Three passes over 4096-group chunks (256 threads x 16 flags):
+//   count    per-chunk number of selected groups;
+//   scan     one block: exclusive prefix of the chunk counts, and the total;
+//   scatter  per chunk, in 16 rounds of 256 consecutive groups: the selected
+//            groups of a round at consecutive positions (coalesced stores).
+// The count pass reads flags as 16-B vectors when the array is 16-B aligned;
+// values (optional) are gathered for the selected groups only.
+// Measured (64M groups, half flagged): 0.31 ms; a first version that wrote
+// each thread's 16-group run itself (strided stores) took 1.14 ms.
+#pragma once
+#include "qe_kernels.hpp"
+
+namespace qe {
+
+constexpr uint32_t kCollectPer = 16;                    // flags per thread
+constexpr uint32_t kCollectChunk = kBlock * kCollectPer;  // groups per block
+
+__device__ __forceinline__ uint32_t collect_bits(const uint8_t *flags, uint64_t G, uint64_t g,
+                                                 bool vec) {
+  // bit i: flag g + i is set
+  uint32_t m = 0;
+  if (vec && g + kCollectPer <= G) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(flags + g);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) m |= ((w[k] >> (8 * b)) & 0xFFu) ? (1u << (4 * k + b)) : 0u;
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kCollectPer; i++)
+      m |= (g + i < G && flags[g + i] != 0) ? (1u << i) : 0u;
+  }
+  return m;
+}
+
+// Block-wide exclusive prefix of v (kBlock threads); *total = block sum.
+__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t *total) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; k++) {
+    before += static_cast<uint32_t>(k) < w ? wsum[k] : 0u;
+    all += wsum[k];
+  }
+  *total = all;
+  return before + inc - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_collect_count(const uint8_t *flags, uint64_t G, bool vec,
+                                                          uint32_t *counts) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kCollectChunk + threadIdx.x * kCollectPer;
+  const uint32_t c = __builtin_popcount(collect_bits(flags, G, g, vec));
+  uint32_t total;
+  block_exclusive(c, &total);
+  if (threadIdx.x == 0) counts[blockIdx.x] = total;
+}
+
+// One block: offsets[b] = sum of counts[0..b), *out_count = the total.
+__global__ __launch_bounds__(1024) void k_collect_scan(const uint32_t *counts, uint64_t nb,
+                                                       uint64_t *offsets, uint64_t *out_count) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  // thread t owns the contiguous range [t*per, (t+1)*per)
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t b0 = t * per, b1 = b0 + per < nb ? b0 + per : nb;
+  uint64_t s = 0;
+  for (uint64_t b = b0; b < b1; b++) s += counts[b];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint64_t o = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += o;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  for (uint64_t b = b0; b < b1; b++) {
+    offsets[b] = run;
+    run += counts[b];
+  }
+  if (t == 1023) *out_count = part[1023];
+}
+
+// Scatter: the chunk is walked in kCollectPer rounds of kBlock consecutive
+// groups (thread t takes group base + r*kBlock + t), so the selected groups
+// of a round land at consecutive positions in lane order: a wave's stores
+// are one contiguous run (ballot + mbcnt for the rank inside the wave, the
+// waves' counts through LDS for the block), not 16-entry runs per thread.
+__global__ __launch_bounds__(kBlock) void k_collect_scatter(const uint8_t *flags, uint64_t G,
+                                                            bool vec, uint64_t goff,
+                                                            const uint64_t *values,
+                                                            const uint64_t *offsets,
+                                                            uint64_t *out_groups,
+                                                            uint64_t *out_values) {
+  (void)vec;
+  __shared__ uint32_t wcnt[kCollectPer][kBlock / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kCollectChunk;
+  bool f[kCollectPer];
+  uint32_t rank[kCollectPer];
+#pragma unroll
+  for (uint32_t r = 0; r < kCollectPer; r++) {
+    const uint64_t g = base + r * kBlock + tid;
+    f[r] = g < G && flags[g] != 0;
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(f[r]);
+    rank[r] = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
+                                        __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
+    if (lane == 0) wcnt[r][w] = static_cast<uint32_t>(__builtin_popcountll(bal));
+  }
+  __syncthreads();
+  uint64_t pos = offsets[blockIdx.x];
+#pragma unroll
+  for (uint32_t r = 0; r < kCollectPer; r++) {
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kBlock / 64; k++) {
+      before += k < w ? wcnt[r][k] : 0u;
+      all += wcnt[r][k];
+    }
+    if (f[r]) {
+      const uint64_t g = base + r * kBlock + tid;
+      const uint64_t p = pos + before + rank[r];
+      if (out_groups) out_groups[p] = goff + g;
+      if (out_values) out_values[p] = values[g];
+    }
+    pos += all;
+  }
+}
+
+}  // namespace qe

@@ -119,6 +119,26 @@ def stats_reduce(stats):
     return out
 
 
+def collect(flags, values=None, group_offset=0, scratch=None):
+    """qe_collect: the groups with flags[g] != 0 in ascending order (the
+    Ready-style delta of a batch step, e.g. qe_replication_round's `adv` with
+    `committed` as values) -> (groups int64[n], values int64[n] or None).
+    One int64 count is read back to size the result."""
+    G = flags.numel()
+    dev = flags.device
+    lib = _lib.lib()
+    if scratch is None:
+        scratch = torch.empty((lib.qe_collect_scratch_bytes(G) + 7) // 8, dtype=torch.int64,
+                              device=dev)
+    groups = torch.empty(max(1, G), dtype=torch.int64, device=dev)
+    vals = torch.empty(max(1, G), dtype=torch.int64, device=dev) if values is not None else None
+    count = torch.empty(1, dtype=torch.int64, device=dev)
+    check("qe_collect", lib.qe_collect(G, group_offset, _ptr(flags), _ptr(values), _ptr(groups),
+                                       _ptr(vals), _ptr(count), _ptr(scratch), _stream(dev)))
+    n = int(count.item())
+    return groups[:n], (vals[:n] if vals is not None else None)
+
+
 def stats_dict(folded):
     v = folded.detach().cpu().numpy().view(np.uint64)
     return {name: int(v[i]) for i, name in enumerate(_lib.STAT_NAMES)}

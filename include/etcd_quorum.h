@@ -553,6 +553,23 @@ typedef struct qe_conf_changes {
 int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress *p,
                   void *stream);
 
+/* ---- Ready deltas ------------------------------------------------------ */
+
+/* The groups a batch step changed, as a dense list in ascending group order:
+ * for every g with flags[g] != 0, out_groups[i] = group_offset + g and (when
+ * out_values is non-NULL) out_values[i] = values[g]; *out_count (device) =
+ * their number.  raft reports a HardState only when it changed
+ * (raft/node.go:571-573 newReady, raft/rawnode.go:152-176 prevHardSt): with
+ * flags = qe_replication_round's `adv` and values = `committed` this is the
+ * per-round commit delta a host ships instead of all G words.  out_groups /
+ * out_values hold up to num_groups entries (NULL: not written).  scratch:
+ * qe_collect_scratch_bytes(num_groups) bytes of device memory, 8-B aligned.
+ * All pointers are device pointers; stream-ordered. */
+size_t qe_collect_scratch_bytes(uint64_t num_groups);
+int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint8_t *flags,
+               const uint64_t *values, uint64_t *out_groups, uint64_t *out_values,
+               uint64_t *out_count, void *scratch, void *stream);
+
 /* ---- statistics -------------------------------------------------------- */
 
 /* out[QE_STATS_COUNTERS] (device) = sum over shards of stats (device). */
