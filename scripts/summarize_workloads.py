@@ -40,6 +40,7 @@ DOMINANT = {
     "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false>", 1),
     "confchange": ("void qe::k_confchange<5>", 1),
     "config4_repl_joint": ("void qe::k_repl_stream<6, true, true,", 2),
+    "ready_collect": ("qe::k_collect_scatter", 1),
 }
 
 
