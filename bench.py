@@ -66,6 +66,9 @@ WORKLOADS = {
     "progress_step": ("16M groups x 5 peers: one round of MsgAppResp accept/reject + "
                       "MsgHeartbeatResp through the full Progress state machine "
                       "(inflights F=8, leader-log model R=4)", 1 << 24, 5, "progress"),
+    "progress_send": ("16M groups x bcastAppend after a proposal (qe_progress_send to the 4 "
+                      "followers, StateReplicate, Inflights F=8 with room): one MsgApp and one "
+                      "ring entry per peer", 1 << 24, 5, "psend"),
     "confchange": ("16M groups x Changer.Simple(AddNode(learner), AddLearnerNode(new)) on "
                    "slot masks: promote a learner, add a learner with initProgress "
                    "(3 voters + 1 learner + 1 free slot)", 1 << 24, 5, "confchange"),
@@ -398,6 +401,51 @@ def setup(name, G, S, kind, d, stats):
                          lib.qe_progress_step(C.byref(p_), C.byref(m_), sp, stream))
 
         return step, bpg, G, "group-rounds", {"ps": ps, "msgs": msgs, "prepare": prepare}
+    if kind == "psend":
+        # raft.appendEntry -> bcastAppend (raft/raft.go:515-522, :432-492):
+        # every follower in StateReplicate with room in its Inflights gets one
+        # MsgApp of up to 16 entries (one ring append, OptimisticUpdate)
+        F, ME = 8, 16
+        ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, max_ents=ME)
+        n = S * ps.stride
+        gen = torch.Generator(device=d.dev).manual_seed(0x5E4D + d.rank)
+        base = torch.randint(1 << 20, 1 << 40, (ps.stride,), device=d.dev, generator=gen)
+        ps.match.copy_(base.repeat(S) + torch.randint(0, 64, (n,), device=d.dev, generator=gen))
+        ps.next.copy_(ps.match + 1 + torch.randint(0, 4, (n,), device=d.dev, generator=gen))
+        ps.flags.fill_(1 | 8)  # StateReplicate, RecentActive
+        ps.istart.copy_(torch.randint(0, F, (n,), device=d.dev, generator=gen).to(torch.uint8))
+        ps.icount.copy_(torch.randint(0, F, (n,), device=d.dev, generator=gen).to(torch.uint8))
+        ps.last_index.copy_(base[:G] + 128)
+        ps.first_index.copy_(base[:G] - 64)
+        full = (1 << S) - 1
+        want = torch.full((G,), full & ~1, dtype=torch.uint8, device=d.dev)  # not the leader
+        sent = torch.zeros(G, dtype=torch.uint8, device=d.dev)
+        snap = torch.zeros(G, dtype=torch.uint8, device=d.dev)
+        mutable = ("next", "icount")
+        pristine = {k: getattr(ps, k).clone() for k in mutable}
+
+        def prepare():
+            for k in mutable:
+                getattr(ps, k).copy_(pristine[k])
+
+        import ctypes as C
+        p_ = ps.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+
+        def step():
+            engine.check("qe_progress_send", lib.qe_progress_send(
+                C.byref(p_), engine._ptr(want), 0, ME, engine._ptr(sent), engine._ptr(snap),
+                stream))
+
+        # per group: want mask, firstIndex/lastIndex read, sent/snap masks
+        # written; per wanted peer Next, flags, Inflights start/count read,
+        # Next, count and the appended entry written (start and flags do not
+        # change): 1 + 16 + 2 + 4 * (11 + 17) = 131 B
+        nw = bin(full & ~1).count("1")
+        bpg = 1 + 16 + 2 + nw * (11 + 17)
+        return step, bpg, G, "group-bcasts", {"ps": ps, "prepare": prepare,
+                                              "t": (want, sent, snap)}
     if kind == "collect":
         gen = torch.Generator(device=d.dev).manual_seed(0xC011 + d.rank)
         flags = (torch.rand(G, device=d.dev, generator=gen) < 0.5).to(torch.uint8)

@@ -759,42 +759,54 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
     x.li = bld64(mk_rsrc(a.last_index + g0, n * 8), w ? o8 : kOOB);
     x.snap = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), w ? o8 : kOOB) : x.fi - 1;
     uint32_t sent = 0, snapm = 0;
+    // every slot's Progress loads first (one batch in flight), then the sends
+    uint64_t nx[S];
+    uint32_t fl[S], st[S], ct[S];
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const bool on = (w >> s) & 1u;
       const uint32_t r8 = on ? o8 : kOOB, r1 = on ? lane : kOOB;
+      nx[s] = bld64(mk_rsrc(a.next + row, n * 8), r8);
+      fl[s] = bld8(mk_rsrc(a.flags + row, n), r1);
+      st[s] = bld8(mk_rsrc(a.istart + row, n), r1);
+      ct[s] = bld8(mk_rsrc(a.icount + row, n), r1);
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      const bool on = (w >> s) & 1u;
       PR p;
       p.match = 0;
-      p.next = bld64(mk_rsrc(a.next + row, n * 8), r8);
-      const uint32_t fl = bld8(mk_rsrc(a.flags + row, n), r1);
-      p.state = fl & QE_PF_STATE;
-      p.probe_sent = (fl & QE_PF_PROBE_SENT) != 0;
-      p.recent_active = (fl & QE_PF_RECENT_ACTIVE) != 0;
-      p.start = bld8(mk_rsrc(a.istart + row, n), r1);
-      p.count = bld8(mk_rsrc(a.icount + row, n), r1);
+      p.next = nx[s];
+      p.state = fl[s] & QE_PF_STATE;
+      p.probe_sent = (fl[s] & QE_PF_PROBE_SENT) != 0;
+      p.recent_active = (fl[s] & QE_PF_RECENT_ACTIVE) != 0;
+      p.start = st[s];
+      p.count = ct[s];
       p.pending = 0;
       p.reset = 0;
-      const uint64_t nx0 = p.next;
-      const uint32_t st0 = p.start, ct0 = p.count;
       x.rb = a.ibuf + static_cast<uint64_t>(s) * a.F * a.stride + g0;
       x.rs = a.stride;
       x.lane = lane;
-      x.row = a.F <= static_cast<uint32_t>(kRingChunk);
+      // one maybeSendAppend appends at most one entry: stored directly at
+      // its ring position (one instruction), not as F entry-row stores
+      x.row = false;
       x.count_msgs = 0;
       x.first_index = 0;
       x.snapped = false;
       PRun run{0, 0, 0};
-      const PRun none{0, 0, 0};
       send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, x, run, ac);
-      if (x.row) ring_flush(x, none, run, n);
       const uint32_t f2 = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
                           (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u);
-      bst64(p.next, mk_rsrc(a.next + row, n * 8), on && p.next != nx0 ? o8 : kOOB);
-      bst64(p.pending, mk_rsrc(a.pending + row, n * 8), on && x.snapped ? o8 : kOOB);
-      bst8(f2, mk_rsrc(a.flags + row, n), on && f2 != fl ? lane : kOOB);
-      bst8(p.start, mk_rsrc(a.istart + row, n), on && p.start != st0 ? lane : kOOB);
-      bst8(p.count, mk_rsrc(a.icount + row, n), on && p.count != ct0 ? lane : kOOB);
+      const bool wn = on && p.next != nx[s], wp = on && x.snapped, wf = on && f2 != fl[s];
+      const bool ws = on && p.start != st[s], wc = on && p.count != ct[s];
+      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wp))
+        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wf)) bst8(f2, mk_rsrc(a.flags + row, n), wf ? lane : kOOB);
+      if (__builtin_amdgcn_ballot_w64(ws)) bst8(p.start, mk_rsrc(a.istart + row, n), ws ? lane : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wc)) bst8(p.count, mk_rsrc(a.icount + row, n), wc ? lane : kOOB);
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
     }

@@ -41,6 +41,7 @@ DOMINANT = {
     "confchange": ("void qe::k_confchange<5>", 1),
     "config4_repl_joint": ("void qe::k_repl_stream<6, true, true,", 2),
     "ready_collect": ("qe::k_collect_scatter", 1),
+    "progress_send": ("void qe::k_progress_send<5,", 1),
 }
 
 
