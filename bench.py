@@ -679,8 +679,8 @@ def run_workload(name, args, d, steps, warmup):
         rv = valu_roofline(name, kern_avg, units)
         if rv:
             extra["roofline_valu"] = rv
-    vi = vmem_issue(name, kern_avg, G if kind in ("elec", "elec_pvcq") else units)  # per group
-    if vi:
+    vi = vmem_issue(name, kern_avg, units) if kind not in ("elec", "elec_pvcq") else None
+    if vi:  # (the elections are VALU-bound: roofline_valu)
         extra["vmem_issue"] = vi
     return {**extra,
         "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
