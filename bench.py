@@ -498,10 +498,13 @@ def setup(name, G, S, kind, d, stats):
                 getattr(cs, k).copy_(pristine[k])
 
         # every input read once (op, count, 2 changes, last_index, 6 masks,
-        # auto_leave, S ids) and every output written once (result,
-        # new_progress, 6 masks, auto_leave, S ids, one initialised Progress
-        # row: match/next/pending + flags/istart/icount)
-        bpg = (1 + 1 + 2 * 9 + 8 + 6 + 1 + 8 * S) + (1 + 1 + 6 + 1 + 8 * S + 27)
+        # auto_leave, S ids) plus the outputs and the words the change
+        # rewrites, once (result, new_progress; inc, learner, is_learner and
+        # tracked change, out / learners_next / auto_leave do not; one slot ID;
+        # one initialised Progress row: match/next/pending + flags/istart/icount).
+        # The kernel writes a block's ID rows back whole (faster than 8-B
+        # scattered stores), so its traffic is 32 B/group above this.
+        bpg = (1 + 1 + 2 * 9 + 8 + 6 + 1 + 8 * S) + (1 + 1 + 4 + 8 + 27)
         import ctypes as C
         c_, x_, p_ = cs.struct(), ch.struct(), ps.struct()
         lib = engine._lib.lib()

@@ -160,9 +160,13 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
     if (a.new_progress) static_cast<MT *>(a.new_progress)[g] = 0;
     return false;
   }
-  auto ld = [&](const void *p) -> uint32_t { return static_cast<const MT *>(p)[g] & full; };
-  CCState c{ld(a.inc), ld(a.out), ld(a.lrn), ld(a.lnx), ld(a.isl), ld(a.trk),
-            a.auto_leave[g] != 0 ? 1u : 0u, 0u};
+  // raw words as loaded: a field whose new value equals them is not stored
+  const uint32_t r_inc = static_cast<const MT *>(a.inc)[g], r_out = static_cast<const MT *>(a.out)[g];
+  const uint32_t r_lrn = static_cast<const MT *>(a.lrn)[g], r_lnx = static_cast<const MT *>(a.lnx)[g];
+  const uint32_t r_isl = static_cast<const MT *>(a.isl)[g], r_trk = static_cast<const MT *>(a.trk)[g];
+  const uint32_t r_al = a.auto_leave[g];
+  CCState c{r_inc & full, r_out & full, r_lrn & full, r_lnx & full, r_isl & full, r_trk & full,
+            r_al != 0 ? 1u : 0u, 0u};
   uint64_t id0[kCCMax];
 #pragma unroll
   for (int s = 0; s < kCCMax; s++) id0[s] = id[s];
@@ -222,14 +226,19 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
     for (int s = 0; s < kCCMax; s++) id[s] = id0[s];
     return false;
   }
-  auto st = [&](void *p, uint32_t v) { static_cast<MT *>(p)[g] = static_cast<MT>(v); };
-  st(a.inc, c.inc);
-  st(a.out, c.out);
-  st(a.lrn, c.lrn);
-  st(a.lnx, c.lnx);
-  st(a.isl, c.isl & c.trk);
-  st(a.trk, c.trk);
-  a.auto_leave[g] = static_cast<uint8_t>(c.al);
+  // only the words the change rewrote (a wave none of whose lanes changes a
+  // field issues no store for it; in a Simple change out, LearnersNext and
+  // AutoLeave never change)
+  auto st = [&](void *p, uint32_t v, uint32_t raw) {
+    if (v != raw) static_cast<MT *>(p)[g] = static_cast<MT>(v);
+  };
+  st(a.inc, c.inc, r_inc);
+  st(a.out, c.out, r_out);
+  st(a.lrn, c.lrn, r_lrn);
+  st(a.lnx, c.lnx, r_lnx);
+  st(a.isl, c.isl & c.trk, r_isl);
+  st(a.trk, c.trk, r_trk);
+  if (c.al != r_al) a.auto_leave[g] = static_cast<uint8_t>(c.al);
 #pragma unroll
   for (int s = 0; s < S; s++) id[s] = ((c.trk >> s) & 1u) ? id[s] : 0;
   if (a.p_match && created) {
