@@ -333,7 +333,7 @@ def setup(name, G, S, kind, d, stats):
         return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
     if kind == "progress":
         # MaxInflightMsgs 8, MaxSizePerMsg = 16 entries, 4-term leader log
-        F, R, ME = 8, 4, 16
+        F, R, ME = 8, int(os.environ.get("QE_BENCH_RUNS", "4")), 16  # R: A/B knob only
         ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff, extras=("self_slot",),
                                   max_ents=ME)
         n = S * ps.stride

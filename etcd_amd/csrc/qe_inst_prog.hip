@@ -41,10 +41,15 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
                        dim3(kBlock), 0, st, a);
     return hip_status(hipGetLastError());
   }
-  // run table in registers: 4 runs cover the common leader log (one or two
-  // older terms before the current one); up to QE_MAX_LOG_RUNS otherwise
+  // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
+  // or two older terms before the current one); 8 keep the block's LDS at
+  // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);
+  // up to QE_MAX_LOG_RUNS otherwise
   if (kind == 2) return launch_progress_step<QE_MAX_LOG_RUNS, true>(a, masked, joint, st);
   if (a.R <= 4) return launch_progress_step<4, false>(a, masked, joint, st);
+#ifndef QE_NO_RM8  // A/B knob: without the 8-run kernel
+  if (a.R <= 8) return launch_progress_step<8, false>(a, masked, joint, st);
+#endif
   return launch_progress_step<QE_MAX_LOG_RUNS, false>(a, masked, joint, st);
 }
 

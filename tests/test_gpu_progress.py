@@ -160,6 +160,26 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras):
         assert_same(ps, pb)
 
 
+@pytest.mark.parametrize("R", [8, 9, 16])
+def test_progress_run_table_sizes(eng, R):
+    """Leader logs of up to QE_MAX_LOG_RUNS term runs: R = 8 is the largest
+    for the 8-run kernel, 9 and 16 take the 16-run one."""
+    rng = np.random.default_rng(500 + R)
+    G, S, F = 2500, 5, 8
+    pb = random_state(rng, G, S, F, R, (), EXTRAS, max_ents=int(rng.integers(0, 4)))
+    ps = to_device(eng, pb, (), EXTRAS)
+    for _ in range(3):
+        mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
+        msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+        stats = eng.stats_buffer(DEV)
+        eng.progress_step(ps, msgs, stats)
+        got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
+        assert_same(ps, pb)
+        assert_outputs(msgs, o, S)
+        np.testing.assert_array_equal(got, o.stats)
+
+
 def test_progress_long_rings_and_bcasts(eng):
     """F = 32 > the 8-entry prefetch (FreeLE continues from memory), small
     max_ents so the send loop fills rings, and every accept advancing the
