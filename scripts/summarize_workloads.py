@@ -93,8 +93,12 @@ def main():
             traffic[wl] = t
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+    # merge: a run that profiled some workloads replaces only their entries
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    merged = json.load(open(tp)) if os.path.exists(tp) else {}
+    merged.update(traffic)
+    with open(tp, "w") as f:
+        json.dump(merged, f, indent=1)
     for wl, t in traffic.items():
         print(f"{wl:20s} {t['hbm_bytes_per_launch'] / 1e9:8.3f} GB/launch  {t['rocprof_avg_ns'] / 1e6:.4f} ms"
               f"  VALU {t.get('valu_insts_per_launch', 0):.3e}")
