@@ -15,7 +15,7 @@ coalesced streams issue 128-B requests, so for the streaming kernels
 (k_cv_stream, k_repl_stream) the read bytes are 2 x FETCH_SIZE, calibrated
 in round 1 (2 x FETCH_SIZE = algorithmic reads within 0.01 %).  Kernels
 whose reads are mostly narrow or scattered (Progress step: 8-B Inflights
-rows, byte loads; confchange; election) issue 64-B requests and read
+rows, byte loads; election) issue 64-B requests and read
 FETCH_SIZE x 1 (checked for the Progress step against its access
 inventory).  usage: summarize_workloads.py <tag> [dir]
 """
@@ -38,7 +38,10 @@ DOMINANT = {
     "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 1),
     "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
     "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false>", 1),
-    "confchange": ("void qe::k_confchange<5>", 1),
+    # confchange: its ID block and u64 rows are read 512 B per instruction
+    # (128-B requests): 2 x FETCH_SIZE = 75.0 B/group = its algorithmic reads
+    # (r02h); round-2 summaries before r02h used 1
+    "confchange": ("void qe::k_confchange<5>", 2),
     "config4_repl_joint": ("void qe::k_repl_stream<6, true, true,", 2),
     "ready_collect": ("qe::k_collect_scatter", 1),
     "progress_send": ("void qe::k_progress_send<5,", 1),
