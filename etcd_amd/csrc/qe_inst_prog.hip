@@ -18,17 +18,18 @@ using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
 #define QE_CAT2(a, b) a##b
 #define QE_CAT(a, b) QE_CAT2(a, b)
 
-template <int RM, bool ACCT>
+template <int RM, bool ACCT, int WPB = kBlock / 64>
 static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
-  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  // the same waves as the 4-wave grid, in blocks of WPB waves
+  const uint64_t nb = static_cast<uint64_t>(grid_for((a.G + 63) / 64, 0, 1)) * ((kBlock / 64) / WPB);
+  const dim3 grid(static_cast<unsigned>(nb < 0x7FFFFFFFull ? nb : 0x7FFFFFFFull));
+  const dim3 blk(64 * WPB);
   if (joint)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT>), grid, dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, WPB>), grid, blk, 0, st, a);
   else if (masked)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT>), grid, dim3(kBlock), 0, st,
-                       a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, WPB>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT>), grid, dim3(kBlock), 0, st,
-                       a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, WPB>), grid, blk, 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -50,7 +51,11 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
 #ifndef QE_NO_RM8  // A/B knob: without the 8-run kernel
   if (a.R <= 8) return launch_progress_step<8, false>(a, masked, joint, st);
 #endif
-  return launch_progress_step<QE_MAX_LOG_RUNS, false>(a, masked, joint, st);
+#ifdef QE_RM16_WPB  // A/B knob: waves per block of the 16-run kernel
+  return launch_progress_step<QE_MAX_LOG_RUNS, false, QE_RM16_WPB>(a, masked, joint, st);
+#else
+  return launch_progress_step<QE_MAX_LOG_RUNS, false, 1>(a, masked, joint, st);
+#endif
 }
 
 }  // namespace qe

@@ -366,8 +366,10 @@ __device__ __forceinline__ void pb_ring(const PArgs &a, const uint64_t *rb, uint
 #define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
 #endif
 
-template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
+// WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
+// (21 KB at S = 5) would allow one 4-wave block per CU
+template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, int WPB = kBlock / 64>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
                           amdgpu_waves_per_eu(S <= 6 ? QE_PSTEP_WAVES : 1))) void
 k_progress_step(PArgs a) {
   constexpr int CH = kRingChunk;
@@ -376,17 +378,16 @@ k_progress_step(PArgs a) {
   Acct<ACCT> ac;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave =
-      static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
-      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+      static_cast<uint64_t>(blockIdx.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * WPB;
   const uint64_t ntiles = (a.G + 63) / 64;
   const uint32_t F = a.F;
   const bool row_ring = F <= CH;  // wave-uniform
   const uint32_t o8 = lane * 8;
   // per wave: Match and m.Index of every slot (phase 1's rows, read again in
   // phase 2) and the group's term runs once a slot needs them
-  __shared__ uint64_t l_mix[kBlock / 64][S][2][64];
-  __shared__ uint64_t l_run[kBlock / 64][RM][2][64];
+  __shared__ uint64_t l_mix[WPB][S][2][64];
+  __shared__ uint64_t l_run[WPB][RM][2][64];
   const uint32_t wv = threadIdx.x >> 6;
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
@@ -727,7 +728,7 @@ k_progress_step(PArgs a) {
   if (a.stats) {
     const int idx[P_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
                           QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
-    block_stats_add<P_N, kBlock>(cnt, idx, a.stats);
+    block_stats_add<P_N, 64 * WPB>(cnt, idx, a.stats);
   }
   acct_flush<ACCT>(ac, a.acct);
 }
