@@ -50,6 +50,11 @@ WORKLOADS = {
     "config3_joint_rot": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked, "
                           "per-group rotated slots) CommittedIndex+VoteResult",
                           1 << 27, 10, "joint_rot"),
+    "config3_joint_packed": ("128M groups x JointConfig 5+5 (S=10 slots, learners masked) "
+                             "built from per-group ConfStates (overlap uniform 0..5 per group, "
+                             "peer IDs in per-group rotated order) through the product packer "
+                             "(qe_pack_order shape bucketing + qe_pack_confstate, per 16M-group "
+                             "batch) CommittedIndex+VoteResult", 1 << 27, 10, "joint_packed"),
     "config4_repl": ("32M groups x 5 voters lockstep replication round (MaybeUpdate, "
                      "CommittedIndex, term-gated commit, ReadIndex quorum)", 1 << 25, 5, "repl"),
     "config4_repl_joint": ("32M groups x joint 5+5 over 6 slots (replacing one voter: "
@@ -200,17 +205,156 @@ class Dist:
 
 
 # ---------------------------------------------------------------------------
+# counter-based synthetic state: every value is a pure function of (seed,
+# GLOBAL group id, slot) through the engine's own generator (qe_gen_groups,
+# dist 1 = uniform 63-bit), so a rank's shard of a multi-rank run holds
+# exactly the groups a single process would hold at the same global ids
+# ---------------------------------------------------------------------------
+def counter_rows(G, S, seed, goff, dev):
+    """[S][stride] int64 tensor of 63-bit uniforms keyed by (seed, goff + g, s)."""
+    b = engine.SlotBatch(G, S, dev, masks=(), votes=False, group_offset=goff)
+    engine.gen_groups(b, seed, dist=1, p_absent=0)
+    return b.match
+
+
+def progress_round_state(ps, msgs, seed=0x5EED):
+    """The progress_step workload: 4 followers in StateReplicate (RecentActive)
+    with 0..F in-flight entries, a 4-term-run leader log, and one round of
+    messages -- 70 % MsgAppResp accepts, 10 % rejects, 10 % heartbeat
+    responses, 10 % none, no message from the leader's own slot 0."""
+    G, S, F, R = ps.G, ps.S, ps.F, ps.R
+    goff, dev, st = ps.group_offset, ps.device, ps.stride
+    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev)  # noqa: E731
+    base = (1 << 20) + u(1, 1)[:st] % ((1 << 40) - (1 << 20))
+    ps.match.copy_(base.repeat(S) + u(2) % 64)
+    ps.next.copy_(ps.match + 1 + u(3) % 4)
+    cnt = (u(4) % (F + 1)).to(torch.int32)
+    ps.peer.copy_(cnt * (1 << 16) + (1 | 8))  # StateReplicate, RecentActive, start 0
+    for k in range(F):  # entry-major rings: [S][F][stride]
+        ps.ibuf.view(S, F, st)[:, k, :] = ps.match.view(S, st) + 1 + 8 * k
+    ps.last_index.copy_(base[:G] + 128)
+    ps.term_start.copy_(base[:G])
+    ps.first_index.copy_(base[:G] - 64)
+    ps.committed.copy_(base[:G])
+    ps.self_slot.fill_(0)  # the leader's own Progress is slot 0
+    rf = ps.run_first.view(R, st)
+    for r in range(R):
+        rf[r].copy_(base - 65 + 40 * r)
+    ps.run_term.view(R, st).copy_(
+        torch.arange(1, R + 1, device=dev).repeat_interleave(st).view(R, st))
+    ps.run_count.fill_(R)
+    v = u(5) % 10
+    ty = torch.where(v < 7, 1, torch.where(v == 7, 2, torch.where(v == 8, 3, 0)))
+    ty.view(S, st)[0] = 0  # no message from the leader itself
+    msgs.type.copy_(ty.to(torch.uint8))
+    # acks stay within the leader's log: match + [0, 64] <= base + 127 < lastIndex
+    msgs.index.copy_(ps.match + u(6) % 65)
+    msgs.reject_hint.copy_(ps.match)
+    msgs.log_term.copy_(u(7) % 4)
+
+
+def psend_state(ps, seed=0x5E4D):
+    """The progress_send workload: followers in StateReplicate with room in
+    their Inflights (start 0..F-1, count 0..F-1), Next a little past Match."""
+    G, S, F = ps.G, ps.S, ps.F
+    goff, dev, st = ps.group_offset, ps.device, ps.stride
+    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev)  # noqa: E731
+    base = (1 << 20) + u(1, 1)[:st] % ((1 << 40) - (1 << 20))
+    ps.match.copy_(base.repeat(S) + u(2) % 64)
+    ps.next.copy_(ps.match + 1 + u(3) % 4)
+    start = (u(4) % F).to(torch.int32)
+    cnt = (u(5) % F).to(torch.int32)
+    ps.peer.copy_(cnt * (1 << 16) + start * (1 << 8) + (1 | 8))  # Replicate, RecentActive
+    ps.last_index.copy_(base[:G] + 128)
+    ps.first_index.copy_(base[:G] - 64)
+
+
+# ---------------------------------------------------------------------------
 # workload setup: returns (step_fn, bytes_per_unit, units_per_step, unit_name)
 # ---------------------------------------------------------------------------
+def joint_confstates(goff, n, dev, seed=0x5EED):
+    """ConfState CSR lists (raft.proto:115-130) of the config-3 shape for the
+    global group ids goff .. goff+n-1: Voters[0] = 5 voters, Voters[1] = 5
+    voters overlapping Voters[0] in o = 0..5 of them (uniform per group),
+    the o peers outside the union are learners -- S = 10 peers per group.
+    Peer IDs are gid * 16 + 1 + ((role + r) % 10) with a per-group rotation
+    r, so ascending-ID slot order interleaves the halves differently from
+    group to group.  (o, r) come from the engine's counter generator keyed
+    by the global group id; the lists are built on `dev` and copied to host
+    memory, where the packer reads them.  Returns (ConfStates, overlap)."""
+    from etcd_amd.packing import ConfStates
+    h = counter_rows(n, 1, seed, goff, dev)[:n]
+    o = h % 6
+    r = (h >> 8) % 10
+    base = (torch.arange(goff, goff + n, device=dev, dtype=torch.int64) * 16 + 1).view(n, 1)
+    k = torch.arange(10, device=dev)
+    rot = (k.view(1, 10) + k.view(10, 1)) % 10                     # rot[r][role]
+    outt = torch.stack([rot[:, 5 - ov:10 - ov] for ov in range(6)])  # [o][r][5]
+    lrn = torch.stack([(10 - ov + torch.arange(5, device=dev).view(1, 5) + k.view(10, 1)) % 10
+                       for ov in range(6)])                         # [o][r][5]
+    voters = (base + rot[r, :5]).reshape(-1)
+    outgoing = (base + outt[o, r]).reshape(-1)
+    learners = torch.masked_select(base + lrn[o, r], torch.arange(5, device=dev).view(1, 5) <
+                                   o.view(n, 1))
+    loff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    loff[1:] = torch.cumsum(o, 0)
+    off5 = torch.arange(n + 1, dtype=torch.int64, device=dev) * 5
+    host = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+    cs = ConfStates.from_csr(n, (host(voters), host(off5)), (host(outgoing), host(off5)),
+                             (host(learners), host(loff)))
+    return cs, o.cpu().numpy()
+
+
+def pack_joint_batches(b, goff, chunk=1 << 24):
+    """Build batch `b`'s masks through the product packer: per 16M-group
+    batch, ConfStates -> qe_pack_order (shape bucketing) -> qe_pack_confstate
+    with that order -> masks copied into HBM at the batch's positions.
+    Returns the device perm (packed position -> global group id - goff)."""
+    import ctypes as C
+    from etcd_amd import _lib
+    from etcd_amd.packing import _np_ptr
+    lib = _lib.lib()
+    G, S = b.G, b.S
+    perm_all = torch.empty(G, dtype=torch.int64, device=b.device)
+    md = np.uint16
+    for c0 in range(0, G, chunk):
+        n = min(chunk, G - c0)
+        cs, _ = joint_confstates(goff + c0, n, b.device)
+        perm = np.zeros(n, np.uint64)
+        nsh = C.c_uint64(0)
+        st = cs.struct()
+        engine.check("qe_pack_order", lib.qe_pack_order(C.byref(st), S, _np_ptr(perm),
+                                                         C.byref(nsh)))
+        cs.perm = perm
+        st = cs.struct()
+        inc, out, lrn = (np.zeros(n, md) for _ in range(3))
+        ids = np.empty(S * n, np.uint64)
+        nflag = C.c_uint64(0)
+        engine.check("qe_pack_confstate", lib.qe_pack_confstate(
+            C.byref(st), S, _np_ptr(inc), _np_ptr(out), _np_ptr(lrn), _np_ptr(ids), None,
+            C.byref(nflag)))
+        assert nflag.value == 0
+        for dst, a in ((b.inc, inc), (b.out, out), (b.learner, lrn)):
+            dst[c0:c0 + n].copy_(torch.from_numpy(a.view(np.int16)))
+        perm_all[c0:c0 + n].copy_(torch.from_numpy((perm + np.uint64(c0)).view(np.int64)))
+        del cs, ids
+    return perm_all
+
+
 def setup(name, G, S, kind, d, stats):
     goff = d.rank * G
-    if kind in ("majority", "joint", "joint_rot"):
+    if kind in ("majority", "joint", "joint_rot", "joint_packed"):
         masks = () if kind == "majority" else ("inc", "out", "learner")
         b = engine.SlotBatch(G, S, d.dev, masks=masks, group_offset=goff)
         if kind == "joint":
             engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5, mask_mode=2)
         elif kind == "joint_rot":
             engine.gen_groups(b, 0x5EED, n_inc=5, n_out=5, mask_mode=0)
+        elif kind == "joint_packed":
+            # masks through the packer; Match / votes from the generator at
+            # the packed positions (values do not depend on the layout)
+            pack_joint_batches(b, goff)
+            engine.gen_groups(b, 0x5EED, values_only=True)
         else:
             engine.gen_groups(b, 0x5EED)
         # BASELINE config 2/3 outputs: CommittedIndex + VoteResult per group
@@ -332,48 +476,19 @@ def setup(name, G, S, kind, d, stats):
         bpg = (8 + 1 + 1 + 1 + 1 + 1 + 8 + 1 + 1 + 1) / steps_per_launch
         return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
     if kind == "progress":
-        # MaxInflightMsgs 8, MaxSizePerMsg = 16 entries, 4-term leader log
         F, R, ME = 8, int(os.environ.get("QE_BENCH_RUNS", "4")), 16  # R: A/B knob only
         ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff, extras=("self_slot",),
                                   max_ents=ME)
-        n = S * ps.stride
-        gen = torch.Generator(device=d.dev).manual_seed(0x5EED + d.rank)
-        base = torch.randint(1 << 20, 1 << 40, (ps.stride,), device=d.dev, generator=gen)
-        ps.match.copy_((base.repeat(S) + torch.randint(0, 64, (n,), device=d.dev, generator=gen)))
-        ps.next.copy_(ps.match + 1 + torch.randint(0, 4, (n,), device=d.dev, generator=gen))
-        ps.flags.fill_(1 | 8)  # StateReplicate, RecentActive
-        ps.icount.copy_(torch.randint(0, F + 1, (n,), device=d.dev, generator=gen).to(torch.uint8))
-        for k in range(F):  # entry-major rings: [S][F][stride]
-            ps.ibuf.view(S, F, ps.stride)[:, k, :] = ps.match.view(S, ps.stride) + 1 + 8 * k
-        ps.last_index.copy_(base[:G] + 128)
-        ps.term_start.copy_(base[:G])
-        ps.first_index.copy_(base[:G] - 64)
-        ps.committed.copy_(base[:G])
-        ps.self_slot.fill_(0)  # the leader's own Progress is slot 0
-        rf = ps.run_first.view(R, ps.stride)
-        for r in range(R):
-            rf[r].copy_(base - 65 + 40 * r)
-        ps.run_term.view(R, ps.stride).copy_(
-            torch.arange(1, R + 1, device=d.dev).repeat_interleave(ps.stride).view(R, ps.stride))
-        ps.run_count.fill_(R)
         msgs = engine.PeerMsgs(ps)
         msgs.snap = msgs.timeout_now = None  # no snapshots / transfers in this workload
-        u = torch.rand(n, device=d.dev, generator=gen)
-        ty = torch.where(u < 0.7, 1, torch.where(u < 0.8, 2, torch.where(u < 0.9, 3, 0)))
-        ty.view(S, ps.stride)[0] = 0  # no message from the leader itself
-        msgs.type.copy_(ty.to(torch.uint8))
-        # acks stay within the leader's log: match + [0, 64] <= base + 127 < lastIndex
-        msgs.index.copy_(ps.match + torch.randint(0, 65, (n,), device=d.dev, generator=gen))
-        msgs.reject_hint.copy_(ps.match)
-        lt = torch.randint(0, 4, (n,), device=d.dev, generator=gen)
-        msgs.log_term.copy_(lt)
+        progress_round_state(ps, msgs)
         # Every timed launch steps the SAME fresh state with the same round
         # of messages: the mutable state is restored from a pristine copy
         # before each launch (outside the kernel's HIP events), so no launch
         # sees stale, already-applied duplicates.  The Inflights buffer needs
         # no restore: a round appends only into free ring entries, and the
         # live entries it reads are the restored (start, count) window.
-        mutable = ("match", "next", "pending", "flags", "istart", "icount", "committed")
+        mutable = ("match", "next", "pending", "peer", "committed")
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
         def prepare():
@@ -385,7 +500,9 @@ def setup(name, G, S, kind, d, stats):
         # message, the Progress fields each event needs, PendingSnapshot only
         # in StateSnapshot, the Inflights entries FreeLE examines, the
         # term-run table when findConflictByTerm runs; writes of changed
-        # fields, appended Inflights entries and the outputs), once each.
+        # fields, appended Inflights entries and the outputs), once each --
+        # the rules the oracle restates (tests/test_gpu_progress.py checks
+        # the two counts are equal on this workload's state).
         prepare()
         total = engine.progress_bytes_requested(ps, msgs)
         prepare()
@@ -407,21 +524,12 @@ def setup(name, G, S, kind, d, stats):
         # MsgApp of up to 16 entries (one ring append, OptimisticUpdate)
         F, ME = 8, 16
         ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, max_ents=ME)
-        n = S * ps.stride
-        gen = torch.Generator(device=d.dev).manual_seed(0x5E4D + d.rank)
-        base = torch.randint(1 << 20, 1 << 40, (ps.stride,), device=d.dev, generator=gen)
-        ps.match.copy_(base.repeat(S) + torch.randint(0, 64, (n,), device=d.dev, generator=gen))
-        ps.next.copy_(ps.match + 1 + torch.randint(0, 4, (n,), device=d.dev, generator=gen))
-        ps.flags.fill_(1 | 8)  # StateReplicate, RecentActive
-        ps.istart.copy_(torch.randint(0, F, (n,), device=d.dev, generator=gen).to(torch.uint8))
-        ps.icount.copy_(torch.randint(0, F, (n,), device=d.dev, generator=gen).to(torch.uint8))
-        ps.last_index.copy_(base[:G] + 128)
-        ps.first_index.copy_(base[:G] - 64)
+        psend_state(ps)
         full = (1 << S) - 1
         want = torch.full((G,), full & ~1, dtype=torch.uint8, device=d.dev)  # not the leader
         sent = torch.zeros(G, dtype=torch.uint8, device=d.dev)
         snap = torch.zeros(G, dtype=torch.uint8, device=d.dev)
-        mutable = ("next", "icount")
+        mutable = ("next", "peer")
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
         def prepare():
@@ -435,15 +543,14 @@ def setup(name, G, S, kind, d, stats):
 
         def step():
             engine.check("qe_progress_send", lib.qe_progress_send(
-                C.byref(p_), engine._ptr(want), 0, ME, engine._ptr(sent), engine._ptr(snap),
-                stream))
+                C.byref(p_), engine._ptr(want), 0, engine._ptr(sent), engine._ptr(snap), stream))
 
         # per group: want mask, firstIndex/lastIndex read, sent/snap masks
-        # written; per wanted peer Next, flags, Inflights start/count read,
-        # Next, count and the appended entry written (start and flags do not
-        # change): 1 + 16 + 2 + 4 * (11 + 17) = 131 B
+        # written; per wanted peer Next and the packed word read, Next, the
+        # word (count changes) and the appended entry written:
+        # 1 + 16 + 2 + 4 * (12 + 20) = 147 B
         nw = bin(full & ~1).count("1")
-        bpg = 1 + 16 + 2 + nw * (11 + 17)
+        bpg = 1 + 16 + 2 + nw * (12 + 20)
         return step, bpg, G, "group-bcasts", {"ps": ps, "prepare": prepare,
                                               "t": (want, sent, snap)}
     if kind == "collect":
@@ -458,7 +565,8 @@ def setup(name, G, S, kind, d, stats):
         vals = torch.empty(G, dtype=torch.int64, device=d.dev)
         count = torch.empty(1, dtype=torch.int64, device=d.dev)
         stream = engine._stream(d.dev)
-        args_ = [G, goff] + [engine._ptr(t) for t in (flags, values, groups, vals, count, scratch)]
+        args_ = [G, goff, None] + [engine._ptr(t) for t in (flags, values, groups, vals, count,
+                                                             scratch)]
 
         def step():
             engine.check("qe_collect", lib.qe_collect(*args_, stream))
@@ -475,8 +583,8 @@ def setup(name, G, S, kind, d, stats):
         ps = engine.ProgressState(G, S, 1, 1, d.dev)
         ch = engine.ConfChanges(G, S, 2, d.dev)
         gid = torch.arange(G, device=d.dev, dtype=torch.int64) + goff
-        ids = gid.view(G, 1) * 8 + torch.arange(1, S + 1, device=d.dev).view(1, S)
-        ids[:, 4] = 0  # slot 4 free
+        ids = gid.view(1, G) * 8 + torch.arange(1, S + 1, device=d.dev).view(S, 1)  # [S][G]
+        ids[4] = 0  # slot 4 free
         cs.slot_ids.copy_(ids.reshape(-1))
         cs.inc.fill_(0b00111)
         cs.learner.fill_(0b01000)
@@ -498,13 +606,12 @@ def setup(name, G, S, kind, d, stats):
                 getattr(cs, k).copy_(pristine[k])
 
         # every input read once (op, count, 2 changes, last_index, 6 masks,
-        # auto_leave, S ids) plus the outputs and the words the change
-        # rewrites, once (result, new_progress; inc, learner, is_learner and
-        # tracked change, out / learners_next / auto_leave do not; one slot ID;
-        # one initialised Progress row: match/next/pending + flags/istart/icount).
-        # The kernel writes a block's ID rows back whole (faster than 8-B
-        # scattered stores), so its traffic is 32 B/group above this.
-        bpg = (1 + 1 + 2 * 9 + 8 + 6 + 1 + 8 * S) + (1 + 1 + 4 + 8 + 27)
+        # auto_leave, the 4 tracked slots' ids) plus the outputs and the words
+        # the change rewrites, once (result, new_progress; inc, learner,
+        # is_learner and tracked change, out / learners_next / auto_leave do
+        # not; one slot ID -- its own [S][G] row, ABI 3; one initialised
+        # Progress row: match/next/pending + the packed word).
+        bpg = (1 + 1 + 2 * 9 + 8 + 6 + 1 + 8 * 4) + (1 + 1 + 4 + 8 + 28)
         import ctypes as C
         c_, x_, p_ = cs.struct(), ch.struct(), ps.struct()
         lib = engine._lib.lib()
@@ -834,7 +941,7 @@ def main():
     if d.rank == 0:
         desc, G, S, kind = WORKLOADS[args.workload]
         traffic = load_traffic(args.workload)
-        majority_like = kind in ("majority", "joint", "joint_rot")
+        majority_like = kind in ("majority", "joint", "joint_rot", "joint_packed")
         vs = None
         if cpu is not None and majority_like:
             vs = main_res["value"] / cpu["value"]

@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 2
+QE_ABI_VERSION = 3
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -93,18 +93,17 @@ class QeConfStateCSR(C.Structure):
     _fields_ = [("num_groups", u64), ("voters", vp), ("voters_off", vp),
                 ("voters_outgoing", vp), ("outgoing_off", vp), ("learners", vp),
                 ("learners_off", vp), ("learners_next", vp), ("learners_next_off", vp),
-                ("auto_leave", vp)]
+                ("auto_leave", vp), ("perm", vp)]
 
 
 class QeProgress(C.Structure):
     _fields_ = [
         ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("inflight_cap", u32),
-        ("stride", u64), ("match", vp), ("next", vp), ("pending_snapshot", vp), ("flags", vp),
-        ("infl_start", vp), ("infl_count", vp), ("infl_buf", vp), ("committed", vp),
+        ("stride", u64), ("match", vp), ("next", vp), ("pending_snapshot", vp), ("peer", vp),
+        ("infl_buf", vp), ("committed", vp),
         ("term_start", vp), ("first_index", vp), ("last_index", vp), ("log_runs", u32),
         ("reserved", u32), ("run_first", vp), ("run_term", vp), ("run_count", vp),
         ("inc_mask", vp), ("out_mask", vp),
-        # ABI 2
         ("tracked", vp), ("self_slot", vp), ("lead_transferee", vp), ("snap_index", vp),
         ("max_ents", u32), ("reserved2", u32),
     ]
@@ -113,11 +112,13 @@ class QeProgress(C.Structure):
 class QePeerMsgs(C.Structure):
     _fields_ = [("type", vp), ("index", vp), ("reject_hint", vp), ("log_term", vp),
                 ("sent", vp), ("bcast", vp), ("snap", vp), ("timeout_now", vp),
-                ("msg_count", vp), ("msg_index", vp), ("bytes_requested", vp)]
+                ("msg_count", vp), ("msg_index", vp), ("bytes_requested", vp),
+                ("read_acks", vp), ("read_ctx", vp), ("read_ok", vp)]
 
 
 QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
 QE_PF_STATE, QE_PF_PROBE_SENT, QE_PF_RECENT_ACTIVE = 3, 4, 8
+QE_PW_START_SHIFT, QE_PW_COUNT_SHIFT = 8, 16
 QE_MSG_NONE, QE_MSG_APP_RESP, QE_MSG_APP_RESP_REJECT, QE_MSG_HEARTBEAT_RESP = 0, 1, 2, 3
 QE_MSG_SNAP_STATUS, QE_MSG_SNAP_STATUS_REJECT, QE_MSG_UNREACHABLE = 4, 5, 6
 QE_MAX_INFLIGHT = 255
@@ -166,17 +167,19 @@ PROTOTYPES = {
                                     vp, vp]),
     "qe_stats_reduce": (C.c_int, [vp, vp, vp]),
     "qe_collect_scratch_bytes": (C.c_size_t, [u64]),
-    "qe_collect": (C.c_int, [u64, u64, vp, vp, vp, vp, vp, vp, vp]),
+    "qe_collect": (C.c_int, [u64, u64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "qe_gen_groups": (C.c_int, [C.POINTER(QeGroups), C.POINTER(QeGenParams), vp]),
     "qe_apply_append_resps": (C.c_int, [u64, u32, u64, vp, vp, u64, vp, vp, vp, vp, vp]),
     "qe_pack_confstate": (C.c_int, [C.POINTER(QeConfStateCSR), u32, vp, vp, vp, vp, vp, vp]),
     "qe_pack_conf": (C.c_int, [C.POINTER(QeConfStateCSR), C.POINTER(QeConf), vp, vp]),
-    "qe_pack_match": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, u64, vp]),
-    "qe_pack_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp]),
+    "qe_pack_order": (C.c_int, [C.POINTER(QeConfStateCSR), u32, vp, vp]),
+    "qe_pack_match": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp, u64, vp]),
+    "qe_pack_votes": (C.c_int, [u64, u32, vp, vp, vp, vp, vp, vp, vp]),
     "qe_slot_lookup": (C.c_int, [u64, u32, vp, u64, vp, vp, vp]),
     "qe_pack_threads": (C.c_int, [C.c_int]),
     "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
-    "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, u32, vp, vp, vp]),
+    "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp]),
+    "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),
                                 C.POINTER(QeProgress), vp]),
     "qe_comm_id_bytes": (C.c_size_t, []),

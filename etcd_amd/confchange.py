@@ -119,7 +119,7 @@ def ChangeBatch(changers, ops, ccs, device=None):
         for k, cc in enumerate(ccs[g]):
             typ[k, g], node[k, g] = cc.Type, cc.NodeID
         li[g] = c.LastIndex
-    cs.slot_ids.copy_(torch.from_numpy(ids.reshape(-1).view(np.int64)))
+    cs.slot_ids.copy_(torch.from_numpy(np.ascontiguousarray(ids.T).reshape(-1).view(np.int64)))
     for k, v in masks.items():
         a = v.astype(md)
         getattr(cs, k).copy_(torch.from_numpy(a.view(np.int16) if md == np.uint16 else a))

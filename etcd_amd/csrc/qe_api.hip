@@ -373,9 +373,8 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   if (p->num_groups && p->stride < p->num_groups) return QE_EINVAL;
   if (p->out_mask && !p->inc_mask) return QE_EINVAL;
   if (p->num_groups &&
-      (!p->match || !p->next || !p->pending_snapshot || !p->flags || !p->infl_start ||
-       !p->infl_count || !p->infl_buf || !p->committed || !p->term_start || !p->first_index ||
-       !p->last_index))
+      (!p->match || !p->next || !p->pending_snapshot || !p->peer || !p->infl_buf ||
+       !p->committed || !p->term_start || !p->first_index || !p->last_index))
     return QE_EINVAL;
   if (p->num_groups && p->log_runs && (!p->run_first || !p->run_term || !p->run_count))
     return QE_EINVAL;
@@ -391,9 +390,7 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.match = p->match;
   a.next = p->next;
   a.pending = p->pending_snapshot;
-  a.flags = p->flags;
-  a.istart = p->infl_start;
-  a.icount = p->infl_count;
+  a.pw = p->peer;
   a.ibuf = p->infl_buf;
   a.committed = p->committed;
   a.term_start = p->term_start;
@@ -432,6 +429,9 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
   a.msg_count = m->msg_count;
   a.msg_index = m->msg_index;
   a.acct = m->bytes_requested;
+  a.read_acks = m->read_acks;
+  a.read_ctx = m->read_ctx;
+  a.read_ok = m->read_ok;
   a.stats = stats;
   const int kind = m->bytes_requested ? 2 : 0;
   return dispatch_progress(p->num_slots, a, kind, p->inc_mask != nullptr, p->out_mask != nullptr,
@@ -439,7 +439,7 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
 }
 
 int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
-                     uint32_t max_ents, void *sent, void *snap, void *stream) {
+                     void *sent, void *snap, void *stream) {
   PArgs a;
   int rc = progress_args(p, a);
   if (rc) return rc;
@@ -447,10 +447,32 @@ int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_em
   if (!want) return QE_EINVAL;
   a.want = want;
   a.send_if_empty = send_if_empty;
-  a.max_ents = max_ents;
   a.sent = sent;
   a.snap = snap;
   return dispatch_progress(p->num_slots, a, 1, false, false, static_cast<hipStream_t>(stream));
+}
+
+int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stats,
+                    void *stream) {
+  if (!p) return QE_EINVAL;
+  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
+    return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (p->stride < p->num_groups || !p->peer) return QE_EINVAL;
+  if (p->out_mask && !p->inc_mask) return QE_EINVAL;
+  PArgs a{};
+  a.G = p->num_groups;
+  a.goff = p->group_offset;
+  a.stride = p->stride;
+  a.pw = p->peer;
+  a.inc = p->inc_mask;
+  a.out = p->out_mask;
+  a.tracked = p->tracked;
+  a.self_slot = p->self_slot;
+  a.qactive = quorum_active;
+  a.stats = stats;
+  return dispatch_progress(p->num_slots, a, 3, p->inc_mask != nullptr, p->out_mask != nullptr,
+                           static_cast<hipStream_t>(stream));
 }
 
 int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress *p,
@@ -488,16 +510,12 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
     if (p->num_groups != c->num_groups || p->num_slots != c->num_slots ||
         p->stride < p->num_groups)
       return QE_EINVAL;
-    if (!p->match || !p->next || !p->pending_snapshot || !p->flags || !p->infl_start ||
-        !p->infl_count)
-      return QE_EINVAL;
+    if (!p->match || !p->next || !p->pending_snapshot || !p->peer) return QE_EINVAL;
     a.pstride = p->stride;
     a.p_match = p->match;
     a.p_next = p->next;
     a.p_pending = p->pending_snapshot;
-    a.p_flags = p->flags;
-    a.p_istart = p->infl_start;
-    a.p_icount = p->infl_count;
+    a.p_pw = p->peer;
   }
   const dim3 grid(static_cast<unsigned>((a.G + kBlock - 1) / kBlock));
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -517,9 +535,9 @@ size_t qe_collect_scratch_bytes(uint64_t num_groups) {
   return static_cast<size_t>(nb * (sizeof(uint32_t) + sizeof(uint64_t)) + 64);
 }
 
-int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint8_t *flags,
-               const uint64_t *values, uint64_t *out_groups, uint64_t *out_values,
-               uint64_t *out_count, void *scratch, void *stream) {
+int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint64_t *perm,
+               const uint8_t *flags, const uint64_t *values, uint64_t *out_groups,
+               uint64_t *out_values, uint64_t *out_count, void *scratch, void *stream) {
   if (!out_count || (num_groups && (!flags || !scratch))) return QE_EINVAL;
   if (out_values && !values) return QE_EINVAL;
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -536,7 +554,7 @@ int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint8_t *flags,
                      num_groups, vec, counts);
   hipLaunchKernelGGL(k_collect_scan, dim3(1), dim3(1024), 0, st, counts, nb, offsets, out_count);
   hipLaunchKernelGGL(k_collect_scatter, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, st, flags,
-                     num_groups, vec, group_offset, values, offsets, out_groups, out_values);
+                     num_groups, vec, group_offset, perm, values, offsets, out_groups, out_values);
   return hip_status(hipGetLastError());
 }
 

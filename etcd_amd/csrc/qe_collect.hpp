@@ -108,6 +108,7 @@ __global__ __launch_bounds__(1024) void k_collect_scan(const uint32_t *counts, u
 // waves' counts through LDS for the block), not 16-entry runs per thread.
 __global__ __launch_bounds__(kBlock) void k_collect_scatter(const uint8_t *flags, uint64_t G,
                                                             bool vec, uint64_t goff,
+                                                            const uint64_t *perm,
                                                             const uint64_t *values,
                                                             const uint64_t *offsets,
                                                             uint64_t *out_groups,
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_collect_scatter(const uint8_t *flags
     if (f[r]) {
       const uint64_t g = base + r * kBlock + tid;
       const uint64_t p = pos + before + rank[r];
-      if (out_groups) out_groups[p] = goff + g;
+      if (out_groups) out_groups[p] = goff + (perm ? perm[g] : g);
       if (out_values) out_values[p] = values[g];
     }
     pos += all;

@@ -28,7 +28,7 @@ struct CCArgs {
   void *new_progress;
   // optional Progress rows to initialise ([S][pstride])
   uint64_t *p_match, *p_next, *p_pending;
-  uint8_t *p_flags, *p_istart, *p_icount;
+  uint32_t *p_pw;
 };
 
 struct CCState {
@@ -148,17 +148,20 @@ __device__ __forceinline__ int cc_apply(const CCArgs &a, uint64_t g, CCState &c,
   return c.inc == 0 ? QE_CC_ERR_REMOVED_ALL : QE_CC_OK;
 }
 
-// One group's change.  `id` holds the group's slot IDs on entry and the
-// IDs to store on exit; returns true when the group's state changed.
+// One group's change (one lane).  Slot IDs are ID-major, [S][G]: the
+// group's tracked IDs are loaded row by row (consecutive lanes, consecutive
+// addresses), and only the IDs the change rewrites are stored -- a created
+// slot's new ID, a removed slot's 0 -- so a change touches one ID row, not
+// the group's whole ID block.
 template <int S>
-__device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (&id)[kCCMax]) {
+__device__ __forceinline__ void cc_group(const CCArgs &a, uint64_t g) {
   using MT = typename std::conditional<(S <= 8), uint8_t, uint16_t>::type;
   constexpr uint32_t full = (1u << S) - 1u;
   const uint32_t op = a.op[g];
   if (op == QE_CC_OP_NONE) {
     a.result[g] = QE_CC_OK;
     if (a.new_progress) static_cast<MT *>(a.new_progress)[g] = 0;
-    return false;
+    return;
   }
   // raw words as loaded: a field whose new value equals them is not stored
   const uint32_t r_inc = static_cast<const MT *>(a.inc)[g], r_out = static_cast<const MT *>(a.out)[g];
@@ -167,10 +170,15 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
   const uint32_t r_al = a.auto_leave[g];
   CCState c{r_inc & full, r_out & full, r_lrn & full, r_lnx & full, r_isl & full, r_trk & full,
             r_al != 0 ? 1u : 0u, 0u};
+  // the tracked slots' IDs (an untracked slot's ID is ignored)
+  uint64_t id[kCCMax];
+#pragma unroll
+  for (int s = 0; s < kCCMax; s++)
+    id[s] = (s < S && ((c.trk >> s) & 1u)) ? a.ids[static_cast<uint64_t>(s) * a.G + g] : 0ull;
   uint64_t id0[kCCMax];
 #pragma unroll
   for (int s = 0; s < kCCMax; s++) id0[s] = id[s];
-  const uint32_t inc0 = c.inc;
+  const uint32_t inc0 = c.inc, trk0 = c.trk;
   int rc = cc_invariants<S>(c, id) ? QE_CC_OK : QE_CC_ERR_INVARIANT;  // checkAndCopy
   if (rc == QE_CC_OK) {
     if (op == QE_CC_OP_SIMPLE) {  // :130-147
@@ -221,11 +229,7 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
   a.result[g] = static_cast<uint8_t>(rc);
   const uint32_t created = rc == QE_CC_OK ? (c.newp & c.trk) : 0u;
   if (a.new_progress) static_cast<MT *>(a.new_progress)[g] = static_cast<MT>(created);
-  if (rc != QE_CC_OK) {  // a failed change keeps the group's state
-#pragma unroll
-    for (int s = 0; s < kCCMax; s++) id[s] = id0[s];
-    return false;
-  }
+  if (rc != QE_CC_OK) return;  // a failed change keeps the group's state
   // only the words the change rewrote (a wave none of whose lanes changes a
   // field issues no store for it; in a Simple change out, LearnersNext and
   // AutoLeave never change)
@@ -239,8 +243,12 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
   st(a.isl, c.isl & c.trk, r_isl);
   st(a.trk, c.trk, r_trk);
   if (c.al != r_al) a.auto_leave[g] = static_cast<uint8_t>(c.al);
+  // a slot the change tracks or untracks: its new ID (0 when removed)
+  const uint32_t flip = (c.trk ^ trk0) & full;
 #pragma unroll
-  for (int s = 0; s < S; s++) id[s] = ((c.trk >> s) & 1u) ? id[s] : 0;
+  for (int s = 0; s < S; s++)
+    if ((flip >> s) & 1u)
+      a.ids[static_cast<uint64_t>(s) * a.G + g] = ((c.trk >> s) & 1u) ? id[s] : 0ull;
   if (a.p_match && created) {
     const uint64_t li = a.last_index[g];
     for (int s = 0; s < S; s++) {
@@ -249,43 +257,15 @@ __device__ __forceinline__ bool cc_group(const CCArgs &a, uint64_t g, uint64_t (
       a.p_match[r] = 0;
       a.p_next[r] = li;
       a.p_pending[r] = 0;
-      a.p_flags[r] = QE_PR_PROBE | QE_PF_RECENT_ACTIVE;
-      a.p_istart[r] = 0;
-      a.p_icount[r] = 0;
+      a.p_pw[r] = QE_PR_PROBE | QE_PF_RECENT_ACTIVE;  // empty Inflights
     }
   }
-  return true;
 }
 
-// The slot IDs are [G][S] (the packer's layout): a lane's S IDs sit S*8
-// bytes apart from its neighbour's.  The block stages its kBlock*S IDs
-// through LDS with consecutive-lane 8-B loads and stores (every wave
-// instruction moves one contiguous 512 B), and lanes read and write their
-// own S IDs in LDS.  IDs go back to HBM only from blocks where some group's
-// change succeeded.
 template <int S>
 __global__ __launch_bounds__(kBlock) void k_confchange(CCArgs a) {
-  __shared__ uint64_t sid[kBlock * S];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t gb = static_cast<uint64_t>(blockIdx.x) * kBlock;
-  const uint64_t left = a.G - gb;
-  const uint32_t nb = left < kBlock ? static_cast<uint32_t>(left) : kBlock;
-  const uint32_t nw = nb * S;
-  uint64_t *blk = a.ids + gb * S;
-  for (uint32_t i = tid; i < nw; i += kBlock) sid[i] = __builtin_nontemporal_load(blk + i);
-  __syncthreads();
-  uint64_t id[kCCMax];
-#pragma unroll
-  for (int s = 0; s < kCCMax; s++) id[s] = (s < S && tid < nb) ? sid[tid * S + s] : 0;
-  bool changed = false;
-  if (tid < nb) changed = cc_group<S>(a, gb + tid, id);
-  if (changed) {
-#pragma unroll
-    for (int s = 0; s < S; s++) sid[tid * S + s] = id[s];
-  }
-  if (__syncthreads_or(changed)) {
-    for (uint32_t i = tid; i < nw; i += kBlock) __builtin_nontemporal_store(sid[i], blk + i);
-  }
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (g < a.G) cc_group<S>(a, g);
 }
 
 }  // namespace qe

@@ -495,7 +495,7 @@ std::vector<Result> ChangeBatch(const std::vector<const Changer *> &changers,
     uint32_t s = 0;
     for (const auto &kv : t.Progress) {
       const uint64_t id = kv.first, b = 1u << s;
-      memcpy(&h[o_ids + 8 * (g * S + s)], &id, 8);
+      memcpy(&h[o_ids + 8 * (s * G + g)], &id, 8);  // ID-major [S][G]
       m[0] |= t.Voters.c[0].ids.count(id) ? b : 0;
       m[1] |= t.Voters.c[1].ids.count(id) ? b : 0;
       m[2] |= t.Learners.count(id) ? b : 0;
@@ -570,7 +570,7 @@ std::vector<Result> ChangeBatch(const std::vector<const Changer *> &changers,
     for (uint32_t s = 0; s < S; s++) {
       if (((trk >> s) & 1u) == 0) continue;
       uint64_t id;
-      memcpy(&id, &h[o_ids + 8 * (g * S + s)], 8);
+      memcpy(&id, &h[o_ids + 8 * (s * G + g)], 8);
       if ((inc >> s) & 1u) r.Config.Voters.c[0].ids.insert(id);
       if ((outm >> s) & 1u) r.Config.Voters.c[1].ids.insert(id);
       if ((lrn >> s) & 1u) r.Config.Learners.insert(id);

@@ -33,15 +33,40 @@ static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStre
   return hip_status(hipGetLastError());
 }
 
+// qe_progress_send: chunks of up to kSendTPW tiles per wave (as the stream
+// commit kernel: a batch too small to give every CU 32 waves at that chunk
+// gets shorter chunks, >= 2 so the two register sets still overlap)
+static int launch_progress_send(PArgs a, hipStream_t st) {
+  const uint64_t tiles = (a.G + 63) / 64;
+  const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
+  uint64_t chunk = g_tiles_per_wave > 0 ? static_cast<uint64_t>(g_tiles_per_wave)
+                                        : (tiles + waves - 1) / waves;
+  if (chunk < 2) chunk = 2;
+  if (chunk > static_cast<uint64_t>(kSendTPW)) chunk = kSendTPW;
+  a.chunk = static_cast<uint32_t>(chunk);
+  const uint64_t per_block = (kBlock / 64) * chunk;
+  const uint64_t blocks = (tiles + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+                     0, st, a);
+  return hip_status(hipGetLastError());
+}
+
+static int launch_check_quorum(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  if (joint) hipLaunchKernelGGL((k_check_quorum<S, MT, true, true>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_check_quorum<S, MT, true, false>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_check_quorum<S, MT, false, false>), grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 // kind 0: qe_progress_step, 1: qe_progress_send, 2: qe_progress_step with
-// byte accounting (instrumented variant, measurement only)
+// byte accounting (instrumented variant, measurement only), 3:
+// qe_check_quorum
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
-  if (kind == 1) {
-    hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(grid_for((a.G + 63) / 64, 0, 1)),
-                       dim3(kBlock), 0, st, a);
-    return hip_status(hipGetLastError());
-  }
+  if (kind == 1) return launch_progress_send(a, st);
+  if (kind == 3) return launch_check_quorum(a, masked, joint, st);
   // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
   // or two older terms before the current one); 8 keep the block's LDS at
   // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);

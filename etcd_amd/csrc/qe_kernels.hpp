@@ -681,7 +681,7 @@ struct PArgs {
   uint64_t G, goff, stride;
   uint32_t F, R;
   uint64_t *match, *next, *pending;
-  uint8_t *flags, *istart, *icount;
+  uint32_t *pw;  // [S][stride] packed per-peer words (QE_PW_*)
   uint64_t *ibuf;
   uint64_t *committed;
   const uint64_t *term_start, *first_index, *last_index, *snap_index;
@@ -696,10 +696,16 @@ struct PArgs {
   void *sent, *snap, *tnow;
   uint8_t *bcast, *msg_count;
   uint64_t *msg_index, *acct;
+  void *read_acks;
+  const void *read_ctx;
+  uint8_t *read_ok;
   uint64_t *stats;
   // send
   const void *want;
   uint32_t send_if_empty;
+  uint32_t chunk;  // k_progress_send: tiles per wave chunk
+  // check quorum
+  uint8_t *qactive;
 };
 
 struct PR {
@@ -707,6 +713,20 @@ struct PR {
   uint32_t state, probe_sent, recent_active, start, count;
   uint32_t reset;  // ResetState ran: PendingSnapshot must be written back
 };
+
+// The packed per-peer word (include/etcd_quorum.h QE_PW_*).
+__device__ __forceinline__ void pr_unpack(PR &p, uint32_t w) {
+  p.state = w & QE_PF_STATE;
+  p.probe_sent = (w >> 2) & 1u;
+  p.recent_active = (w >> 3) & 1u;
+  p.start = (w >> QE_PW_START_SHIFT) & 0xFFu;
+  p.count = (w >> QE_PW_COUNT_SHIFT) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t pr_pack(const PR &p) {
+  return p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
+         (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u) | (p.start << QE_PW_START_SHIFT) |
+         (p.count << QE_PW_COUNT_SHIFT);
+}
 
 __device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:84-90
   p.reset = 1;
@@ -769,7 +789,7 @@ __device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t i
   else return joint_committed<S>(v, inc, out);
 }
 
-enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_CSUM, P_N };
+enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_READ, P_CSUM, P_N };
 
 // k_progress_step: qe_progress.hpp
 

@@ -7,7 +7,16 @@
 // Slot order per group: JointConfig.IDs() (raft/quorum/joint.go:30-38) in
 // ascending ID order, then learners in ascending ID order.  Every quorum
 // function is order-free, so this choice is free; ascending order makes the
-// packing deterministic.  Work is split over std::threads by group range.
+// packing deterministic.  Slot IDs are stored ID-major, [S][G] (slot s of
+// packed group i at slot_ids[s*G + i]), so a kernel that rewrites one slot's
+// ID touches one row.
+//
+// Group order (ABI 3): packed position i holds the caller's group perm[i]
+// (identity when cs->perm is NULL).  qe_pack_order computes the
+// shape-bucketed order -- groups sorted by configuration shape, so the 64
+// groups of a wave have their voters in the same low slots and the joint
+// commit kernel fetches only those slot rows.  Work is split
+// over std::threads by group range.
 #include <stdint.h>
 #include <string.h>
 
@@ -22,23 +31,39 @@ namespace {
 
 int g_pack_threads = 0;  // 0 = hardware_concurrency (capped at 16)
 
-template <typename F>
-void parallel_for(uint64_t n, F f) {
+// Contiguous ranges of [0, n), one per worker thread (deterministic for a
+// given n and thread setting, so two passes see the same split).
+std::vector<std::pair<uint64_t, uint64_t>> ranges_of(uint64_t n) {
   unsigned nt = g_pack_threads > 0 ? static_cast<unsigned>(g_pack_threads)
                                    : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  if (n < 4096 || nt <= 1) {
-    f(0, n);
-    return;
-  }
+  if (n < 4096) nt = 1;
   if (nt > n / 1024) nt = static_cast<unsigned>(std::max<uint64_t>(1, n / 1024));
-  std::vector<std::thread> th;
+  std::vector<std::pair<uint64_t, uint64_t>> r;
   const uint64_t chunk = (n + nt - 1) / nt;
   for (unsigned t = 0; t < nt; t++) {
     const uint64_t b = t * chunk, e = std::min(n, b + chunk);
     if (b >= e) break;
-    th.emplace_back([=] { f(b, e); });
+    r.emplace_back(b, e);
   }
+  if (r.empty()) r.emplace_back(0, n);
+  return r;
+}
+
+// f(thread_index, begin, end) over the ranges of ranges_of(n)
+template <typename F>
+void parallel_ranges(const std::vector<std::pair<uint64_t, uint64_t>> &r, F f) {
+  if (r.size() == 1) {
+    f(0u, r[0].first, r[0].second);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < r.size(); t++) th.emplace_back([&, t] { f(t, r[t].first, r[t].second); });
   for (auto &x : th) x.join();
+}
+
+template <typename F>
+void parallel_for(uint64_t n, F f) {
+  parallel_ranges(ranges_of(n), [&](unsigned, uint64_t b, uint64_t e) { f(b, e); });
 }
 
 inline void put_mask(void *p, uint32_t mb, uint64_t g, uint32_t v) {
@@ -53,12 +78,27 @@ inline int slot_of(const uint64_t *ids, uint32_t S, uint64_t id) {
   return -1;
 }
 
+// The S slot IDs of packed group i from the ID-major block.
+inline void gather_ids(const uint64_t *slot_ids, uint64_t G, uint32_t S, uint64_t i,
+                       uint64_t *ids) {
+  for (uint32_t s = 0; s < S; s++) ids[s] = slot_ids[s * G + i];
+}
+
 struct List {
   const uint64_t *ids;
   const uint64_t *off;
   bool has(uint64_t) const { return ids && off; }
   const uint64_t *begin(uint64_t g) const { return ids + off[g]; }
   const uint64_t *end(uint64_t g) const { return ids + off[g + 1]; }
+};
+
+struct Lists {
+  List voters, outgoing, learners, lnext;
+  explicit Lists(const qe_confstate_csr *cs)
+      : voters{cs->voters, cs->voters_off},
+        outgoing{cs->voters_outgoing, cs->outgoing_off},
+        learners{cs->learners, cs->learners_off},
+        lnext{cs->learners_next, cs->learners_next_off} {}
 };
 
 }  // namespace
@@ -77,15 +117,31 @@ namespace {
 
 // One group of a ConfState CSR batch in slot form: ids[S] (0 = unused), the
 // masks of Voters[0], Voters[1], Learners, LearnersNext, and QE_PACK_* flags.
-// A flagged group (too many peers, zero ID) is left empty.
+// A flagged group (too many peers, zero ID) is left empty.  nv / nl: the
+// number of distinct voters (union of both halves) and learners placed;
+// ni / no: distinct voters of each half.
 struct PackedGroup {
   uint32_t mi, mo, ml, mlnx, flags;
+  uint32_t nv, nl, ni, no;
 };
 
-PackedGroup pack_group(const List &voters, const List &outgoing, const List &learners,
-                       const List &lnext, uint64_t g, uint32_t S, uint64_t *ids) {
-  PackedGroup r{0, 0, 0, 0, 0};
-  uint64_t vbuf[2 * QE_MAX_SLOTS + 2], lbuf[QE_MAX_SLOTS + 1];
+uint32_t count_unique(const List &l, uint64_t g, uint64_t *buf, bool &over) {
+  if (!l.has(g)) return 0;
+  uint32_t n = 0;
+  for (const uint64_t *p = l.begin(g); p != l.end(g); ++p) {
+    if (n >= 2 * QE_MAX_SLOTS + 1) {
+      over = true;
+      break;
+    }
+    buf[n++] = *p;
+  }
+  std::sort(buf, buf + n);
+  return static_cast<uint32_t>(std::unique(buf, buf + n) - buf);
+}
+
+PackedGroup pack_group(const Lists &L, uint64_t g, uint32_t S, uint64_t *ids) {
+  PackedGroup r{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t vbuf[2 * QE_MAX_SLOTS + 2], lbuf[QE_MAX_SLOTS + 1], tmp[2 * QE_MAX_SLOTS + 2];
   memset(ids, 0, sizeof(uint64_t) * S);
   // voters of both halves, ascending + deduplicated (JointConfig.IDs)
   uint32_t nv = 0;
@@ -96,13 +152,17 @@ PackedGroup pack_group(const List &voters, const List &outgoing, const List &lea
       vbuf[nv++] = *p;
     }
   };
-  add_voters(voters);
-  add_voters(outgoing);
+  add_voters(L.voters);
+  add_voters(L.outgoing);
   std::sort(vbuf, vbuf + nv);
   nv = static_cast<uint32_t>(std::unique(vbuf, vbuf + nv) - vbuf);
+  bool over = false;
+  r.ni = count_unique(L.voters, g, tmp, over);
+  r.no = count_unique(L.outgoing, g, tmp, over);
+  if (over) r.flags |= QE_PACK_TOO_MANY_PEERS;
   uint32_t nl = 0;
-  if (learners.has(g)) {
-    for (const uint64_t *p = learners.begin(g); p != learners.end(g); ++p) {
+  if (L.learners.has(g)) {
+    for (const uint64_t *p = L.learners.begin(g); p != L.learners.end(g); ++p) {
       if (std::binary_search(vbuf, vbuf + nv, *p)) {
         r.flags |= QE_PACK_LEARNER_IS_VOTER;  // confchange.go:308-318 invariant
         continue;
@@ -115,11 +175,11 @@ PackedGroup pack_group(const List &voters, const List &outgoing, const List &lea
   nl = static_cast<uint32_t>(std::unique(lbuf, lbuf + nl) - lbuf);
   if (nv + nl > S) r.flags |= QE_PACK_TOO_MANY_PEERS;
   // LearnersNext must be outgoing voters (confchange.go:299-306)
-  if (lnext.has(g)) {
-    for (const uint64_t *p = lnext.begin(g); p != lnext.end(g); ++p) {
+  if (L.lnext.has(g)) {
+    for (const uint64_t *p = L.lnext.begin(g); p != L.lnext.end(g); ++p) {
       bool in_out = false;
-      if (outgoing.has(g))
-        for (const uint64_t *q = outgoing.begin(g); q != outgoing.end(g); ++q)
+      if (L.outgoing.has(g))
+        for (const uint64_t *q = L.outgoing.begin(g); q != L.outgoing.end(g); ++q)
           in_out |= (*q == *p);
       if (!in_out) r.flags |= QE_PACK_LEARNER_NEXT_NOT_OUTGOING;
     }
@@ -130,6 +190,8 @@ PackedGroup pack_group(const List &voters, const List &outgoing, const List &lea
     if (vbuf[i] == 0) r.flags |= QE_PACK_ZERO_ID;
   for (uint32_t i = 0; i < nl; i++)
     if (lbuf[i] == 0) r.flags |= QE_PACK_ZERO_ID;
+  r.nv = nv;
+  r.nl = nl;
   if (!(r.flags & QE_PACK_TOO_MANY_PEERS) && !(r.flags & QE_PACK_ZERO_ID)) {
     for (uint32_t i = 0; i < nv; i++) ids[i] = vbuf[i];
     for (uint32_t i = 0; i < nl; i++) ids[nv + i] = lbuf[i];
@@ -140,18 +202,83 @@ PackedGroup pack_group(const List &voters, const List &outgoing, const List &lea
         if (s >= 0) m |= 1u << s;
       }
     };
-    mark(voters, r.mi);
-    mark(outgoing, r.mo);
-    mark(lnext, r.mlnx);
+    mark(L.voters, r.mi);
+    mark(L.outgoing, r.mo);
+    mark(L.lnext, r.mlnx);
     r.mlnx &= r.mo;  // only outgoing voters can be LearnersNext
     for (uint32_t i = 0; i < nl; i++) r.ml |= 1u << (nv + i);
   }
   return r;
 }
 
+// Shape key of a group: (union size, |Voters[0]|, |Voters[1]|, learners),
+// each 0..16 for a placeable group; flagged groups (left empty) sort last.
+constexpr uint32_t kShapeDim = QE_MAX_SLOTS + 1;
+constexpr uint32_t kShapes = kShapeDim * kShapeDim * kShapeDim * kShapeDim + 1;
+
+uint32_t shape_key(const Lists &L, uint64_t g, uint32_t S) {
+  uint64_t ids[QE_MAX_SLOTS];
+  const PackedGroup r = pack_group(L, g, S, ids);
+  if (r.flags & (QE_PACK_TOO_MANY_PEERS | QE_PACK_ZERO_ID)) return kShapes - 1;
+  return ((r.nv * kShapeDim + r.ni) * kShapeDim + r.no) * kShapeDim + r.nl;
+}
+
+bool perm_ok(const uint64_t *perm, uint64_t G) {
+  if (!perm) return true;
+  std::atomic<bool> ok{true};
+  parallel_for(G, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; i++)
+      if (perm[i] >= G) { ok = false; return; }
+  });
+  return ok.load();
+}
+
 }  // namespace
 
 extern "C" {
+
+int qe_pack_order(const qe_confstate_csr *cs, uint32_t num_slots, uint64_t *perm,
+                  uint64_t *num_shapes) {
+  if (!cs || !perm) return QE_EINVAL;
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  const uint64_t G = cs->num_groups;
+  if (num_shapes) *num_shapes = 0;
+  if (G == 0) return QE_OK;
+  if (!cs->voters || !cs->voters_off) return QE_EINVAL;
+  const Lists L(cs);
+  const uint32_t S = num_slots;
+  // stable counting sort by shape: per-thread histograms over the thread's
+  // contiguous range, bucket-major / thread-minor offsets, then each thread
+  // scatters its range in order
+  const auto rg = ranges_of(G);
+  const size_t nt = rg.size();
+  std::vector<uint32_t> key(G);
+  std::vector<uint64_t> hist(nt * kShapes, 0);
+  parallel_ranges(rg, [&](unsigned t, uint64_t b, uint64_t e) {
+    uint64_t *h = &hist[t * kShapes];
+    for (uint64_t g = b; g < e; g++) {
+      key[g] = shape_key(L, g, S);
+      h[key[g]]++;
+    }
+  });
+  uint64_t run = 0, shapes = 0;
+  for (uint32_t k = 0; k < kShapes; k++) {
+    uint64_t tot = 0;
+    for (size_t t = 0; t < nt; t++) {
+      const uint64_t c = hist[t * kShapes + k];
+      hist[t * kShapes + k] = run;
+      run += c;
+      tot += c;
+    }
+    shapes += tot != 0;
+  }
+  parallel_ranges(rg, [&](unsigned t, uint64_t b, uint64_t e) {
+    uint64_t *h = &hist[t * kShapes];
+    for (uint64_t g = b; g < e; g++) perm[h[key[g]]++] = g;
+  });
+  if (num_shapes) *num_shapes = shapes;
+  return QE_OK;
+}
 
 int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_mask,
                       void *out_mask, void *learner_mask, uint64_t *slot_ids,
@@ -162,19 +289,21 @@ int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_
   if (num_flagged) *num_flagged = 0;
   if (G == 0) return QE_OK;
   if (!cs->voters || !cs->voters_off) return QE_EINVAL;
+  if (!perm_ok(cs->perm, G)) return QE_EINVAL;
   const uint32_t S = num_slots, mb = S <= 8 ? 1 : 2;
-  const List voters{cs->voters, cs->voters_off}, outgoing{cs->voters_outgoing, cs->outgoing_off};
-  const List learners{cs->learners, cs->learners_off};
-  const List lnext{cs->learners_next, cs->learners_next_off};
+  const Lists L(cs);
   std::atomic<uint64_t> flagged{0};
   parallel_for(G, [&](uint64_t b, uint64_t e) {
     uint64_t local_flagged = 0;
-    for (uint64_t g = b; g < e; g++) {
-      const PackedGroup r = pack_group(voters, outgoing, learners, lnext, g, S, slot_ids + g * S);
-      put_mask(inc_mask, mb, g, r.mi);
-      put_mask(out_mask, mb, g, r.mo);
-      put_mask(learner_mask, mb, g, r.ml);
-      if (group_flags) group_flags[g] = r.flags;
+    uint64_t ids[QE_MAX_SLOTS];
+    for (uint64_t i = b; i < e; i++) {
+      const uint64_t g = cs->perm ? cs->perm[i] : i;
+      const PackedGroup r = pack_group(L, g, S, ids);
+      for (uint32_t s = 0; s < S; s++) slot_ids[s * G + i] = ids[s];
+      put_mask(inc_mask, mb, i, r.mi);
+      put_mask(out_mask, mb, i, r.mo);
+      put_mask(learner_mask, mb, i, r.ml);
+      if (group_flags) group_flags[i] = r.flags;
       local_flagged += r.flags != 0;
     }
     flagged += local_flagged;
@@ -195,26 +324,32 @@ int qe_pack_conf(const qe_confstate_csr *cs, const qe_conf *out, uint32_t *group
   if (!out->slot_ids || !out->inc_mask || !out->out_mask || !out->learner_mask ||
       !out->learners_next_mask || !out->is_learner || !out->tracked || !out->auto_leave)
     return QE_EINVAL;
+  if (!perm_ok(cs->perm, G)) return QE_EINVAL;
   const uint32_t S = out->num_slots, mb = S <= 8 ? 1 : 2;
-  const List voters{cs->voters, cs->voters_off}, outgoing{cs->voters_outgoing, cs->outgoing_off};
-  const List learners{cs->learners, cs->learners_off};
-  const List lnext{cs->learners_next, cs->learners_next_off};
+  const Lists L(cs);
   std::atomic<uint64_t> flagged{0};
   parallel_for(G, [&](uint64_t b, uint64_t e) {
     uint64_t local_flagged = 0;
-    for (uint64_t g = b; g < e; g++) {
-      uint64_t *ids = out->slot_ids + g * S;
-      const PackedGroup r = pack_group(voters, outgoing, learners, lnext, g, S, ids);
+    uint64_t ids[QE_MAX_SLOTS];
+    for (uint64_t i = b; i < e; i++) {
+      const uint64_t g = cs->perm ? cs->perm[i] : i;
+      const PackedGroup r = pack_group(L, g, S, ids);
       uint32_t trk = 0;
-      for (uint32_t s = 0; s < S; s++) trk |= ids[s] ? (1u << s) : 0u;
-      put_mask(out->inc_mask, mb, g, r.mi);
-      put_mask(out->out_mask, mb, g, r.mo);
-      put_mask(out->learner_mask, mb, g, r.ml);
-      put_mask(out->learners_next_mask, mb, g, r.mlnx);
-      put_mask(out->is_learner, mb, g, r.ml);  // LearnersNext stay !IsLearner (confchange.go:299-306)
-      put_mask(out->tracked, mb, g, trk);
-      out->auto_leave[g] = (cs->auto_leave && r.flags == 0) ? (cs->auto_leave[g] != 0) : 0;
-      if (group_flags) group_flags[g] = r.flags;
+      for (uint32_t s = 0; s < S; s++) {
+        out->slot_ids[s * G + i] = ids[s];
+        trk |= ids[s] ? (1u << s) : 0u;
+      }
+      put_mask(out->inc_mask, mb, i, r.mi);
+      put_mask(out->out_mask, mb, i, r.mo);
+      put_mask(out->learner_mask, mb, i, r.ml);
+      put_mask(out->learners_next_mask, mb, i, r.mlnx);
+      put_mask(out->is_learner, mb, i, r.ml);  // LearnersNext stay !IsLearner (confchange.go:299-306)
+      put_mask(out->tracked, mb, i, trk);
+      // restore.go:118-155: AutoLeave takes effect only through EnterJoint,
+      // i.e. in a joint config; a non-joint ConfState restores AutoLeave =
+      // false (checkInvariants rejects AutoLeave without Voters[1])
+      out->auto_leave[i] = (cs->auto_leave && r.flags == 0 && r.mo != 0) ? (cs->auto_leave[g] != 0) : 0;
+      if (group_flags) group_flags[i] = r.flags;
       local_flagged += r.flags != 0;
     }
     flagged += local_flagged;
@@ -224,24 +359,29 @@ int qe_pack_conf(const qe_confstate_csr *cs, const qe_conf *out, uint32_t *group
 }
 
 int qe_pack_match(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
-                  const uint64_t *prog_off, const uint64_t *prog_ids, const uint64_t *prog_match,
-                  uint64_t *match, uint64_t stride, uint64_t *num_unknown) {
+                  const uint64_t *perm, const uint64_t *prog_off, const uint64_t *prog_ids,
+                  const uint64_t *prog_match, uint64_t *match, uint64_t stride,
+                  uint64_t *num_unknown) {
   if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
   if (num_unknown) *num_unknown = 0;
   if (num_groups == 0) return QE_OK;
   if (!slot_ids || !prog_off || !prog_ids || !prog_match || !match) return QE_EINVAL;
   if (stride < num_groups) return QE_EINVAL;
+  if (!perm_ok(perm, num_groups)) return QE_EINVAL;
   const uint32_t S = num_slots;
+  const uint64_t G = num_groups;
   std::atomic<uint64_t> unknown{0};
-  parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
+  parallel_for(G, [&](uint64_t b, uint64_t e) {
     uint64_t u = 0;
-    for (uint64_t g = b; g < e; g++) {
-      const uint64_t *ids = slot_ids + g * S;
-      for (uint32_t s = 0; s < S; s++) match[s * stride + g] = 0;  // absent
+    uint64_t ids[QE_MAX_SLOTS];
+    for (uint64_t i = b; i < e; i++) {
+      const uint64_t g = perm ? perm[i] : i;
+      gather_ids(slot_ids, G, S, i, ids);
+      for (uint32_t s = 0; s < S; s++) match[s * stride + i] = 0;  // absent
       for (uint64_t k = prog_off[g]; k < prog_off[g + 1]; k++) {
         const int s = slot_of(ids, S, prog_ids[k]);
         if (s < 0 || prog_ids[k] == 0) { u++; continue; }
-        match[static_cast<uint64_t>(s) * stride + g] = prog_match[k];
+        match[static_cast<uint64_t>(s) * stride + i] = prog_match[k];
       }
     }
     unknown += u;
@@ -251,15 +391,19 @@ int qe_pack_match(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_
 }
 
 int qe_pack_votes(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
-                  const uint64_t *vote_off, const uint64_t *vote_ids, const uint8_t *vote_vals,
-                  void *voted, void *granted) {
+                  const uint64_t *perm, const uint64_t *vote_off, const uint64_t *vote_ids,
+                  const uint8_t *vote_vals, void *voted, void *granted) {
   if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
   if (num_groups == 0) return QE_OK;
   if (!slot_ids || !vote_off || !vote_ids || !vote_vals || !voted || !granted) return QE_EINVAL;
+  if (!perm_ok(perm, num_groups)) return QE_EINVAL;
   const uint32_t S = num_slots, mb = S <= 8 ? 1 : 2;
-  parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
-    for (uint64_t g = b; g < e; g++) {
-      const uint64_t *ids = slot_ids + g * S;
+  const uint64_t G = num_groups;
+  parallel_for(G, [&](uint64_t b, uint64_t e) {
+    uint64_t ids[QE_MAX_SLOTS];
+    for (uint64_t i = b; i < e; i++) {
+      const uint64_t g = perm ? perm[i] : i;
+      gather_ids(slot_ids, G, S, i, ids);
       uint32_t vd = 0, gr = 0;
       for (uint64_t k = vote_off[g]; k < vote_off[g + 1]; k++) {
         const int s = slot_of(ids, S, vote_ids[k]);
@@ -269,8 +413,8 @@ int qe_pack_votes(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_
         vd |= bit;
         if (vote_vals[k]) gr |= bit;
       }
-      put_mask(voted, mb, g, vd);
-      put_mask(granted, mb, g, gr);
+      put_mask(voted, mb, i, vd);
+      put_mask(granted, mb, i, gr);
     }
   });
   return QE_OK;
@@ -283,10 +427,15 @@ int qe_slot_lookup(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot
   if (!slot_ids || !group || !id || !slot) return QE_EINVAL;
   const uint32_t S = num_slots;
   parallel_for(n, [&](uint64_t b, uint64_t e) {
+    uint64_t ids[QE_MAX_SLOTS];
     for (uint64_t i = b; i < e; i++) {
       const uint64_t g = group[i];
-      slot[i] = (g < num_groups && id[i] != 0) ? static_cast<int8_t>(slot_of(slot_ids + g * S, S, id[i]))
-                                                : static_cast<int8_t>(-1);
+      if (g >= num_groups || id[i] == 0) {
+        slot[i] = -1;
+        continue;
+      }
+      gather_ids(slot_ids, num_groups, S, g, ids);
+      slot[i] = static_cast<int8_t>(slot_of(ids, S, id[i]));
     }
   });
   return QE_OK;

@@ -55,18 +55,27 @@ __device__ __forceinline__ void bst64(uint64_t v, rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst8(uint32_t v, rsrc_t r, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, 0);
 }
+__device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst32(uint32_t v, rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+}
 template <typename MT>
-__device__ __forceinline__ void bst_mask(uint32_t v, rsrc_t r, uint32_t lane) {
+__device__ __forceinline__ void bst_mask(uint32_t v, rsrc_t r, uint32_t lane, bool on = true) {
+  const uint32_t off = on ? lane * static_cast<uint32_t>(sizeof(MT)) : kOOB;
   if constexpr (sizeof(MT) == 1)
-    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, lane, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, 0);
   else
-    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v), r, lane * 2, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v), r, off, 0, 0);
 }
 
 // Byte accounting of the instrumented variant (ACCT): the bytes of every
 // access the reference logic needs (field granularity, each once), i.e. the
 // algorithmic bytes of the round.  Re-reads (Match, m.Index in phase 2)
-// are not counted.
+// are not counted.  The rules are restated independently by
+// the oracle (orc_progress_step_batch's byte count), and the GPU tests
+// require the two counts to be equal.
 template <bool ACCT>
 struct Acct {
   uint64_t b = 0;
@@ -88,6 +97,8 @@ __device__ __forceinline__ void acct_flush(const Acct<ACCT> &ac, uint64_t *acct)
 // Checksum of the round: a per-group part from the commit pass and a
 // per-group part from the peer pass (oracle/quorum_oracle.c orc_checksum_step).
 constexpr uint64_t kSentSalt = 0xD1B54A32D192ED03ull;
+constexpr uint64_t kReadSalt = 0x8CB92BA72F3D8DD7ull;   // a released ReadIndex request
+constexpr uint64_t kQuorumSalt = 0xA0761D6478BD642Full; // CheckQuorum: quorum active
 
 // ---------------------------------------------------------------------------
 // Sends: raft.maybeSendAppend (raft/raft.go:432-492) in closed form.
@@ -312,37 +323,33 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
 // ---------------------------------------------------------------------------
 struct PB {  // per-peer loads of one slot
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
-  uint32_t fl, st, ct;
+  uint32_t w;                   // the packed per-peer word (QE_PW_*)
   uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring (pb_ring)
 };
 
-// Loads of slot row `row` (= s*stride + tile0): the Progress fields of a
-// touched peer and RejectHint/LogTerm of a reject.
+// Loads of slot row `row` (= s*stride + tile0): Next and the packed word of
+// a peer that may be touched (`ld`, a superset of the lanes the round
+// touches) and RejectHint/LogTerm of a reject.  The byte accounting is done
+// by the caller, on the lanes the round actually touches.
 // A wave-level branch skips each group of loads no lane needs (an issued
 // vector memory instruction costs the CU's memory path about the same
 // whether or not its lanes are masked off).
-template <bool ACCT>
 __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *l_mix,
-                                        uint32_t n, uint32_t lane, bool touched, bool rej,
-                                        bool has_ix, PB &b, Acct<ACCT> &ac) {
+                                        uint32_t n, uint32_t lane, bool ld, bool rej,
+                                        bool has_ix, PB &b) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
   b.nx = 0;
-  b.fl = b.st = b.ct = 0;
-  if (__builtin_amdgcn_ballot_w64(touched)) {
-    const uint32_t o8 = touched ? lane * 8 : kOOB, o1 = touched ? lane : kOOB;
-    b.nx = bld64(mk_rsrc(a.next + row, n * 8), o8);
-    b.fl = bld8(mk_rsrc(a.flags + row, n), o1);
-    b.st = bld8(mk_rsrc(a.istart + row, n), o1);
-    b.ct = bld8(mk_rsrc(a.icount + row, n), o1);
+  b.w = 0;
+  if (__builtin_amdgcn_ballot_w64(ld)) {
+    b.nx = bld64(mk_rsrc(a.next + row, n * 8), ld ? lane * 8 : kOOB);
+    b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
   }
   b.hn = b.lt = 0;
   if (__builtin_amdgcn_ballot_w64(rej)) {
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
   }
-  ac.add(touched, 11);
-  ac.add(rej, 16);
 #pragma unroll
   for (int k = 0; k < kRingChunk; k++) b.rw[k] = 0;
 }
@@ -416,9 +423,22 @@ k_progress_step(PArgs a) {
     const rsrc_t r_commit = mk_rsrc(a.committed + g0, n * 8);
     const uint64_t c0 = bld64(r_commit, o8);
     const uint64_t snap_ld = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), o8) : 0;
+    // ReadIndex (ABI 3): the pending request's acks and the slots whose
+    // heartbeat response carries its context
+    const bool rd = a.read_acks != nullptr;  // wave-uniform
+    const uint32_t acks0 =
+        rd ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.read_acks) + g0, n * sizeof(MT)),
+                            lane) & kFull)
+           : 0u;
+    const uint32_t rctx =
+        (rd && a.read_ctx)
+            ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.read_ctx) + g0, n * sizeof(MT)),
+                             lane) & kFull)
+            : kFull;
     ac.add(live, (MASKED ? sizeof(MT) : 0) + (JOINT ? sizeof(MT) : 0) +
                      (a.tracked ? sizeof(MT) : 0) + (a.self_slot ? 1 : 0) +
-                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0));
+                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0) +
+                     (rd ? sizeof(MT) : 0) + ((rd && a.read_ctx) ? sizeof(MT) : 0));
     uint64_t m0[S];
     uint32_t ty[S];
 #pragma unroll
@@ -458,8 +478,8 @@ k_progress_step(PArgs a) {
       const uint32_t t0 = ty_of(0);
       const bool msg = t0 >= QE_MSG_APP_RESP && t0 <= QE_MSG_UNREACHABLE;
       const bool ld = (trk & 1u) && (msg || self != 0u);
-      pb_load<ACCT>(a, g0, &l_mix[wv][0][0][0], n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT,
-                    has_ix_of(0), cur, ac);
+      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT,
+              has_ix_of(0), cur);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
@@ -492,6 +512,8 @@ k_progress_step(PArgs a) {
     x.lane = lane;
     x.row = row_ring;
     uint32_t sent = 0, snapm = 0, tnow = 0;
+    uint32_t acks = acks0;
+    bool released = false;
     auto touched_of = [&](uint32_t s) -> bool {
       const bool tr = (trk >> s) & 1u;
       const uint32_t t = ty_of(s);
@@ -512,17 +534,15 @@ k_progress_step(PArgs a) {
       const bool touched = touched_of(s);
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
-        pb_load<ACCT>(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
-                      ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt, ac);
+        pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
+                ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt);
       if (row_ring) pb_ring(a, a.ibuf + static_cast<uint64_t>(s) * F * a.stride + g0, lane, ring_of(s), cur);
+      ac.add(touched, 12);  // Next + the packed word
+      ac.add(touched && tt == QE_MSG_APP_RESP_REJECT, 16);  // RejectHint + LogTerm
       PR p;
       p.match = cur.mt;
       p.next = cur.nx;
-      p.state = cur.fl & QE_PF_STATE;
-      p.probe_sent = (cur.fl & QE_PF_PROBE_SENT) != 0;
-      p.recent_active = (cur.fl & QE_PF_RECENT_ACTIVE) != 0;
-      p.start = cur.st;
-      p.count = cur.ct;
+      pr_unpack(p, cur.w);
       p.reset = 0;
       // PendingSnapshot is read only in StateSnapshot (every other state only
       // ever overwrites it)
@@ -657,6 +677,13 @@ k_progress_step(PArgs a) {
             free_le<ACCT>(p, first, c_old, fo, r1, x, ac);
           }
           k2 = p.match < li ? 1u : 0u;
+          // ReadOnlySafe (raft.go:1296-1309): recvAck, then the request is
+          // released (readOnly.advance) once the acks win the vote; a later
+          // response of the round finds it gone (recvAck returns nil)
+          if (rd && !released && ((rctx >> s) & 1u)) {
+            acks |= 1u << s;
+            released = joint_vote(mi, mo, acks, acks) == kVoteWon;
+          }
         } else if (tt == QE_MSG_SNAP_STATUS || tt == QE_MSG_SNAP_STATUS_REJECT) {  // :1310-1331
           if (p.state == QE_PR_SNAPSHOT) {
             if (tt == QE_MSG_SNAP_STATUS_REJECT) p.pending = 0;
@@ -674,30 +701,23 @@ k_progress_step(PArgs a) {
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
       if (row_ring) ring_flush(x, r1, r2, n);
-      // ---- stores: the peer's new Progress (unchanged words and bytes skipped) ----
-      const uint32_t w8 = touched ? o8 : kOOB, w1 = touched ? lane : kOOB;
-      const uint32_t fl = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
-                          (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u);
+      // ---- stores: the peer's new Progress (unchanged words skipped) ----
+      const uint32_t nw = pr_pack(p);
       const bool wm = touched && up, wn = touched && p.next != cur.nx;
       const bool wp = touched && (p.pending != pd0 || p.reset);
-      const bool wf = touched && fl != cur.fl, ws = touched && p.start != cur.st;
-      const bool wc = touched && p.count != cur.ct;
+      const bool ww = touched && nw != cur.w;
       if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? w8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
       if (__builtin_amdgcn_ballot_w64(wp))
-        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? w8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wf)) bst8(fl, mk_rsrc(a.flags + row, n), wf ? w1 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(ws)) bst8(p.start, mk_rsrc(a.istart + row, n), ws ? w1 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wc)) bst8(p.count, mk_rsrc(a.icount + row, n), wc ? w1 : kOOB);
+        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), ww ? lane * 4 : kOOB);
       if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
       if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
         bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);
-      ac.add(wf, 1);
-      ac.add(ws, 1);
-      ac.add(wc, 1);
+      ac.add(ww, 4);
       ac.add(live && a.msg_count, 1);
       ac.add(x.count_msgs && a.msg_index, 8);
       sent |= x.count_msgs ? (1u << s) : 0u;
@@ -711,6 +731,14 @@ k_progress_step(PArgs a) {
     if (a.snap) bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
     if (a.tnow) bst_mask<MT>(tnow, opt_rsrc(static_cast<const MT *>(a.tnow), g0, n), lane);
     if (a.bcast) bst8(bc, opt_rsrc(static_cast<const uint8_t *>(a.bcast), g0, n), lane);
+    if (rd) {
+      const bool wa = acks != acks0;
+      if (__builtin_amdgcn_ballot_w64(wa))
+        bst_mask<MT>(acks, mk_rsrc(static_cast<MT *>(a.read_acks) + g0, n * sizeof(MT)), lane, wa);
+      ac.add(live && wa, sizeof(MT));
+    }
+    if (a.read_ok) bst8(released ? 1u : 0u, opt_rsrc(a.read_ok, g0, n), lane);
+    ac.add(live && a.read_ok, 1);
     ac.add(live && c != c0, 8);
     ac.add(live && a.sent, sizeof(MT));
     ac.add(live && a.snap, sizeof(MT));
@@ -721,13 +749,16 @@ k_progress_step(PArgs a) {
       cnt[P_GROUPS] += 1;
       cnt[P_SUM] += c;
       cnt[P_ADV] += (c != c0);
+      cnt[P_READ] += released ? 1u : 0u;
       cnt[P_CSUM] += mix64(gh ^ c ^ (static_cast<uint64_t>(bc) << 62)) +
-                     mix64(gh ^ (static_cast<uint64_t>(sent) << 40) ^ kSentSalt);
+                     mix64(gh ^ (static_cast<uint64_t>(sent) << 40) ^ kSentSalt) +
+                     (released ? mix64(gh ^ kReadSalt) : 0ull);
     }
   }
   if (a.stats) {
     const int idx[P_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
-                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_CHECKSUM};
+                          QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_READ_RELEASED,
+                          QE_STAT_CHECKSUM};
     block_stats_add<P_N, 64 * WPB>(cnt, idx, a.stats);
   }
   acct_flush<ACCT>(ac, a.acct);
@@ -737,82 +768,183 @@ k_progress_step(PArgs a) {
 // once for every slot of want[g] (bcastAppend after a proposal,
 // raft/raft.go:515-522).  PendingSnapshot is never read (BecomeSnapshot
 // only writes it).
+//
+// Software-pipelined like the stream commit kernel (qe_stream.hpp): a wave
+// owns a chunk of up to kSendTPW tiles, the chunk's want masks are staged in
+// LDS first (so a tile's Progress loads depend on an LDS read, not on a
+// vector load queued behind the previous tile's traffic), and two register
+// sets keep tile t+1's Progress loads in flight while tile t sends.
+constexpr int kSendTPW = 8;
+
+template <int S>
+struct SendSet {
+  uint64_t fi, li, sn;
+  uint64_t nx[S];
+  uint32_t pw[S];
+};
+
+template <int S>
+__device__ __forceinline__ void ps_issue(const PArgs &a, uint64_t t, uint32_t lane, uint32_t w,
+                                         SendSet<S> &x) {
+  const uint64_t g0 = t * 64;
+  const uint32_t n = tile_n(a.G, t);
+  const uint32_t o8 = lane * 8, o4 = lane * 4;
+  x.fi = bld64(mk_rsrc(a.first_index + g0, n * 8), w ? o8 : kOOB);
+  x.li = bld64(mk_rsrc(a.last_index + g0, n * 8), w ? o8 : kOOB);
+  x.sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), w ? o8 : kOOB) : 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+    x.nx[s] = bld64(mk_rsrc(a.next + row, n * 8), bit_off(w, s, o8));
+    x.pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), bit_off(w, s, o4));
+  }
+}
+
+template <int S, typename MT>
+__device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t lane, uint32_t w,
+                                          const SendSet<S> &x) {
+  const uint64_t g0 = t * 64;
+  const uint32_t n = tile_n(a.G, t);
+  Acct<false> ac;
+  PSend xs;
+  xs.F = a.F;
+  xs.me = a.max_ents;
+  xs.fi = x.fi;
+  xs.li = x.li;
+  xs.snap = a.snap_index ? x.sn : x.fi - 1;
+  xs.rs = a.stride;
+  xs.lane = lane;
+  // one maybeSendAppend appends at most one entry: stored directly at its
+  // ring position (one instruction), not as F entry-row stores
+  xs.row = false;
+  uint32_t sent = 0, snapm = 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+    const bool on = (w >> s) & 1u;
+    PR p;
+    p.match = 0;
+    p.next = x.nx[s];
+    pr_unpack(p, x.pw[s]);
+    p.pending = 0;
+    p.reset = 0;
+    xs.rb = a.ibuf + static_cast<uint64_t>(s) * a.F * a.stride + g0;
+    xs.count_msgs = 0;
+    xs.first_index = 0;
+    xs.snapped = false;
+    PRun run{0, 0, 0};
+    send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
+    const uint32_t nw = pr_pack(p);
+    const bool wn = on && p.next != x.nx[s], wp = on && xs.snapped, ww = on && nw != x.pw[s];
+    if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
+    if (__builtin_amdgcn_ballot_w64(wp))
+      bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? lane * 8 : kOOB);
+    if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), ww ? lane * 4 : kOOB);
+    sent |= xs.count_msgs ? (1u << s) : 0u;
+    snapm |= xs.snapped ? (1u << s) : 0u;
+  }
+  bst_mask<MT>(sent, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+  bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+}
+
 template <int S, typename MT>
 __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
-  Acct<false> ac;
+  __shared__ uint32_t lds_w[kBlock / 64][kSendTPW][64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  const uint32_t chunk = a.chunk;  // <= kSendTPW (host-checked)
+  const uint64_t t0 = (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv) * chunk;
+  const uint32_t nt =
+      t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < chunk ? ntiles - t0 : chunk) : 0u;
+  if (nt == 0) return;  // no block-level barrier below
+  // the chunk's want masks (a tile past the chunk: n = 0, mask 0)
+#pragma unroll
+  for (int k = 0; k < kSendTPW; k++) {
+    const uint64_t t = t0 + k;
+    const uint32_t n = static_cast<uint32_t>(k) < nt ? tile_n(a.G, t) : 0u;
+    lds_w[wv][k][lane] =
+        ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.want) + t * 64, n * sizeof(MT)), lane) &
+        kFull;
+  }
+  // tile k of the chunk, or past the end (no loads, no stores, want 0)
+  auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k : ntiles; };
+  auto want_of = [&](uint32_t k) -> uint32_t { return k < nt ? lds_w[wv][k][lane] : 0u; };
+  SendSet<S> xa, xb;
+  ps_issue<S>(a, tix(0), lane, want_of(0), xa);
+  for (uint32_t k = 0; k < nt; k += 2) {
+    ps_issue<S>(a, tix(k + 1), lane, want_of(k + 1), xb);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the sends
+    ps_finish<S, MT>(a, tix(k), lane, want_of(k), xa);
+    ps_issue<S>(a, tix(k + 2), lane, want_of(k + 2), xa);
+    __builtin_amdgcn_sched_barrier(0);
+    ps_finish<S, MT>(a, tix(k + 1), lane, want_of(k + 1), xb);
+  }
+}
+
+// qe_check_quorum: MsgCheckQuorum (raft/raft.go:997-1018) over the resident
+// Progress words.  One lane per group, a wave per 64-group tile; only the
+// tracked slots' words are loaded, only changed words are stored.
+template <int S, typename MT, bool MASKED, bool JOINT>
+__global__ __launch_bounds__(kBlock) void k_check_quorum(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  uint64_t cnt[3] = {0, 0, 0};
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave =
-      static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
-      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
   const uint64_t ntiles = (a.G + 63) / 64;
-  const uint32_t o8 = lane * 8;
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
-    const uint32_t w =
-        ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.want) + g0, n * sizeof(MT)), lane) & kFull;
-    PSend x;
-    x.F = a.F;
-    x.me = a.max_ents;
-    x.fi = bld64(mk_rsrc(a.first_index + g0, n * 8), w ? o8 : kOOB);
-    x.li = bld64(mk_rsrc(a.last_index + g0, n * 8), w ? o8 : kOOB);
-    x.snap = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), w ? o8 : kOOB) : x.fi - 1;
-    uint32_t sent = 0, snapm = 0;
-    // every slot's Progress loads first (one batch in flight), then the sends
-    uint64_t nx[S];
-    uint32_t fl[S], st[S], ct[S];
+    const uint32_t mi =
+        MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * sizeof(MT)), lane) &
+                  kFull)
+               : kFull;
+    const uint32_t mo =
+        JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * sizeof(MT)), lane) &
+                 kFull)
+              : 0u;
+    const uint32_t trk =
+        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0,
+                                           n * sizeof(MT)), lane) & kFull)
+                  : kFull;
+    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
+    uint32_t w[S];
+#pragma unroll
+    for (int s = 0; s < S; s++)
+      w[s] = bld32(mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
+                   bit_off(trk, s, lane * 4));
+    // the leader sees itself active (when it still has a Progress)
+    const uint32_t selfb = self < static_cast<uint32_t>(S) ? ((1u << self) & trk) : 0u;
+    uint32_t ra = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) ra |= ((w[s] >> 3) & 1u) << s;
+    ra = (ra & trk) | selfb;
+    // QuorumActive: every voter with a Progress votes its RecentActive
+    const uint32_t present = (mi | mo) & trk;
+    const bool qa = joint_vote(mi, mo, present, ra & present) == kVoteWon;
+    // Visit: RecentActive = false for every tracked peer but the leader
 #pragma unroll
     for (int s = 0; s < S; s++) {
-      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
-      const bool on = (w >> s) & 1u;
-      const uint32_t r8 = on ? o8 : kOOB, r1 = on ? lane : kOOB;
-      nx[s] = bld64(mk_rsrc(a.next + row, n * 8), r8);
-      fl[s] = bld8(mk_rsrc(a.flags + row, n), r1);
-      st[s] = bld8(mk_rsrc(a.istart + row, n), r1);
-      ct[s] = bld8(mk_rsrc(a.icount + row, n), r1);
+      const uint32_t nw = (w[s] & ~QE_PF_RECENT_ACTIVE) | (((selfb >> s) & 1u) ? QE_PF_RECENT_ACTIVE : 0u);
+      const bool wr = ((trk >> s) & 1u) && nw != w[s];
+      if (__builtin_amdgcn_ballot_w64(wr))
+        bst32(nw, mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
+              wr ? lane * 4 : kOOB);
     }
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
-      const bool on = (w >> s) & 1u;
-      PR p;
-      p.match = 0;
-      p.next = nx[s];
-      p.state = fl[s] & QE_PF_STATE;
-      p.probe_sent = (fl[s] & QE_PF_PROBE_SENT) != 0;
-      p.recent_active = (fl[s] & QE_PF_RECENT_ACTIVE) != 0;
-      p.start = st[s];
-      p.count = ct[s];
-      p.pending = 0;
-      p.reset = 0;
-      x.rb = a.ibuf + static_cast<uint64_t>(s) * a.F * a.stride + g0;
-      x.rs = a.stride;
-      x.lane = lane;
-      // one maybeSendAppend appends at most one entry: stored directly at
-      // its ring position (one instruction), not as F entry-row stores
-      x.row = false;
-      x.count_msgs = 0;
-      x.first_index = 0;
-      x.snapped = false;
-      PRun run{0, 0, 0};
-      send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, x, run, ac);
-      const uint32_t f2 = p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
-                          (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u);
-      const bool wn = on && p.next != nx[s], wp = on && x.snapped, wf = on && f2 != fl[s];
-      const bool ws = on && p.start != st[s], wc = on && p.count != ct[s];
-      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wp))
-        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wf)) bst8(f2, mk_rsrc(a.flags + row, n), wf ? lane : kOOB);
-      if (__builtin_amdgcn_ballot_w64(ws)) bst8(p.start, mk_rsrc(a.istart + row, n), ws ? lane : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wc)) bst8(p.count, mk_rsrc(a.icount + row, n), wc ? lane : kOOB);
-      sent |= x.count_msgs ? (1u << s) : 0u;
-      snapm |= x.snapped ? (1u << s) : 0u;
+    if (a.qactive) bst8(qa ? 1u : 0u, opt_rsrc(a.qactive, g0, n), lane);
+    if (lane < n) {
+      cnt[0] += 1;
+      cnt[1] += qa ? 0u : 1u;
+      cnt[2] += mix64(((a.goff + g0 + lane) * kPhi) ^ (static_cast<uint64_t>(ra) << 32) ^
+                      (qa ? kQuorumSalt : 0ull));
     }
-    bst_mask<MT>(sent, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
-    bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+  }
+  if (a.stats) {
+    const int idx[3] = {QE_STAT_GROUPS, QE_STAT_STEPDOWNS, QE_STAT_CHECKSUM};
+    block_stats_add<3, kBlock>(cnt, idx, a.stats);
   }
 }
 

@@ -119,11 +119,12 @@ def stats_reduce(stats):
     return out
 
 
-def collect(flags, values=None, group_offset=0, scratch=None):
-    """qe_collect: the groups with flags[g] != 0 in ascending order (the
-    Ready-style delta of a batch step, e.g. qe_replication_round's `adv` with
-    `committed` as values) -> (groups int64[n], values int64[n] or None).
-    One int64 count is read back to size the result."""
+def collect(flags, values=None, group_offset=0, scratch=None, perm=None):
+    """qe_collect: the groups with flags[g] != 0 in ascending position order
+    (the Ready-style delta of a batch step, e.g. qe_replication_round's `adv`
+    with `committed` as values) -> (groups int64[n], values int64[n] or None).
+    perm (device int64[G], qe_pack_order) maps packed positions back to the
+    caller's group ids.  One int64 count is read back to size the result."""
     G = flags.numel()
     dev = flags.device
     lib = _lib.lib()
@@ -133,7 +134,8 @@ def collect(flags, values=None, group_offset=0, scratch=None):
     groups = torch.empty(max(1, G), dtype=torch.int64, device=dev)
     vals = torch.empty(max(1, G), dtype=torch.int64, device=dev) if values is not None else None
     count = torch.empty(1, dtype=torch.int64, device=dev)
-    check("qe_collect", lib.qe_collect(G, group_offset, _ptr(flags), _ptr(values), _ptr(groups),
+    check("qe_collect", lib.qe_collect(G, group_offset, _ptr(perm), _ptr(flags), _ptr(values),
+                                       _ptr(groups),
                                        _ptr(vals), _ptr(count), _ptr(scratch), _stream(dev)))
     n = int(count.item())
     return groups[:n], (vals[:n] if vals is not None else None)
@@ -145,10 +147,14 @@ def stats_dict(folded):
 
 
 def gen_groups(batch, seed, dist=0, p_absent=3277, p_voted=52429, p_granted=39322, n_inc=0,
-               n_out=0, mask_mode=0):
-    """Fill `batch` with the counter-based synthetic generator."""
+               n_out=0, mask_mode=0, values_only=False):
+    """Fill `batch` with the counter-based synthetic generator.
+    values_only: Match and votes only, the batch's masks are left as they are
+    (e.g. as a packer wrote them)."""
     p = QeGenParams(seed, 0, dist, p_absent, p_voted, p_granted, n_inc, n_out, mask_mode, 0)
     g = batch.struct()
+    if values_only:
+        g.inc_mask = g.out_mask = g.learner_mask = None
     check("qe_gen_groups", _lib.lib().qe_gen_groups(C.byref(g), C.byref(p),
                                                      _stream(batch.device)))
     return batch
@@ -280,12 +286,21 @@ def tune(key, value):
     check("qe_tune", _lib.lib().qe_tune(key.encode(), int(value)))
 
 
+def pack_peer_word(flags, start=0, count=0):
+    """The packed per-peer word (include/etcd_quorum.h QE_PW_*): flag bits
+    (StateType | ProbeSent << 2 | RecentActive << 3), Inflights.start << 8,
+    Inflights.count << 16.  numpy arrays or ints."""
+    return ((np.asarray(flags, np.uint32) & 0xF) | (np.asarray(start, np.uint32) << 8) |
+            (np.asarray(count, np.uint32) << 16)).astype(np.uint32)
+
+
 class ProgressState:
     """Device-resident leader-side Progress of G groups (qe_progress):
-    match/next/pending [S][stride], flags, Inflights rings [S][F][stride] (entry-major),
-    committed, and the leader-log model (term runs).  `extras` allocates the
-    optional per-group arrays of ABI 2: "tracked" (slot mask), "self_slot",
-    "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""
+    match/next/pending [S][stride], the packed per-peer words `peer` [S][stride]
+    (int32 storage of the u32 QE_PW_* words), Inflights rings [S][F][stride]
+    (entry-major), committed, and the leader-log model (term runs).  `extras`
+    allocates the optional per-group arrays: "tracked" (slot mask),
+    "self_slot", "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""
 
     def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None,
                  extras=(), max_ents=0):
@@ -303,9 +318,7 @@ class ProgressState:
         self.match = torch.zeros(n, dtype=i64, device=dev)
         self.next = torch.ones(n, dtype=i64, device=dev)
         self.pending = torch.zeros(n, dtype=i64, device=dev)
-        self.flags = torch.zeros(n, dtype=u8, device=dev)
-        self.istart = torch.zeros(n, dtype=u8, device=dev)
-        self.icount = torch.zeros(n, dtype=u8, device=dev)
+        self.peer = torch.zeros(n, dtype=torch.int32, device=dev)
         self.ibuf = torch.zeros(self.S * self.F * self.stride, dtype=i64, device=dev)
         self.committed = torch.zeros(self.G, dtype=i64, device=dev)
         self.term_start = torch.zeros(self.G, dtype=i64, device=dev)
@@ -328,19 +341,27 @@ class ProgressState:
     def struct(self):
         return _lib.QeProgress(
             self.G, self.group_offset, self.S, self.F, self.stride, _ptr(self.match),
-            _ptr(self.next), _ptr(self.pending), _ptr(self.flags), _ptr(self.istart),
-            _ptr(self.icount), _ptr(self.ibuf), _ptr(self.committed), _ptr(self.term_start),
+            _ptr(self.next), _ptr(self.pending), _ptr(self.peer), _ptr(self.ibuf),
+            _ptr(self.committed), _ptr(self.term_start),
             _ptr(self.first_index), _ptr(self.last_index), self.R, 0, _ptr(self.run_first),
             _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
             _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
             _ptr(self.snap_index), self.max_ents, 0)
 
-    ARRAYS = ("match", "next", "pending", "flags", "istart", "icount", "ibuf", "committed",
+    ARRAYS = ("match", "next", "pending", "peer", "ibuf", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
               "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
 
     def load_host(self, **arrays):
-        """numpy arrays (uint64 as uint64, masks/flags as uint8/uint16)."""
+        """numpy arrays (uint64 as uint64, masks as uint8/uint16, peer words
+        as uint32).  flags / istart / icount (uint8 arrays, any subset) are
+        packed into the peer words (absent fields 0)."""
+        fields = {k: arrays.pop(k) for k in ("flags", "istart", "icount") if k in arrays}
+        if fields:
+            n = max(np.asarray(v).size for v in fields.values())
+            z = np.zeros(n, np.uint32)
+            arrays["peer"] = pack_peer_word(fields.get("flags", z), fields.get("istart", z),
+                                            fields.get("icount", z))
         for k, a in arrays.items():
             dst = getattr(self, k)
             if dst is None or a is None:
@@ -350,6 +371,8 @@ class ProgressState:
                 a = a.view(np.int64)
             elif a.dtype == np.uint16:
                 a = a.view(np.int16)
+            elif a.dtype == np.uint32:
+                a = a.view(np.int32)
             a = a.reshape(-1)[: dst.numel()]
             dst[: a.size].copy_(torch.from_numpy(a.copy()).to(self.device))
         return self
@@ -363,7 +386,12 @@ class ProgressState:
                 continue
             a = t.cpu().numpy()
             out[k] = a.view(np.uint64) if a.dtype == np.int64 else (
-                a.view(np.uint16) if a.dtype == np.int16 else a)
+                a.view(np.uint16) if a.dtype == np.int16 else (
+                    a.view(np.uint32) if a.dtype == np.int32 else a))
+        w = out["peer"]
+        out["flags"] = (w & 0xFF).astype(np.uint8)
+        out["istart"] = ((w >> 8) & 0xFF).astype(np.uint8)
+        out["icount"] = ((w >> 16) & 0xFF).astype(np.uint8)
         return out
 
 
@@ -386,12 +414,32 @@ class PeerMsgs:
         self.msg_count = torch.zeros(n, dtype=torch.uint8, device=dev) if outputs else None
         self.msg_index = torch.zeros(n, dtype=torch.int64, device=dev) if outputs else None
         self.bytes_requested = None
+        # ReadIndex (ABI 3): None unless the caller tracks a pending request
+        self.read_acks = None   # [G] mask-typed, rw
+        self.read_ctx = None    # [G] mask-typed
+        self.read_ok = None     # [G] uint8 out
+
+    def track_reads(self, ps, acks, ctx=None):
+        """Attach ReadIndex state: acks / ctx are [G] mask tensors (or numpy
+        arrays); read_ok is allocated."""
+        md = mask_torch_dtype(ps.S)
+
+        def dev(x):
+            if x is None or torch.is_tensor(x):
+                return x
+            a = np.ascontiguousarray(x)
+            return torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).to(ps.device)
+        self.read_acks = dev(acks).to(md)
+        self.read_ctx = dev(ctx).to(md) if ctx is not None else None
+        self.read_ok = torch.zeros(ps.G, dtype=torch.uint8, device=ps.device)
+        return self
 
     def struct(self):
         return _lib.QePeerMsgs(_ptr(self.type), _ptr(self.index), _ptr(self.reject_hint),
                                _ptr(self.log_term), _ptr(self.sent), _ptr(self.bcast),
                                _ptr(self.snap), _ptr(self.timeout_now), _ptr(self.msg_count),
-                               _ptr(self.msg_index), _ptr(self.bytes_requested))
+                               _ptr(self.msg_index), _ptr(self.bytes_requested),
+                               _ptr(self.read_acks), _ptr(self.read_ctx), _ptr(self.read_ok))
 
 
 def progress_step(ps, msgs, stats=None):
@@ -413,19 +461,32 @@ def progress_bytes_requested(ps, msgs):
     return int(acct.item())
 
 
-def progress_send(ps, want, send_if_empty=False, max_ents=0):
+def progress_send(ps, want, send_if_empty=False):
+    """qe_progress_send: MaxSizePerMsg is ps.max_ents (ABI 3)."""
     sent = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
     snap = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
     p = ps.struct()
     check("qe_progress_send", _lib.lib().qe_progress_send(
-        C.byref(p), _ptr(want), int(bool(send_if_empty)), int(max_ents), _ptr(sent), _ptr(snap),
+        C.byref(p), _ptr(want), int(bool(send_if_empty)), _ptr(sent), _ptr(snap),
         _stream(ps.device)))
     return sent, snap
 
 
+def check_quorum(ps, quorum_active=None, stats=None):
+    """qe_check_quorum: MsgCheckQuorum on every group's leader
+    (raft/raft.go:997-1018) over the resident Progress words -> uint8[G]
+    QuorumActive (0 = the leader steps down)."""
+    if quorum_active is None:
+        quorum_active = torch.empty(ps.G, dtype=torch.uint8, device=ps.device)
+    p = ps.struct()
+    check("qe_check_quorum", _lib.lib().qe_check_quorum(C.byref(p), _ptr(quorum_active),
+                                                         _ptr(stats), _stream(ps.device)))
+    return quorum_active
+
+
 class ConfState:
     """Device-resident tracker.Config + ProgressMap key set of G groups in
-    slot form (qe_conf): slot_ids [G][S], slot masks for Voters[0],
+    slot form (qe_conf): slot_ids ID-major [S][G], slot masks for Voters[0],
     Voters[1], Learners, LearnersNext, Progress.IsLearner and tracked slots,
     and AutoLeave."""
 
@@ -448,7 +509,7 @@ class ConfState:
 
     def host(self):
         md = mask_np_dtype(self.S)
-        out = {"slot_ids": self.slot_ids.cpu().numpy().view(np.uint64).reshape(self.G, self.S),
+        out = {"slot_ids": self.slot_ids.cpu().numpy().view(np.uint64).reshape(self.S, self.G).T,
                "auto_leave": self.auto_leave.cpu().numpy()}
         for k in self.MASKS:
             out[k] = getattr(self, k).cpu().numpy().view(md)

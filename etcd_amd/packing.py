@@ -28,7 +28,10 @@ class PackedGroups:
         self.voted = np.zeros(G, md)
         self.granted = np.zeros(G, md)
         self.recent = np.zeros(G, md)
-        self.slot_ids = np.zeros((G, S), dtype=np.uint64)  # 0 = unused slot
+        # ID-major [S][G] (the C ABI's layout); slot_ids is its [G][S] view
+        self.slot_ids_sg = np.zeros((S, G), dtype=np.uint64)  # 0 = unused slot
+        self.slot_ids = self.slot_ids_sg.T
+        self.perm = None  # packed position -> caller group (qe_pack_order)
         self.joint = False
 
 
@@ -103,7 +106,9 @@ def _csr(lists):
 
 class ConfStates:
     """G raftpb.ConfState messages (raft/raftpb/raft.proto:115-130) in CSR
-    form: each field is (ids uint64, off uint64[G+1]) or None."""
+    form: each field is (ids uint64, off uint64[G+1]) or None.  `perm`
+    (uint64[G] or None) is the packing order: packed position i takes group
+    perm[i] (qe_pack_order)."""
 
     def __init__(self, voters, voters_outgoing=None, learners=None, learners_next=None,
                  auto_leave=None):
@@ -114,6 +119,20 @@ class ConfStates:
         self.learners_next = _csr(learners_next) if learners_next is not None else None
         self.auto_leave = (None if auto_leave is None else
                            np.ascontiguousarray(np.asarray(auto_leave, dtype=np.uint8)))
+        self.perm = None
+
+    @classmethod
+    def from_csr(cls, G, voters, voters_outgoing=None, learners=None, learners_next=None,
+                 auto_leave=None):
+        """Build from ready CSR pairs (ids uint64, off uint64[G+1]) without
+        going through Python lists (large batches)."""
+        c = cls.__new__(cls)
+        c.G = int(G)
+        c.voters, c.voters_outgoing = voters, voters_outgoing
+        c.learners, c.learners_next = learners, learners_next
+        c.auto_leave = auto_leave
+        c.perm = None
+        return c
 
     def struct(self):
         from ._lib import QeConfStateCSR
@@ -124,23 +143,41 @@ class ConfStates:
                               p(self.voters_outgoing, 0), p(self.voters_outgoing, 1),
                               p(self.learners, 0), p(self.learners, 1),
                               p(self.learners_next, 0), p(self.learners_next, 1),
-                              _np_ptr(self.auto_leave))
+                              _np_ptr(self.auto_leave), _np_ptr(self.perm))
 
 
 def _np_ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def pack_confstates(cs, num_slots):
-    """Native qe_pack_confstate -> PackedGroups (masks, slot_ids) + flags."""
+def pack_order(cs, num_slots):
+    """Native qe_pack_order: the shape-bucketed packing order (perm[i] = the
+    caller's group at packed position i) and the number of distinct shapes."""
     from . import _lib
+    perm = np.zeros(cs.G, dtype=np.uint64)
+    nshape = ctypes.c_uint64(0)
+    st = cs.struct()
+    _lib.check("qe_pack_order", _lib.lib().qe_pack_order(ctypes.byref(st), num_slots,
+                                                         _np_ptr(perm), ctypes.byref(nshape)))
+    return perm, int(nshape.value)
+
+
+def pack_confstates(cs, num_slots, bucketed=False):
+    """Native qe_pack_confstate -> PackedGroups (masks, slot_ids) + flags.
+    bucketed: pack in qe_pack_order's shape order (p.perm maps packed
+    positions back to cs's groups); otherwise in cs.perm's order (identity
+    when None)."""
+    from . import _lib
+    if bucketed:
+        cs.perm = pack_order(cs, num_slots)[0]
     p = PackedGroups(cs.G, num_slots)
+    p.perm = cs.perm
     flags = np.zeros(cs.G, dtype=np.uint32)
     nflag = ctypes.c_uint64(0)
     st = cs.struct()
     _lib.check("qe_pack_confstate", _lib.lib().qe_pack_confstate(
         ctypes.byref(st), num_slots, _np_ptr(p.inc), _np_ptr(p.out), _np_ptr(p.learner),
-        _np_ptr(p.slot_ids), _np_ptr(flags), ctypes.byref(nflag)))
+        _np_ptr(p.slot_ids_sg), _np_ptr(flags), ctypes.byref(nflag)))
     p.flags = flags
     p.num_flagged = int(nflag.value)
     p.joint = cs.voters_outgoing is not None
@@ -155,7 +192,7 @@ def pack_conf(cs, num_slots):
     from . import _lib
     G, S = cs.G, int(num_slots)
     md = np.uint8 if S <= 8 else np.uint16
-    arr = {"slot_ids": np.zeros(G * S, np.uint64), "auto_leave": np.zeros(G, np.uint8)}
+    arr = {"slot_ids": np.zeros(S * G, np.uint64), "auto_leave": np.zeros(G, np.uint8)}  # [S][G]
     for k in ("inc", "out", "learner", "learners_next", "is_learner", "tracked"):
         arr[k] = np.zeros(G, md)
     st = cs.struct()
@@ -171,7 +208,8 @@ def pack_conf(cs, num_slots):
 
 
 def pack_progress(p, progress, stride=None):
-    """progress: list (per group) of {id: Match} -> p.match via qe_pack_match."""
+    """progress: list (per caller group) of {id: Match} -> p.match (packed
+    order, through p.perm) via qe_pack_match."""
     from . import _lib
     ids, off = _csr([list(d.keys()) for d in progress])
     vals = np.fromiter((v for d in progress for v in d.values()), dtype=np.uint64,
@@ -180,20 +218,20 @@ def pack_progress(p, progress, stride=None):
     match = np.zeros(p.S * stride, dtype=np.uint64)
     unknown = ctypes.c_uint64(0)
     _lib.check("qe_pack_match", _lib.lib().qe_pack_match(
-        p.G, p.S, _np_ptr(p.slot_ids), _np_ptr(off), _np_ptr(ids), _np_ptr(vals),
-        _np_ptr(match), stride, ctypes.byref(unknown)))
+        p.G, p.S, _np_ptr(p.slot_ids_sg), _np_ptr(p.perm), _np_ptr(off), _np_ptr(ids),
+        _np_ptr(vals), _np_ptr(match), stride, ctypes.byref(unknown)))
     p.match = match.reshape(p.S, stride)[:, : p.G]
     return int(unknown.value)
 
 
 def pack_votes(p, votes):
-    """votes: list (per group) of [(id, bool), ...] in arrival order."""
+    """votes: list (per caller group) of [(id, bool), ...] in arrival order."""
     from . import _lib
     ids, off = _csr([[i for i, _ in v] for v in votes])
     vals = np.fromiter((int(b) for v in votes for _, b in v), dtype=np.uint8, count=int(off[-1]))
     _lib.check("qe_pack_votes", _lib.lib().qe_pack_votes(
-        p.G, p.S, _np_ptr(p.slot_ids), _np_ptr(off), _np_ptr(ids), _np_ptr(vals),
-        _np_ptr(p.voted), _np_ptr(p.granted)))
+        p.G, p.S, _np_ptr(p.slot_ids_sg), _np_ptr(p.perm), _np_ptr(off), _np_ptr(ids),
+        _np_ptr(vals), _np_ptr(p.voted), _np_ptr(p.granted)))
 
 
 def slot_lookup(p, group, ids):
@@ -202,5 +240,5 @@ def slot_lookup(p, group, ids):
     ids = np.ascontiguousarray(ids, dtype=np.uint64)
     out = np.zeros(len(ids), dtype=np.int8)
     _lib.check("qe_slot_lookup", _lib.lib().qe_slot_lookup(
-        p.G, p.S, _np_ptr(p.slot_ids), len(ids), _np_ptr(group), _np_ptr(ids), _np_ptr(out)))
+        p.G, p.S, _np_ptr(p.slot_ids_sg), len(ids), _np_ptr(group), _np_ptr(ids), _np_ptr(out)))
     return out

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 2  /* 2: qe_progress / qe_peer_msgs extended (stepLeader sends) */
+#define QE_ABI_VERSION 3  /* 3: see INTEGRATION.md "ABI 3" (layout changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -277,13 +277,27 @@ int qe_election_steps(const qe_election_state *st,
 
 /* ---- Progress state machine ------------------ */
 
-/* tracker.StateType (raft/tracker/state.go) and per-peer flag bits */
+/* tracker.StateType (raft/tracker/state.go) and the packed per-peer word
+ * (ABI 3: one u32 per peer replaces the flags / Inflights.start /
+ * Inflights.count byte rows of ABI 2, so a peer's small fields move in one
+ * 4-byte access):
+ *   bits 0-1   StateType (QE_PR_*)          bit 2  Progress.ProbeSent
+ *   bit 3      Progress.RecentActive        bits 4-7  reserved (0)
+ *   bits 8-15  Inflights.start              bits 16-23  Inflights.count
+ *   bits 24-31 reserved (0)
+ * Reserved bits must be 0 on input; the kernels write them as 0. */
 #define QE_PR_PROBE 0
 #define QE_PR_REPLICATE 1
 #define QE_PR_SNAPSHOT 2
-#define QE_PF_STATE 3u          /* flags & QE_PF_STATE = StateType           */
+#define QE_PF_STATE 3u          /* word & QE_PF_STATE = StateType            */
 #define QE_PF_PROBE_SENT 4u     /* Progress.ProbeSent                        */
 #define QE_PF_RECENT_ACTIVE 8u  /* Progress.RecentActive                     */
+#define QE_PW_START_SHIFT 8     /* Inflights.start = (word >> 8) & 0xFF       */
+#define QE_PW_COUNT_SHIFT 16    /* Inflights.count = (word >> 16) & 0xFF      */
+#define QE_PW_PACK(state, probe_sent, recent_active, start, count)                 \
+  ((uint32_t)(state) | ((probe_sent) ? QE_PF_PROBE_SENT : 0u) |                   \
+   ((recent_active) ? QE_PF_RECENT_ACTIVE : 0u) |                                 \
+   ((uint32_t)(start) << QE_PW_START_SHIFT) | ((uint32_t)(count) << QE_PW_COUNT_SHIFT))
 #define QE_MAX_INFLIGHT 255     /* Inflights capacity (MaxInflightMsgs)      */
 #define QE_MAX_LOG_RUNS 16      /* term runs of the leader-log model          */
 
@@ -313,9 +327,9 @@ typedef struct qe_progress {
   uint64_t stride;
   uint64_t *match, *next;       /* [S][stride]                               */
   uint64_t *pending_snapshot;   /* [S][stride]                               */
-  uint8_t *flags;               /* [S][stride] QE_PF_* bits                  */
-  uint8_t *infl_start;          /* [S][stride] Inflights.start               */
-  uint8_t *infl_count;          /* [S][stride] Inflights.count               */
+  uint32_t *peer;               /* [S][stride] packed per-peer word (ABI 3):
+                                   StateType, ProbeSent, RecentActive,
+                                   Inflights.start / count (QE_PW_*)         */
   uint64_t *infl_buf;           /* [S][F][stride] Inflights.buffer, entry-
                                    major: entry k of slot s of group g at
                                    (s*F + k)*stride + g                      */
@@ -361,13 +375,29 @@ typedef struct qe_peer_msgs {
                                    written only where msg_count > 0          */
   uint64_t *bytes_requested;    /* measurement aid, normally NULL: when set,
                                    an instrumented kernel adds the bytes the
-                                   round reads and writes (field granularity)
-                                   to *bytes_requested                       */
+                                   round reads and writes (field granularity,
+                                   the rules of DESIGN.md §3) to
+                                   *bytes_requested                          */
+  /* ABI 3: ReadIndex under ReadOnlySafe (raft.go:1296-1309,
+   * read_only.go:68-76).  NULL read_acks = no pending request tracked. */
+  void *read_acks;              /* [G] rw mask-typed: acks of the group's
+                                   pending ReadIndex request (recvAck; the
+                                   leader's own ack is set by the caller at
+                                   addRequest, raft.go:1834-1836)           */
+  const void *read_ctx;         /* [G] mask-typed: slots whose
+                                   MsgHeartbeatResp carries the request's
+                                   context (len(m.Context) > 0); NULL =
+                                   every heartbeat response does            */
+  uint8_t *read_ok;             /* [G] out (may be NULL): 1 when a response
+                                   of this round made VoteResult(acks) ==
+                                   VoteWon (readOnly.advance releases the
+                                   request; later responses of the round
+                                   find it gone and record nothing)         */
 } qe_peer_msgs;
 
 /* Leader-side handling of one message per peer, slots in ascending order
  * (stepLeader, raft/raft.go:1099-1338), with every send the reference makes
- * while handling the message executed in place:
+ * while handling the message executed in place (max_ents from p):
  *   MsgAppResp reject: RecentActive; findConflictByTerm (raft/log.go:147-168)
  *     when LogTerm > 0; MaybeDecrTo (progress.go:170-193) -> Replicate ->
  *     BecomeProbe, sendAppend.
@@ -378,7 +408,9 @@ typedef struct qe_peer_msgs {
  *     `for maybeSendAppend(from, false) {}`; MsgTimeoutNow to the lead
  *     transferee once its Match == lastIndex (raft.go:1275-1281).
  *   MsgHeartbeatResp: RecentActive, ProbeSent = false, FreeFirstOne when the
- *     inflights are full, sendAppend if Match < lastIndex.
+ *     inflights are full, sendAppend if Match < lastIndex; with read_acks,
+ *     a response carrying the request's context: recvAck, and the request
+ *     is released once Voters.VoteResult(acks) == VoteWon.
  *   MsgSnapStatus (StateSnapshot only): reject -> PendingSnapshot = 0;
  *     BecomeProbe; ProbeSent = true (raft.go:1310-1331).
  *   MsgUnreachable: Replicate -> BecomeProbe (raft.go:1332-1338).
@@ -389,6 +421,19 @@ typedef struct qe_peer_msgs {
 int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
                      void *stream);
 
+/* MsgCheckQuorum on every group's leader (stepLeader, raft/raft.go:997-1018):
+ * the leader's own Progress (self_slot, when tracked) becomes RecentActive;
+ * quorum_active[g] = ProgressTracker.QuorumActive() (raft/tracker/
+ * tracker.go:215-225: Voters.VoteResult with each voter's vote = its
+ * RecentActive, a voter without a Progress missing) -- 0 means the leader
+ * steps down (becomeFollower); then RecentActive = false for every tracked
+ * slot but the leader's (prs.Visit, raft.go:1013-1017).  Reads inc_mask /
+ * out_mask / tracked / self_slot and the peer words of p, rewrites only the
+ * words that change.  quorum_active may be NULL.  stats: groups, stepdowns
+ * (QE_STAT_STEPDOWNS), checksum. */
+int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stats,
+                    void *stream);
+
 /* raft.sendAppend / maybeSendAppend(to, send_if_empty) once for the slots of
  * want[g] (raft.go:432-492; bcastAppend after a proposal is want = every
  * tracked slot but the leader's, send_if_empty = 1): paused peers get
@@ -397,11 +442,12 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
  * send_if_empty -- this check comes before the snapshot branch; Next >
  * lastIndex sends an empty MsgApp; Next < firstIndex sends a MsgSnap to a
  * recently active peer (BecomeSnapshot(snap_index)); otherwise up to
- * max_ents entries (0 = noLimit): Replicate -> OptimisticUpdate +
- * Inflights.Add, Probe -> ProbeSent.  sent / snap (mask-typed [G], may be
- * NULL) report the outcome. */
+ * p->max_ents entries (0 = noLimit; ABI 3 takes MaxSizePerMsg from p, as
+ * qe_progress_step does): Replicate -> OptimisticUpdate + Inflights.Add,
+ * Probe -> ProbeSent.  sent / snap (mask-typed [G], may be NULL) report the
+ * outcome. */
 int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
-                     uint32_t max_ents, void *sent, void *snap, void *stream);
+                     void *sent, void *snap, void *stream);
 
 /* ---- sparse MsgAppResp deltas ------------------------------------------ */
 
@@ -429,6 +475,10 @@ typedef struct qe_confstate_csr {
   const uint64_t *learners, *learners_off;
   const uint64_t *learners_next, *learners_next_off;
   const uint8_t *auto_leave;    /* [G] ConfState.auto_leave (ABI 2; NULL = false) */
+  const uint64_t *perm;         /* ABI 3: packed position i takes the caller's
+                                   group perm[i] (qe_pack_order); NULL =
+                                   identity.  Every packer output is in
+                                   packed order. */
 } qe_confstate_csr;
 
 /* group_flags bits reported by qe_pack_confstate */
@@ -437,28 +487,50 @@ typedef struct qe_confstate_csr {
 #define QE_PACK_LEARNER_NEXT_NOT_OUTGOING 4u /* confchange.go:299-306 violated   */
 #define QE_PACK_ZERO_ID 8u                 /* ID 0 is raft.None                   */
 
+/* Shape bucketing (ABI 3; the order the JointConfig kernels want, DESIGN.md
+ * §2): perm[i] = the caller's group placed at packed position i, groups
+ * sorted by configuration shape -- (|Voters[0] u Voters[1]|, |Voters[0]|,
+ * |Voters[1]|, learners) ascending, caller order within a shape (stable);
+ * groups the packer would flag sort last.  With cs->perm = perm the groups
+ * of one shape fill consecutive 64-group tiles: every lane of a wave has its
+ * voters in the same low slots (voters are placed first), so the joint
+ * commit kernel fetches exactly the union's slot rows.  Quorum results are
+ * order-free per group; the host maps packed outputs back through perm
+ * (qe_collect does it on the device).  *num_shapes (optional) = distinct
+ * shapes.  perm is a HOST array of num_groups entries. */
+int qe_pack_order(const qe_confstate_csr *cs, uint32_t num_slots, uint64_t *perm,
+                  uint64_t *num_shapes);
+
 /* Slot assignment: voters of both halves ascending, then learners ascending.
- * Writes the three masks (mask-typed, may be NULL), slot_ids[G][S] (0 =
+ * Writes the three masks (mask-typed, may be NULL), slot_ids (ABI 3:
+ * ID-major [S][G], slot s of packed group i at slot_ids[s*G + i]; 0 =
  * unused slot) and optional per-group flags; *num_flagged counts flagged
- * groups.  Multi-threaded (qe_pack_threads). */
+ * groups.  Outputs are in packed order (cs->perm).  Multi-threaded
+ * (qe_pack_threads). */
 int qe_pack_confstate(const qe_confstate_csr *cs, uint32_t num_slots, void *inc_mask,
                       void *out_mask, void *learner_mask, uint64_t *slot_ids,
                       uint32_t *group_flags, uint64_t *num_flagged);
 
-/* Progress.Match of each peer (CSR prog_ids/prog_match) into match[S][stride]
- * (host); peers without a slot are counted in *num_unknown. */
+/* Progress.Match of each peer (CSR prog_ids/prog_match, in the caller's
+ * group order) into match[S][stride] (host, packed order); packed group i
+ * reads CSR row perm[i] (NULL = identity; ABI 3).  slot_ids as written by
+ * qe_pack_confstate ([S][G]).  Peers without a slot are counted in
+ * *num_unknown. */
 int qe_pack_match(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
-                  const uint64_t *prog_off, const uint64_t *prog_ids,
+                  const uint64_t *perm, const uint64_t *prog_off, const uint64_t *prog_ids,
                   const uint64_t *prog_match, uint64_t *match, uint64_t stride,
                   uint64_t *num_unknown);
 
-/* ProgressTracker.Votes (CSR vote_ids / vote_vals 0|1) into voted/granted
- * bitmaps; the first vote per peer sticks (tracker.go:258-263). */
+/* ProgressTracker.Votes (CSR vote_ids / vote_vals 0|1, caller order) into
+ * voted/granted bitmaps (packed order, through perm as qe_pack_match); the
+ * first vote per peer sticks (tracker.go:258-263). */
 int qe_pack_votes(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
-                  const uint64_t *vote_off, const uint64_t *vote_ids, const uint8_t *vote_vals,
-                  void *voted, void *granted);
+                  const uint64_t *perm, const uint64_t *vote_off, const uint64_t *vote_ids,
+                  const uint8_t *vote_vals, void *voted, void *granted);
 
-/* (group, id) -> slot (-1 if the id has no slot) for routing deltas. */
+/* (packed group, id) -> slot (-1 if the id has no slot) for routing deltas;
+ * slot_ids [S][G].  A caller that bucketed maps its group id to the packed
+ * position with the inverse of perm. */
 int qe_slot_lookup(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot_ids,
                    uint64_t n, const uint64_t *group, const uint64_t *id, int8_t *slot);
 
@@ -498,13 +570,15 @@ int qe_pack_threads(int n);
  * is tracked when it holds a Progress (ProgressMap key); Voters[0],
  * Voters[1], Learners and LearnersNext are slot masks ([G], u8 for
  * num_slots <= 8, else u16) over tracked slots; is_learner is
- * Progress.IsLearner.  slot_ids is [G][S] as written by qe_pack_confstate;
- * the ids of untracked slots are ignored on input and written as 0. */
+ * Progress.IsLearner.  slot_ids is ID-major [S][G] (ABI 3: slot s of group
+ * g at slot_ids[s*G + g]) as written by qe_pack_confstate, so a change
+ * rewrites only the changed slot's row; the ids of untracked slots are
+ * ignored on input and written as 0. */
 typedef struct qe_conf {
   uint64_t num_groups;
   uint32_t num_slots;
   uint32_t reserved;
-  uint64_t *slot_ids;           /* [G][S]                                   */
+  uint64_t *slot_ids;           /* [S][G]                                   */
   void *inc_mask, *out_mask;    /* Voters[0], Voters[1]                     */
   void *learner_mask;           /* Learners                                 */
   void *learners_next_mask;     /* LearnersNext                             */
@@ -555,9 +629,11 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
 
 /* ---- Ready deltas ------------------------------------------------------ */
 
-/* The groups a batch step changed, as a dense list in ascending group order:
- * for every g with flags[g] != 0, out_groups[i] = group_offset + g and (when
- * out_values is non-NULL) out_values[i] = values[g]; *out_count (device) =
+/* The groups a batch step changed, as a dense list in ascending position
+ * order: for every g with flags[g] != 0, out_groups[i] = group_offset + g
+ * (ABI 3: group_offset + perm[g] when perm is non-NULL -- the caller's group
+ * id of a shape-bucketed batch, qe_pack_order) and (when out_values is
+ * non-NULL) out_values[i] = values[g]; *out_count (device) =
  * their number.  raft reports a HardState only when it changed
  * (raft/node.go:571-573 newReady, raft/rawnode.go:152-176 prevHardSt): with
  * flags = qe_replication_round's `adv` and values = `committed` this is the
@@ -566,9 +642,9 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
  * qe_collect_scratch_bytes(num_groups) bytes of device memory, 8-B aligned.
  * All pointers are device pointers; stream-ordered. */
 size_t qe_collect_scratch_bytes(uint64_t num_groups);
-int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint8_t *flags,
-               const uint64_t *values, uint64_t *out_groups, uint64_t *out_values,
-               uint64_t *out_count, void *scratch, void *stream);
+int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint64_t *perm,
+               const uint8_t *flags, const uint64_t *values, uint64_t *out_groups,
+               uint64_t *out_values, uint64_t *out_count, void *scratch, void *stream);
 
 /* ---- statistics -------------------------------------------------------- */
 

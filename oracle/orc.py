@@ -59,6 +59,7 @@ def _declare(L):
         "orc_soa_run": (dbl, [u64, u32, u64, vp, vp, vp, vp, vp, vp, vp, i32, i32]),
         "orc_max_threads": (i32, []),
         "orc_progress_step_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcMsgs), vp, i32]),
+        "orc_check_quorum_batch": (None, [C.POINTER(OrcProg), vp, vp]),
         "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
@@ -160,8 +161,8 @@ class OrcProg(C.Structure):
     _fields_ = [
         ("G", C.c_uint64), ("goff", C.c_uint64), ("S", C.c_uint32), ("F", C.c_uint32),
         ("stride", C.c_uint64), ("match", C.c_void_p), ("next", C.c_void_p),
-        ("pending", C.c_void_p), ("flags", C.c_void_p), ("istart", C.c_void_p),
-        ("icount", C.c_void_p), ("ibuf", C.c_void_p), ("committed", C.c_void_p),
+        ("pending", C.c_void_p), ("pw", C.c_void_p), ("ibuf", C.c_void_p),
+        ("committed", C.c_void_p),
         ("term_start", C.c_void_p), ("first_index", C.c_void_p), ("last_index", C.c_void_p),
         ("R", C.c_uint32), ("reserved", C.c_uint32), ("run_first", C.c_void_p),
         ("run_term", C.c_void_p), ("run_count", C.c_void_p), ("inc", C.c_void_p),
@@ -175,13 +176,26 @@ class OrcMsgs(C.Structure):
     _fields_ = [("type", C.c_void_p), ("index", C.c_void_p), ("hint", C.c_void_p),
                 ("logterm", C.c_void_p), ("sent", C.c_void_p), ("bcast", C.c_void_p),
                 ("snap", C.c_void_p), ("timeout_now", C.c_void_p), ("msg_count", C.c_void_p),
-                ("msg_index", C.c_void_p)]
+                ("msg_index", C.c_void_p), ("read_acks", C.c_void_p), ("read_ctx", C.c_void_p),
+                ("read_ok", C.c_void_p), ("bytes", C.c_void_p)]
+
+
+PF_STATE, PF_PROBE_SENT, PF_RECENT_ACTIVE = 3, 4, 8
+
+
+def pack_word(flags, start, count):
+    """Packed per-peer word (QE_PW_*): the flag bits (StateType, ProbeSent,
+    RecentActive), Inflights.start << 8, Inflights.count << 16."""
+    return (np.asarray(flags, np.uint32) & 0xF) | (np.asarray(start, np.uint32) << 8) | \
+        (np.asarray(count, np.uint32) << 16)
 
 
 class ProgressBatch:
     """Host mirror of qe_progress (numpy arrays, same layout).  Optional
     per-group arrays (tracked, self_slot, lead_transferee, snap_index) are
-    None unless set."""
+    None unless set.  `pw` holds the packed per-peer words; `flags`,
+    `istart`, `icount` are read-only views of their fields (set_peer
+    rewrites them)."""
 
     OPTIONAL = ("inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
 
@@ -193,9 +207,7 @@ class ProgressBatch:
         self.match = np.zeros(n, np.uint64)
         self.next = np.ones(n, np.uint64)
         self.pending = np.zeros(n, np.uint64)
-        self.flags = np.zeros(n, np.uint8)
-        self.istart = np.zeros(n, np.uint8)
-        self.icount = np.zeros(n, np.uint8)
+        self.pw = np.zeros(n, np.uint32)
         self.ibuf = np.zeros(S * F * self.stride, np.uint64)
         self.committed = np.zeros(G, np.uint64)
         self.term_start = np.zeros(G, np.uint64)
@@ -207,6 +219,25 @@ class ProgressBatch:
         for k in self.OPTIONAL:
             setattr(self, k, None)
 
+    @property
+    def flags(self):
+        return (self.pw & 0xFF).astype(np.uint8)
+
+    @property
+    def istart(self):
+        return ((self.pw >> 8) & 0xFF).astype(np.uint8)
+
+    @property
+    def icount(self):
+        return ((self.pw >> 16) & 0xFF).astype(np.uint8)
+
+    def set_peer(self, flags=None, istart=None, icount=None):
+        """Rewrite fields of the packed words (None keeps a field)."""
+        f = self.flags if flags is None else np.broadcast_to(flags, self.pw.shape)
+        st = self.istart if istart is None else np.broadcast_to(istart, self.pw.shape)
+        ct = self.icount if icount is None else np.broadcast_to(icount, self.pw.shape)
+        self.pw[:] = pack_word(f, st, ct)
+
     def copy(self):
         c = ProgressBatch.__new__(ProgressBatch)
         for k, v in self.__dict__.items():
@@ -215,7 +246,7 @@ class ProgressBatch:
 
     def struct(self, goff=0):
         return OrcProg(self.G, goff, self.S, self.F, self.stride, P(self.match), P(self.next),
-                       P(self.pending), P(self.flags), P(self.istart), P(self.icount),
+                       P(self.pending), P(self.pw),
                        P(self.ibuf), P(self.committed), P(self.term_start), P(self.first_index),
                        P(self.last_index), self.R, 0, P(self.run_first), P(self.run_term),
                        P(self.run_count), P(self.inc), P(self.out), P(self.tracked),
@@ -234,22 +265,45 @@ class StepOut:
         self.timeout_now = np.zeros(pb.G, md)
         self.msg_count = np.zeros(pb.S * pb.stride, np.uint8)
         self.msg_index = np.zeros(pb.S * pb.stride, np.uint64)
+        self.read_ok = np.zeros(pb.G, np.uint8)
         self.stats = np.zeros(NSTAT, np.uint64)
+        self.bytes = np.zeros(1, np.uint64)
 
 
-def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0):
-    """One round of stepLeader message handling (oracle).  Returns StepOut."""
+def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0, read_acks=None,
+                  read_ctx=None, outputs=True, count_bytes=False):
+    """One round of stepLeader message handling (oracle).  Returns StepOut.
+    read_acks (mask array, updated in place) / read_ctx: the ReadIndex
+    request of each group (ABI 3).  outputs=False leaves the optional outputs
+    NULL (as a kernel call without them); count_bytes: o.bytes[0] = the
+    round's algorithmic bytes by the accounting rules."""
     o = StepOut(pb)
-    m = OrcMsgs(P(mtype), P(mindex), P(mhint), P(mlogterm), P(o.sent), P(o.bcast), P(o.snap),
-                P(o.timeout_now), P(o.msg_count), P(o.msg_index))
+    opt = (lambda a: P(a)) if outputs else (lambda a: None)
+    m = OrcMsgs(P(mtype), P(mindex), P(mhint), P(mlogterm), opt(o.sent), opt(o.bcast),
+                opt(o.snap), opt(o.timeout_now), opt(o.msg_count), opt(o.msg_index),
+                P(read_acks), P(read_ctx) if read_acks is not None else None,
+                P(o.read_ok) if (read_acks is not None and outputs) else None,
+                P(o.bytes) if count_bytes else None)
     s = pb.struct(goff)
     lib().orc_progress_step_batch(C.byref(s), C.byref(m), P(o.stats), threads)
     return o
 
 
-def progress_send(pb, want, send_if_empty, max_ents):
+def progress_send(pb, want, send_if_empty, max_ents=None):
+    """max_ents: None = pb.max_ents (ABI 3 takes MaxSizePerMsg from the state)."""
     sent = np.zeros(pb.G, mask_dtype(pb.S))
     snap = np.zeros(pb.G, mask_dtype(pb.S))
     s = pb.struct()
-    lib().orc_progress_send_batch(C.byref(s), P(want), send_if_empty, max_ents, P(sent), P(snap))
+    me = pb.max_ents if max_ents is None else max_ents
+    lib().orc_progress_send_batch(C.byref(s), P(want), send_if_empty, me, P(sent), P(snap))
     return sent, snap
+
+
+def check_quorum(pb, goff=0):
+    """MsgCheckQuorum on every group's leader (oracle).  Returns (quorum
+    active uint8[G], stats)."""
+    qa = np.zeros(pb.G, np.uint8)
+    stats = np.zeros(NSTAT, np.uint64)
+    s = pb.struct(goff)
+    lib().orc_check_quorum_batch(C.byref(s), P(qa), P(stats))
+    return qa, stats

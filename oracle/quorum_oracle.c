@@ -851,25 +851,34 @@ typedef struct orc_pr {
   uint32_t start, count, size; /* Inflights (raft/tracker/inflights.go:22-36) */
   uint64_t *buf;               /* strided view: buf[k * bstride] */
   uint64_t bstride;
+  uint32_t reset;              /* ResetState ran this round (byte accounting) */
+  uint64_t *acct;              /* byte accounting sink, or NULL             */
 } orc_pr;
 
 static inline uint64_t *ib(orc_pr *p, uint32_t k) { return &p->buf[(uint64_t)k * p->bstride]; }
 
-/* inflights.go:55-71 Add */
+/* inflights.go:55-71 Add (accounting: the 8-B entry written) */
 static void infl_add(orc_pr *p, uint64_t x) {
   uint32_t nx = p->start + p->count;
   if (nx >= p->size) nx -= p->size;
   *ib(p, nx) = x;
   p->count++;
+  if (p->acct) *p->acct += 8;
 }
-/* inflights.go:87-113 FreeLE */
+/* inflights.go:87-113 FreeLE (accounting: every entry the loop reads,
+ * min(count, freed + 1) of them) */
 static void infl_free_le(orc_pr *p, uint64_t to) {
-  if (p->count == 0 || to < *ib(p, p->start)) return;
+  if (p->count == 0) return;
+  if (to < *ib(p, p->start)) {
+    if (p->acct) *p->acct += 8;
+    return;
+  }
   uint32_t idx = p->start, i;
   for (i = 0; i < p->count; i++) {
     if (to < *ib(p, idx)) break;
     if (++idx >= p->size) idx -= p->size;
   }
+  if (p->acct) *p->acct += 8 * (uint64_t)(i < p->count ? i + 1 : i);
   p->count -= i;
   p->start = idx;
   if (p->count == 0) p->start = 0;
@@ -878,6 +887,7 @@ static int infl_full(const orc_pr *p) { return p->count == p->size; }
 
 /* progress.go:84-90 ResetState */
 static void pr_reset_state(orc_pr *p, uint32_t st) {
+  p->reset = 1;
   p->probe_sent = 0;
   p->pending = 0;
   p->state = st;
@@ -961,15 +971,17 @@ uint64_t orc_find_conflict_by_term(uint32_t nruns, const uint64_t *first, const 
 }
 
 /* The leader-side state of G groups (mirrors qe_progress of
- * include/etcd_quorum.h, ABI 2) and one round of peer messages (mirrors
+ * include/etcd_quorum.h, ABI 3) and one round of peer messages (mirrors
  * qe_peer_msgs).  Slot s of group g lives at [s*stride + g]; entry k of
- * that peer's Inflights ring at ibuf[(s*F + k)*stride + g] (entry-major). */
+ * that peer's Inflights ring at ibuf[(s*F + k)*stride + g] (entry-major).
+ * pw is the packed per-peer word: StateType bits 0-1, ProbeSent bit 2,
+ * RecentActive bit 3, Inflights.start bits 8-15, Inflights.count 16-23. */
 typedef struct orc_prog {
   uint64_t G, goff;
   uint32_t S, F;
   uint64_t stride;
   uint64_t *match, *next, *pending;
-  uint8_t *flags, *istart, *icount;
+  uint32_t *pw;
   uint64_t *ibuf;
   uint64_t *committed;
   const uint64_t *term_start, *first_index, *last_index;
@@ -993,35 +1005,43 @@ typedef struct orc_msgs {
   void *timeout_now;   /* [G] slots sent MsgTimeoutNow                    */
   uint8_t *msg_count;  /* [S][stride] messages sent to the peer           */
   uint64_t *msg_index; /* [S][stride] m.Index of the first of them        */
+  void *read_acks;     /* [G] rw ReadIndex acks (NULL: none tracked)      */
+  const void *read_ctx;/* [G] heartbeat responses carrying the context    */
+  uint8_t *read_ok;    /* [G] out: request released this round            */
+  uint64_t *bytes;     /* byte accounting (DESIGN.md §3 rules), or NULL   */
 } orc_msgs;
 
 /* message kinds (qe_peer_msgs.type) */
 enum { M_NONE = 0, M_APP_RESP, M_APP_RESP_REJECT, M_HEARTBEAT_RESP, M_SNAP_STATUS,
        M_SNAP_STATUS_REJECT, M_UNREACHABLE };
 
+static uint32_t pr_word(const orc_pr *p) {
+  return p->state | (p->probe_sent ? PF_PROBE_SENT : 0) | (p->recent_active ? PF_RECENT_ACTIVE : 0) |
+         (p->start << 8) | (p->count << 16);
+}
 static void pr_load2(orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   uint64_t off = s * a->stride + g;
+  uint32_t w = a->pw[off];
   p->match = a->match[off];
   p->next = a->next[off];
   p->pending = a->pending[off];
-  p->state = a->flags[off] & PF_STATE;
-  p->probe_sent = (a->flags[off] & PF_PROBE_SENT) != 0;
-  p->recent_active = (a->flags[off] & PF_RECENT_ACTIVE) != 0;
-  p->start = a->istart[off];
-  p->count = a->icount[off];
+  p->state = w & PF_STATE;
+  p->probe_sent = (w & PF_PROBE_SENT) != 0;
+  p->recent_active = (w & PF_RECENT_ACTIVE) != 0;
+  p->start = (w >> 8) & 0xFFu;
+  p->count = (w >> 16) & 0xFFu;
   p->size = a->F;
   p->buf = a->ibuf + (uint64_t)s * a->F * a->stride + g; /* entry k at buf[k*stride] */
   p->bstride = a->stride;
+  p->reset = 0;
+  p->acct = NULL;
 }
 static void pr_store2(const orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   uint64_t off = s * a->stride + g;
   a->match[off] = p->match;
   a->next[off] = p->next;
   a->pending[off] = p->pending;
-  a->flags[off] = (uint8_t)(p->state | (p->probe_sent ? PF_PROBE_SENT : 0) |
-                            (p->recent_active ? PF_RECENT_ACTIVE : 0));
-  a->istart[off] = (uint8_t)p->start;
-  a->icount[off] = (uint8_t)p->count;
+  a->pw[off] = pr_word(p);
 }
 
 /* Per-group context of one round: the log model and the message record. */
@@ -1078,11 +1098,13 @@ static int send_append(orc_gctx *c, orc_pr *p, uint32_t s, int send_if_empty) {
   return 1;
 }
 
-/* Two per-group parts: (commit, bcast count) and the sent mask (the GPU
- * adds them in its commit pass and its peer pass). */
-uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast) {
+/* Per-group parts: (commit, bcast count), the sent mask and a released
+ * ReadIndex request. */
+uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast,
+                           uint32_t released) {
   return orc_mix64((gid * PHI) ^ committed ^ ((uint64_t)bcast << 62)) +
-         orc_mix64((gid * PHI) ^ ((uint64_t)send << 40) ^ 0xD1B54A32D192ED03ull);
+         orc_mix64((gid * PHI) ^ ((uint64_t)send << 40) ^ 0xD1B54A32D192ED03ull) +
+         (released ? orc_mix64((gid * PHI) ^ 0x8CB92BA72F3D8DD7ull) : 0);
 }
 
 /* One round of leader-side message handling per group, messages taken in
@@ -1114,6 +1136,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
   uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
   uint32_t full = (1u << S) - 1u;
   uint64_t st[NSTAT];
+  uint64_t bytes = 0;
   memset(st, 0, sizeof(st));
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
@@ -1121,6 +1144,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
 #pragma omp parallel
   {
     uint64_t ls[NSTAT];
+    uint64_t lbytes = 0;
     memset(ls, 0, sizeof(ls));
 #pragma omp for schedule(static)
     for (int64_t gi = 0; gi < (int64_t)a->G; gi++) {
@@ -1146,13 +1170,27 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         rf[r] = a->run_first[r * a->stride + g];
         rt[r] = a->run_term[r * a->stride + g];
       }
+      /* ReadOnlySafe: the pending request's acks (read_only.go:68-76) */
+      uint32_t acks = m->read_acks ? ld_mask(m->read_acks, mb, g) & full : 0, acks0 = acks;
+      uint32_t rctx = (m->read_acks && m->read_ctx) ? ld_mask(m->read_ctx, mb, g) & full : full;
+      int released = 0;
+      /* byte accounting (only when m->bytes): everything the round needs,
+       * field granularity, each once */
+      uint64_t B = 0;
       orc_pr prs[16];
-      uint64_t vals[16];
+      uint64_t vals[16], match0[16], next0[16], pend0[16];
+      uint32_t word0[16], state0[16];
       for (uint32_t s = 0; s < S; s++) {
         pr_load2(&prs[s], a, s, g);
+        if (m->bytes) prs[s].acct = &B;
+        match0[s] = prs[s].match;
+        next0[s] = prs[s].next;
+        pend0[s] = prs[s].pending;
+        word0[s] = a->pw[s * a->stride + g];
+        state0[s] = prs[s].state;
         if (m->msg_count) m->msg_count[s * a->stride + g] = 0;
       }
-      uint32_t bc = 0, tnow = 0;
+      uint32_t bc = 0, tnow = 0, runs_read = 0;
       for (uint32_t s = 0; s < S; s++) {
         if (!((trk >> s) & 1u)) continue; /* no Progress: dropped */
         uint64_t off = s * a->stride + g;
@@ -1161,8 +1199,10 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         if (ty == M_APP_RESP_REJECT) {
           p->recent_active = 1;
           uint64_t probe = m->hint[off];
-          if (m->logterm[off] > 0)
+          if (m->logterm[off] > 0) {
             probe = orc_find_conflict_by_term(nr, rf, rt, li, m->hint[off], m->logterm[off]);
+            runs_read = 1;
+          }
           if (pr_maybe_decr_to(p, m->index[off], probe)) {
             if (p->state == PR_REPLICATE) pr_become_probe(p);
             send_append(&c, p, s, 1);
@@ -1200,6 +1240,13 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
           p->probe_sent = 0;
           if (p->state == PR_REPLICATE && infl_full(p)) infl_free_le(p, *ib(p, p->start));
           if (p->match < li) send_append(&c, p, s, 1);
+          /* :1296-1309: ReadOnlySafe with a context -> recvAck; a won vote
+           * releases the request (readOnly.advance removes it, so a later
+           * response's recvAck returns nil and records nothing) */
+          if (m->read_acks && !released && ((rctx >> s) & 1u)) {
+            acks |= 1u << s;
+            if (orc_joint_vote(mi, mo, acks, acks) == VOTE_WON) released = 1;
+          }
         } else if (ty == M_SNAP_STATUS || ty == M_SNAP_STATUS_REJECT) {
           if (p->state == PR_SNAPSHOT) {
             if (ty == M_SNAP_STATUS_REJECT) p->pending = 0;
@@ -1210,19 +1257,99 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
           if (p->state == PR_REPLICATE) pr_become_probe(p);
         }
       }
+      if (m->bytes) {
+        /* per group: masks, log model, commit, ReadIndex masks */
+        B += (a->inc ? mb : 0) + (a->out ? mb : 0) + (a->tracked ? mb : 0) + (a->self_slot ? 1 : 0) +
+             (a->lead_transferee ? 1 : 0) + 32 + (a->snap_index ? 8 : 0) +
+             (m->read_acks ? mb : 0) + ((m->read_acks && m->read_ctx) ? mb : 0);
+        for (uint32_t s = 0; s < S; s++) {
+          uint64_t off = s * a->stride + g;
+          int tr = (trk >> s) & 1u;
+          uint32_t ty = tr ? m->type[off] : 0;
+          int msg = ty >= M_APP_RESP && ty <= M_UNREACHABLE;
+          int touched = tr && (msg || (bc > 0 && s != self));
+          const orc_pr *p = &prs[s];
+          B += 8;                                             /* Match (the commit pass) */
+          B += tr ? 1 : 0;                                    /* message kind            */
+          B += (ty == M_APP_RESP || ty == M_APP_RESP_REJECT) ? 8 : 0; /* m.Index         */
+          if (touched) {
+            B += 12;                                          /* Next + the packed word  */
+            B += ty == M_APP_RESP_REJECT ? 16 : 0;            /* RejectHint, LogTerm     */
+            B += state0[s] == PR_SNAPSHOT ? 8 : 0;            /* PendingSnapshot         */
+            B += p->match != match0[s] ? 8 : 0;
+            B += p->next != next0[s] ? 8 : 0;
+            B += (p->reset || (state0[s] == PR_SNAPSHOT && p->pending != pend0[s])) ? 8 : 0;
+            B += pr_word(p) != word0[s] ? 4 : 0;
+          }
+          B += m->msg_count ? 1 : 0;
+          B += (m->msg_index && m->msg_count && m->msg_count[off]) ? 8 : 0;
+        }
+        B += runs_read ? 1 + 16 * (uint64_t)nr : 0;           /* the term-run table      */
+        B += cm != c0 ? 8 : 0;
+        B += (m->sent ? mb : 0) + (m->snap ? mb : 0) + (m->timeout_now ? mb : 0) +
+             (m->bcast ? 1 : 0) + (m->read_ok ? 1 : 0);
+        B += (m->read_acks && acks != acks0) ? mb : 0;
+        lbytes += B;
+      }
       for (uint32_t s = 0; s < S; s++) pr_store2(&prs[s], a, s, g);
       a->committed[g] = cm;
       if (m->sent) st_mask(m->sent, mb, g, c.sent);
       if (m->snap) st_mask(m->snap, mb, g, c.snapm);
       if (m->timeout_now) st_mask(m->timeout_now, mb, g, tnow);
       if (m->bcast) m->bcast[g] = (uint8_t)bc;
+      if (m->read_acks) st_mask(m->read_acks, mb, g, acks);
+      if (m->read_ok) m->read_ok[g] = (uint8_t)released;
       ls[ST_GROUPS] += 1;
       ls[ST_COMMIT_SUM] += cm;
       ls[ST_COMMIT_ADVANCED] += (cm != c0);
-      ls[ST_CHECKSUM] += orc_checksum_step(a->goff + g, cm, c.sent, bc);
+      ls[ST_READ_RELEASED] += released;
+      ls[ST_CHECKSUM] += orc_checksum_step(a->goff + g, cm, c.sent, bc, released);
     }
 #pragma omp critical
-    for (int k = 0; k < NSTAT; k++) st[k] += ls[k];
+    {
+      for (int k = 0; k < NSTAT; k++) st[k] += ls[k];
+      bytes += lbytes;
+    }
+  }
+  if (stats)
+    for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+  if (m->bytes) *m->bytes += bytes;
+}
+
+/* MsgCheckQuorum on each group's leader (stepLeader, raft/raft.go:997-1018):
+ * `if pr := r.prs.Progress[r.id]; pr != nil { pr.RecentActive = true }`;
+ * `!r.prs.QuorumActive()` -> becomeFollower (qa[g] = 0); then
+ * `r.prs.Visit(... if id != r.id { pr.RecentActive = false })`.
+ * QuorumActive (raft/tracker/tracker.go:215-225) over the Progress map:
+ * votes[id] = RecentActive for every Progress that is not a learner (a
+ * learner is never a voter, confchange.go:308-318, so the voters' Progress
+ * entries are the votes), VoteResult over Voters -- a voter without a
+ * Progress is missing. */
+void orc_check_quorum_batch(const orc_prog *a, uint8_t *qa, uint64_t *stats) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  uint64_t st[NSTAT];
+  memset(st, 0, sizeof(st));
+  for (uint64_t g = 0; g < a->G; g++) {
+    uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+    uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+    uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+    uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+    if (self < S && ((trk >> self) & 1u)) a->pw[self * a->stride + g] |= PF_RECENT_ACTIVE;
+    uint32_t votes = 0, yes = 0;
+    for (uint32_t s = 0; s < S; s++) {
+      if (!((trk >> s) & 1u)) continue;
+      votes |= 1u << s;
+      if (a->pw[s * a->stride + g] & PF_RECENT_ACTIVE) yes |= 1u << s;
+    }
+    int active = orc_joint_vote(mi, mo, votes, yes) == VOTE_WON;
+    for (uint32_t s = 0; s < S; s++)
+      if (((trk >> s) & 1u) && s != self) a->pw[s * a->stride + g] &= ~PF_RECENT_ACTIVE;
+    if (qa) qa[g] = (uint8_t)active;
+    st[ST_GROUPS] += 1;
+    st[ST_STEPDOWNS] += !active;
+    st[ST_CHECKSUM] += orc_mix64(((a->goff + g) * PHI) ^ ((uint64_t)yes << 32) ^
+                                 (active ? 0xA0761D6478BD642Full : 0));
   }
   if (stats)
     for (int k = 0; k < NSTAT; k++) stats[k] += st[k];

@@ -41,7 +41,6 @@ def initial_arrays(sc):
         "flags": np.array([p["state"] | (PF_PROBE_SENT if p["probe_sent"] else 0) |
                            (PF_RECENT_ACTIVE if p["recent_active"] else 0)
                            for p in sc["peers"]], np.uint8),
-        "istart": np.zeros(S, np.uint8),
         "icount": np.array([len(p["ring"]) for p in sc["peers"]], np.uint8),
         "ibuf": np.zeros(S * F_CAP, np.uint64),
         "committed": np.array([lg["committed"]], np.uint64),
@@ -104,7 +103,7 @@ def check_expect(sc, exp, be, out, where):
 
 def run_scenario(sc, be):
     """be: backend with load(arrays), step(t, idx, hint, lt) -> out dict,
-    send(want_mask, sei, max_ents) -> out dict, append(), peer(s), committed()."""
+    send(want_mask, sei) -> out dict, append(), peer(s), committed()."""
     be.load(sc, initial_arrays(sc))
     for i, st in enumerate(sc["steps"]):
         where = f"{sc['name']} step {i} ({st['op']})"
@@ -113,7 +112,7 @@ def run_scenario(sc, be):
             out = be.step(*msg_arrays(sc, st["msgs"]))
         elif st["op"] == "send":
             want = sum(1 << s for s in st["want"])
-            out = be.send(want, st["send_if_empty"], sc["max_ents"])
+            out = be.send(want, st["send_if_empty"])  # MaxSizePerMsg: the state's max_ents
         elif st["op"] == "append":
             be.append()
         check_expect(sc, st.get("expect", {}), be, out, where)
@@ -135,6 +134,8 @@ class OracleBackend:
     def load(self, sc, a):
         S = sc["S"]
         pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
+        a = dict(a)
+        pb.pw = self.orc.pack_word(a.pop("flags"), 0, a.pop("icount"))
         for k, v in a.items():
             setattr(pb, k, v.copy())
         self.pb, self.sc = pb, sc
@@ -144,9 +145,9 @@ class OracleBackend:
         return {"sent": o.sent[0], "snap": o.snap[0], "timeout_now": o.timeout_now[0],
                 "msg_count": o.msg_count, "msg_index": o.msg_index, "bcast": o.bcast[0]}
 
-    def send(self, want, sei, me):
+    def send(self, want, sei):
         w = np.array([want], self.orc.mask_dtype(self.sc["S"]))
-        sent, snap = self.orc.progress_send(self.pb, w, sei, me)
+        sent, snap = self.orc.progress_send(self.pb, w, sei)
         return {"sent": sent[0], "snap": snap[0]}
 
     def append(self):

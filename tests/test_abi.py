@@ -27,7 +27,8 @@ def test_header_declares_expected_surface():
               "qe_record_votes", "qe_replication_round", "qe_election_steps",
               "qe_stats_reduce", "qe_gen_groups", "qe_abi_version", "qe_strerror",
               "qe_mask_bytes", "qe_tune", "qe_allreduce_stats", "qe_comm_init",
-              "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes"]:
+              "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes", "qe_check_quorum",
+              "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange"]:
         assert f in fns
 
 
@@ -56,10 +57,13 @@ int main(void) {
   Z(qe_election_params) F(qe_election_params, steps) F(qe_election_params, p_grant_q16)
   Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
   Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
-  Z(qe_progress) F(qe_progress, infl_buf) F(qe_progress, log_runs) F(qe_progress, out_mask)
-  F(qe_progress, tracked) F(qe_progress, snap_index) F(qe_progress, max_ents)
+  F(qe_confstate_csr, auto_leave) F(qe_confstate_csr, perm)
+  Z(qe_progress) F(qe_progress, peer) F(qe_progress, infl_buf) F(qe_progress, log_runs)
+  F(qe_progress, out_mask) F(qe_progress, tracked) F(qe_progress, snap_index)
+  F(qe_progress, max_ents)
   Z(qe_peer_msgs) F(qe_peer_msgs, bcast) F(qe_peer_msgs, timeout_now) F(qe_peer_msgs, msg_index)
-  F(qe_peer_msgs, bytes_requested)
+  F(qe_peer_msgs, bytes_requested) F(qe_peer_msgs, read_acks) F(qe_peer_msgs, read_ctx)
+  F(qe_peer_msgs, read_ok)
   Z(qe_conf) F(qe_conf, slot_ids) F(qe_conf, tracked) F(qe_conf, auto_leave)
   Z(qe_conf_changes) F(qe_conf_changes, stride) F(qe_conf_changes, node_id)
   F(qe_conf_changes, new_progress)
@@ -92,7 +96,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 2
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 3
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0
@@ -100,8 +104,10 @@ def test_constants_and_introspection():
     assert L.qe_strerror(_lib.QE_EINVAL) == b"invalid argument"
     src = open(HEADER).read()
     for name, val in [("QE_VOTE_PENDING", 1), ("QE_VOTE_LOST", 2), ("QE_VOTE_WON", 3),
-                      ("QE_STATS_COUNTERS", 16), ("QE_STATS_SHARDS", 64), ("QE_EINVAL", -22)]:
-        m = re.search(rf"#define {name} \(?(-?\d+)\)?", src)
+                      ("QE_STATS_COUNTERS", 16), ("QE_STATS_SHARDS", 64), ("QE_EINVAL", -22),
+                      ("QE_PF_RECENT_ACTIVE", 8), ("QE_PW_START_SHIFT", 8),
+                      ("QE_PW_COUNT_SHIFT", 16)]:
+        m = re.search(rf"#define {name} \(?(-?\d+)u?\)?", src)
         assert m and int(m.group(1)) == val, name
 
 
@@ -129,7 +135,12 @@ def test_argument_errors_without_gpu():
     pr = _lib.QeProgress(num_groups=1, num_slots=3, inflight_cap=0, stride=1)
     assert L.qe_progress_step(C.byref(pr), C.byref(_lib.QePeerMsgs()), None, None) == _lib.QE_ERANGE
     pr = _lib.QeProgress(num_groups=1, num_slots=3, inflight_cap=4, stride=1, log_runs=17)
-    assert L.qe_progress_send(C.byref(pr), None, 0, 1, None, None, None) == _lib.QE_ERANGE
+    assert L.qe_progress_send(C.byref(pr), None, 0, None, None, None) == _lib.QE_ERANGE
+    assert L.qe_check_quorum(None, None, None, None) == _lib.QE_EINVAL
+    pr = _lib.QeProgress(num_groups=4, num_slots=3, inflight_cap=4, stride=4)  # no peer words
+    assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_EINVAL
+    pr = _lib.QeProgress(num_groups=0, num_slots=3)  # empty batch is a no-op
+    assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_OK
     assert L.qe_confchange(None, None, None, None) == _lib.QE_EINVAL
     cf = _lib.QeConf(num_groups=4, num_slots=17)
     assert L.qe_confchange(C.byref(cf), C.byref(_lib.QeConfChanges()), None, None) == _lib.QE_EINVAL

@@ -54,7 +54,7 @@ def test_collect_empty_and_no_values(eng):
     import ctypes as C
     lib = eng._lib.lib()
     count = torch.full((1,), 7, dtype=torch.int64, device=DEV)
-    eng.check("qe_collect", lib.qe_collect(0, 0, None, None, None, None, eng._ptr(count), None,
+    eng.check("qe_collect", lib.qe_collect(0, 0, None, None, None, None, None, eng._ptr(count), None,
                                            eng._stream(torch.device(DEV))))
     torch.cuda.synchronize()
     assert int(count.item()) == 0
@@ -65,7 +65,7 @@ def test_collect_empty_and_no_values(eng):
     out = torch.empty(8, dtype=torch.int64, device=DEV)
     f = torch.ones(8, dtype=torch.uint8, device=DEV)
     scratch = torch.empty(64, dtype=torch.int64, device=DEV)
-    rc = lib.qe_collect(8, 0, eng._ptr(f), None, None, eng._ptr(out), eng._ptr(count),
+    rc = lib.qe_collect(8, 0, None, eng._ptr(f), None, None, eng._ptr(out), eng._ptr(count),
                         eng._ptr(scratch), eng._stream(torch.device(DEV)))
     assert rc != 0
     del C

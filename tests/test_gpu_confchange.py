@@ -196,8 +196,8 @@ def test_random_differential(eng, S):
 
 @pytest.mark.parametrize("S,G", [(5, 1), (7, 300), (16, 777)])
 def test_random_differential_ragged(eng, S, G):
-    """Ragged batches: the last block stages fewer than 256 groups' slot IDs
-    through LDS (qe_conf.hpp k_confchange)."""
+    """Ragged batches: the last block holds fewer than 256 groups (one lane
+    per group, ID-major slot rows, qe_conf.hpp k_confchange)."""
     seen = run_differential(eng, S, S, G, 8, 3000 + S)
     assert cc.OK in seen
 
@@ -228,7 +228,7 @@ def test_invalid_inputs(eng):
     lnx = np.where(rng.random(G) < 0.3, sub(0.9) & out, 0)
     isl = (lrn | rng.integers(0, 1 << S, G)) & ~np.where(rng.random(G) < 0.9, lnx, 0)
     al = (rng.random(G) < 0.2).astype(np.uint8)
-    cs.slot_ids.copy_(torch.from_numpy(ids.reshape(-1).view(np.int64)).to(DEV))
+    cs.slot_ids.copy_(torch.from_numpy(np.ascontiguousarray(ids.T).reshape(-1).view(np.int64)).to(DEV))
     for k, v in (("inc", inc), ("out", out), ("learner", lrn), ("learners_next", lnx),
                  ("is_learner", isl), ("tracked", trk)):
         getattr(cs, k).copy_(torch.from_numpy(v.astype(md)).to(DEV))
@@ -238,8 +238,8 @@ def test_invalid_inputs(eng):
     eng.confchange(cs, ch)
     torch.cuda.synchronize()
     res = ch.result.cpu().numpy()
-    # a failed change keeps the group's slot IDs (the block writes them back)
-    ids_after = cs.slot_ids.cpu().numpy().view(np.uint64).reshape(G, S)
+    # a failed change keeps the group's slot IDs (nothing is written)
+    ids_after = cs.slot_ids.cpu().numpy().view(np.uint64).reshape(S, G).T
     failed = res != cc.OK
     assert failed.any() and (ids_after[failed] == ids[failed]).all()
     state = {"slot_ids": ids, "tracked": trk, "is_learner": isl, "inc": inc, "out": out,
@@ -260,6 +260,48 @@ def test_invalid_inputs(eng):
         else:
             assert res[g] != cc.ERR_INVARIANT, g
     assert 100 < n_bad < G - 100
+
+
+def test_change_writes_only_changed_id_rows(eng):
+    """ID-major slot IDs (ABI 3): a change writes the ID of a slot it creates
+    (and 0 for a slot it removes) and leaves every other slot ID -- including
+    garbage in untracked slots, which is ignored -- untouched."""
+    S, G = 5, 1000
+    cs = eng.ConfState(G, S, DEV)
+    ids = np.zeros((S, G), np.uint64)
+    gid = np.arange(G, dtype=np.uint64)
+    for s in range(4):
+        ids[s] = gid * 8 + s + 1
+    ids[4] = 0xDEAD  # untracked garbage
+    cs.slot_ids.copy_(torch.from_numpy(ids.reshape(-1).view(np.int64)).to(DEV))
+    cs.inc.fill_(0b00111)
+    cs.learner.fill_(0b01000)
+    cs.is_learner.fill_(0b01000)
+    cs.tracked.fill_(0b01111)
+    ch = eng.ConfChanges(G, S, 2, DEV)
+    ch.op.fill_(cc.OP_SIMPLE)
+    ch.count.fill_(2)
+    # half the groups: promote the learner + add a learner (new ID -> slot 4);
+    # the other half: remove voter 2 (slot 1) + nothing
+    typ = np.zeros((2, G), np.uint8)
+    node = np.zeros((2, G), np.uint64)
+    half = gid % 2 == 0
+    typ[0] = np.where(half, cc.ADD_NODE, cc.REMOVE_NODE)
+    node[0] = np.where(half, gid * 8 + 4, gid * 8 + 2)
+    typ[1] = cc.ADD_LEARNER_NODE
+    node[1] = np.where(half, gid * 8 + 7, 0)
+    ch.type.copy_(torch.from_numpy(typ.reshape(-1)))
+    ch.node_id.copy_(torch.from_numpy(node.reshape(-1).view(np.int64)))
+    eng.confchange(cs, ch)
+    torch.cuda.synchronize()
+    assert (ch.result.cpu().numpy() == cc.OK).all()
+    after = cs.slot_ids.cpu().numpy().view(np.uint64).reshape(S, G)
+    np.testing.assert_array_equal(after[4][half], (gid * 8 + 7)[half])
+    np.testing.assert_array_equal(after[4][~half], np.full((~half).sum(), 0xDEAD, np.uint64))
+    np.testing.assert_array_equal(after[1][~half], np.zeros((~half).sum(), np.uint64))
+    for s in (0, 2, 3):
+        np.testing.assert_array_equal(after[s], ids[s])
+    np.testing.assert_array_equal(after[1][half], ids[1][half])
 
 
 def test_python_mirror_testdata():
@@ -335,7 +377,7 @@ def test_confstate_round_trip_seeds_confchange(eng):
     ps = eng.ProgressState(G, S, 1, 1, DEV)
     nxt = np.ones(S * ps.stride, np.uint64)
     flg = np.zeros(S * ps.stride, np.uint8)
-    ids = arr["slot_ids"].reshape(G, S)
+    ids = arr["slot_ids"].reshape(S, G).T  # ID-major [S][G]
     for g, o in enumerate(changers):
         for s in range(S):
             if ids[g, s]:

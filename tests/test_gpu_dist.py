@@ -37,11 +37,10 @@ def test_two_ranks_equal_one_process_over_the_union(workload):
     one = _bench(["--gpus", "1", "--groups", str(2 * G)] + common, {})
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
     assert two["config"]["global_groups"] == one["config"]["global_groups"] == 2 * G
-    if workload != "progress_step":
-        # inputs and the election RNG are keyed by the global group id, so
-        # the sharded run and the union agree launch for launch (the
-        # Progress workload draws its synthetic state per rank)
-        assert two["checks"]["stats_checksum"] == one["checks"]["stats_checksum"]
+    # inputs (the Progress workload's state and messages too: bench.py
+    # counter_rows) and the election RNG are keyed by the global group id, so
+    # the sharded run and the union agree launch for launch
+    assert two["checks"]["stats_checksum"] == one["checks"]["stats_checksum"]
     assert two["checks"]["invariant_violations"] == 0
 
 

@@ -696,3 +696,85 @@ def test_wire_format_to_gpu_decisions(eng):
             Q.record_vote(vmap, i, v)
         assert int(commit[g]) == Q.joint_committed(c0, c1, progress[g])
         assert (int(gc[g]), int(rc[g]), int(vote[g])) == Q.tally_votes(c0, c1, set(lrn), vmap)
+
+
+def test_wire_format_bucketed_to_gpu_decisions(eng):
+    """The same wire-format path in the shape-bucketed order (qe_pack_order,
+    ABI 3): packed position i holds the caller's group perm[i]; its commit /
+    vote / tally equal the map-based restatement of that caller group, and
+    qe_collect with the perm reports caller group ids."""
+    import random
+    from etcd_amd.packing import ConfStates, pack_confstates, pack_progress, pack_votes
+    rng = random.Random(199)
+    confs, progress, votes = [], [], []
+    for _ in range(20000):
+        pool = rng.sample(range(1, 1 << 30), 10)
+        c0 = pool[:rng.randint(0, 5)]
+        c1 = (rng.sample(c0, rng.randint(0, len(c0))) + pool[5:5 + rng.randint(0, 3)]
+              if rng.random() < 0.5 else [])
+        lrn = pool[8:8 + rng.randint(0, 2)]
+        confs.append((c0, c1, lrn))
+        peers = list(dict.fromkeys(c0 + c1 + lrn))
+        progress.append({i: rng.randrange(1000) for i in peers if rng.random() < 0.9})
+        votes.append([(i, rng.random() < 0.5) for i in peers if rng.random() < 0.8])
+    cs = ConfStates([c[0] for c in confs], [c[1] for c in confs], [c[2] for c in confs])
+    p = pack_confstates(cs, 12, bucketed=True)
+    perm = p.perm.astype(np.int64)
+    assert sorted(perm.tolist()) == list(range(len(confs)))
+    pack_progress(p, progress)
+    pack_votes(p, votes)
+    b = eng.SlotBatch(p.G, p.S, DEV)
+    b.load_host(p.match, inc=p.inc, out=p.out, learner=p.learner, voted=p.voted,
+                granted=p.granted)
+    out = eng.commit_vote(b)
+    commit = out.commit.cpu().numpy().view(np.uint64)
+    vote, gc, rc = (x.cpu().numpy() for x in (out.vote, out.granted, out.rejected))
+    for i in range(p.G):
+        g = int(perm[i])
+        c0, c1, lrn = confs[g]
+        vmap = {}
+        for k, v in votes[g]:
+            Q.record_vote(vmap, k, v)
+        assert int(commit[i]) == Q.joint_committed(c0, c1, progress[g]), (i, g)
+        assert (int(gc[i]), int(rc[i]), int(vote[i])) == Q.tally_votes(c0, c1, set(lrn), vmap)
+    # Ready deltas in caller ids: the won groups and their commit index
+    flags = (out.vote == 3).to(torch.uint8)
+    perm_d = torch.from_numpy(perm).to(DEV)
+    groups, vals = eng.collect(flags, out.commit, group_offset=1000, perm=perm_d)
+    torch.cuda.synchronize()
+    sel = np.nonzero(vote == 3)[0]
+    np.testing.assert_array_equal(groups.cpu().numpy(), perm[sel] + 1000)
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint64), commit[sel])
+
+
+def test_config3_packed_workload_matches_oracle(eng, orc):
+    """bench.py config3_joint_packed at 2M groups: ConfStates of per-group
+    uniform overlap built by bench.joint_confstates, packed through
+    qe_pack_order + qe_pack_confstate in 1M-group batches; every packed
+    group's commit / vote equals the oracle, the layout is bucketed (each
+    wave's voters sit in the same low slots), and per caller group the
+    packed masks equal an identity packing of the same ConfState."""
+    import bench
+    from etcd_amd.packing import pack_confstates
+    bench.engine = eng
+    G, S, goff = 1 << 21, 10, 12345
+    b = eng.SlotBatch(G, S, DEV, group_offset=goff)
+    perm = bench.pack_joint_batches(b, goff, chunk=1 << 20).cpu().numpy()
+    eng.gen_groups(b, 0x5EED, values_only=True)
+    check_commit_vote(eng, orc, b, goff=goff)
+    h = b.host()
+    uni = (h["inc"] | h["out"]).astype(np.int64)
+    # voters first: the union is the low slots of every group
+    u = np.array([bin(x).count("1") for x in range(1 << S)])[uni]
+    np.testing.assert_array_equal(uni, (1 << u) - 1)
+    # tiles whose 64 groups share one union size: all but the bucket edges
+    tiles = u[: G // 64 * 64].reshape(-1, 64)
+    mixed = int((tiles.min(1) != tiles.max(1)).sum())
+    assert mixed <= 2 * 6 * 2, mixed  # <= 2 edges per shape per 1M batch
+    # per caller group: identity packing of its own ConfState
+    cs, o = bench.joint_confstates(goff, 1 << 20, DEV)
+    ident = pack_confstates(cs, S)
+    first = perm[: 1 << 20]
+    np.testing.assert_array_equal(h["inc"][: 1 << 20], ident.inc[first])
+    np.testing.assert_array_equal(h["out"][: 1 << 20], ident.out[first])
+    np.testing.assert_array_equal(10 - u[: 1 << 20], o[first])

@@ -1,8 +1,12 @@
 """GPU parity of the Progress state machine (qe_progress_step /
-qe_progress_send) against the oracle, which
-tests/test_progress_oracle.py pins to the reference's tables and to the
-leader-side scenarios of tests/golden/progress_scenarios.json.  The same
-scenarios run here through the HIP kernels."""
+qe_progress_send / qe_check_quorum, SURVEY.md §8(f) rows 3-4 and the
+ReadIndex / CheckQuorum decisions) against the oracle, which
+tests/test_progress_oracle.py pins to the reference's tables, the
+leader-side scenarios of tests/golden/progress_scenarios.json and the
+ReadIndex / CheckQuorum transcriptions of tests/leader_round_scenarios.py.
+The same scenarios run here through the HIP kernels, and the instrumented
+kernel's byte count must equal the oracle's restatement of the accounting
+rules exactly."""
 import numpy as np
 import pytest
 import torch
@@ -50,10 +54,10 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
     low = rng.random(n) < 0.08  # compacted: Next < firstIndex (snapshot path)
     pb.next[low] = (rng.random(int(low.sum())) * fi[low]).astype(np.uint64)
     pb.pending[:] = rng.integers(0, 70, n).astype(np.uint64)
-    pb.flags[:] = (rng.integers(0, 3, n) | (rng.integers(0, 2, n) * 4) |
-                   (rng.integers(0, 2, n) * 8)).astype(np.uint8)
-    pb.icount[:] = rng.integers(0, F + 1, n).astype(np.uint8)
-    pb.istart[:] = rng.integers(0, F, n).astype(np.uint8)
+    pb.set_peer(flags=(rng.integers(0, 3, n) | (rng.integers(0, 2, n) * 4) |
+                       (rng.integers(0, 2, n) * 8)).astype(np.uint8),
+                istart=rng.integers(0, F, n).astype(np.uint8),
+                icount=rng.integers(0, F + 1, n).astype(np.uint8))
     base = pb.match.copy()
     for k in range(F):  # entry-major rings: entry k of slot s at (s*F + k)*stride + g
         pb.ibuf[(np.arange(S)[:, None] * F + k) * pb.stride + np.arange(G)[None, :]] = \
@@ -91,8 +95,8 @@ def random_msgs(rng, pb):
 def to_device(eng, pb, masks, extras=()):
     ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride,
                            extras=extras, max_ents=pb.max_ents)
-    ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, flags=pb.flags,
-                 istart=pb.istart, icount=pb.icount, ibuf=pb.ibuf, committed=pb.committed,
+    ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, peer=pb.pw,
+                 ibuf=pb.ibuf, committed=pb.committed,
                  term_start=pb.term_start, first_index=pb.first_index, last_index=pb.last_index,
                  run_first=pb.run_first, run_term=pb.run_term, run_count=pb.run_count,
                  inc=pb.inc, out=pb.out, tracked=pb.tracked, self_slot=pb.self_slot,
@@ -102,9 +106,14 @@ def to_device(eng, pb, masks, extras=()):
 
 def assert_same(ps, pb):
     h = ps.host()
-    for k in ("match", "next", "pending", "flags", "istart", "icount", "committed"):
+    for k in ("match", "next", "pending", "committed"):
         np.testing.assert_array_equal(h[k], getattr(pb, k), err_msg=k)
+    np.testing.assert_array_equal(h["peer"], pb.pw, err_msg="packed peer words")
     np.testing.assert_array_equal(h["ibuf"], pb.ibuf, err_msg="ibuf")
+
+
+def to_dev_mask(a, S):
+    return torch.from_numpy(a.view(np.int16) if S > 8 else a).to(DEV)
 
 
 def load_msgs(eng, ps, mtype, mindex, mhint, mlogterm):
@@ -128,36 +137,75 @@ def assert_outputs(msgs, o, S):
     np.testing.assert_array_equal(got_ix[cnt > 0], o.msg_index[cnt > 0], err_msg="msg_index")
 
 
+def random_reads(rng, pb):
+    """A pending ReadIndex request per group (70 %): the leader's own ack or
+    a random subset, and the heartbeat responses carrying its context."""
+    md = orc.mask_dtype(pb.S)
+    acks = rng.integers(0, 1 << pb.S, pb.G).astype(md)
+    acks[rng.random(pb.G) < 0.5] = 1
+    ctx = rng.integers(0, 1 << pb.S, pb.G).astype(md)
+    ctx[rng.random(pb.G) < 0.3] = (1 << pb.S) - 1
+    return acks, ctx
+
+
 CASES = [(1, (), ()), (3, (), EXTRAS), (5, (), ()), (5, (), EXTRAS), (5, ("inc",), EXTRAS),
          (7, ("inc", "out"), EXTRAS), (10, ("inc", "out"), ()), (16, ("inc",), EXTRAS)]
 
 
+@pytest.mark.parametrize("F", [8, 32])
+@pytest.mark.parametrize("R", [3, 6])
 @pytest.mark.parametrize("S,masks,extras", CASES)
-def test_progress_rounds_match_oracle(eng, S, masks, extras):
-    rng = np.random.default_rng(100 + S + 7 * len(extras))
-    G, F, R = 3001, 8, 6
+def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
+    """Random states and the full message mix (rejects with LogTerm > 0,
+    snapshots, heartbeats with ReadIndex acks, ...) through the 4-run (R = 3,
+    the production kernel) and 8-run (R = 6) kernels, row-resident (F = 8)
+    and memory (F = 32) rings.  Odd rounds run the instrumented variant,
+    whose byte count must equal the oracle's exactly."""
+    rng = np.random.default_rng(100 + S + 7 * len(extras) + 31 * R + F)
+    G = 3001
     pb = random_state(rng, G, S, F, R, masks, extras, max_ents=int(rng.integers(0, 4)))
     ps = to_device(eng, pb, masks, extras)
+    md = orc.mask_dtype(S)
     for rnd in range(6):
         mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
         msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+        acks = ctx = None
+        if rnd % 3 != 2:
+            acks, ctx = random_reads(rng, pb)
+            msgs.track_reads(ps, acks.copy(), ctx if rnd % 3 == 0 else None)
         stats = eng.stats_buffer(DEV)
+        if rnd % 2:
+            msgs.bytes_requested = torch.zeros(1, dtype=torch.int64, device=DEV)
         eng.progress_step(ps, msgs, stats)
         got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
-        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, read_acks=acks,
+                              read_ctx=ctx if rnd % 3 == 0 else None, count_bytes=True)
         assert_same(ps, pb)
         assert_outputs(msgs, o, S)
         np.testing.assert_array_equal(got, o.stats)
+        if acks is not None:
+            np.testing.assert_array_equal(msgs.read_acks.cpu().numpy().view(md), acks)
+            np.testing.assert_array_equal(msgs.read_ok.cpu().numpy(), o.read_ok)
+        if rnd % 2:
+            assert int(msgs.bytes_requested.item()) == int(o.bytes[0]), (rnd, S)
         # a sendAppend / bcastAppend round to random peers
-        md = orc.mask_dtype(S)
         want = rng.integers(0, 1 << S, G).astype(md)
-        tw = torch.from_numpy(want.view(np.int16) if S > 8 else want).to(DEV)
         sei, me = int(rnd % 2), int(rng.integers(0, 5))
-        sent, snap = eng.progress_send(ps, tw, sei, me)
-        o_sent, o_snap = orc.progress_send(pb, want, sei, me)
+        ps.max_ents = pb.max_ents = me
+        sent, snap = eng.progress_send(ps, to_dev_mask(want, S), sei)
+        o_sent, o_snap = orc.progress_send(pb, want, sei)
         np.testing.assert_array_equal(sent.cpu().numpy().view(md), o_sent)
         np.testing.assert_array_equal(snap.cpu().numpy().view(md), o_snap)
         assert_same(ps, pb)
+        # CheckQuorum every third round (RecentActive set by the step above)
+        if rnd % 3 == 1:
+            st2 = eng.stats_buffer(DEV)
+            qa = eng.check_quorum(ps, stats=st2)
+            got2 = eng.stats_reduce(st2).cpu().numpy().view(np.uint64)
+            o_qa, o_st = orc.check_quorum(pb)
+            np.testing.assert_array_equal(qa.cpu().numpy(), o_qa)
+            np.testing.assert_array_equal(got2, o_st)
+            assert_same(ps, pb)
 
 
 @pytest.mark.parametrize("R", [8, 9, 16])
@@ -188,7 +236,7 @@ def test_progress_long_rings_and_bcasts(eng):
     G, S, F, R = 2000, 5, 32, 4
     pb = random_state(rng, G, S, F, R, (), EXTRAS, max_ents=1)
     pb.term_start[:] = 0
-    pb.flags[:] = 1 | 8  # Replicate, RecentActive
+    pb.set_peer(flags=1 | 8)  # Replicate, RecentActive
     ps = to_device(eng, pb, (), EXTRAS)
     for _ in range(4):
         n = S * G
@@ -212,31 +260,51 @@ class GpuBackend:
     def __init__(self, eng):
         self.eng = eng
 
-    def load(self, sc, a):
+    def load(self, sc, a, inc=None):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
         ps = self.eng.ProgressState(1, sc["S"], F_CAP, len(sc["log"]["runs"]), DEV, stride=1,
-                                    extras=EXTRAS, max_ents=sc["max_ents"])
+                                    extras=EXTRAS, max_ents=sc["max_ents"],
+                                    masks=("inc",) if inc is not None else ())
         ps.tracked = None  # every slot holds a Progress (as the oracle backend)
         if "snap_index" not in a:
             ps.snap_index = None
         ps.load_host(**a)
+        if inc is not None:
+            ps.inc.fill_(inc)
         self.ps, self.sc = ps, sc
 
-    def step(self, t, idx, hint, lt):
+    def step(self, t, idx, hint, lt, read=None):
         msgs = load_msgs(self.eng, self.ps, t, idx, hint, lt)
+        md = orc.mask_dtype(self.sc["S"])
+        if read is not None:
+            msgs.track_reads(self.ps, np.array([read[0]], md),
+                             None if read[1] is None else np.array([read[1]], md))
         self.eng.progress_step(self.ps, msgs)
-        return {"sent": int(msgs.sent[0]), "snap": int(msgs.snap[0]),
-                "timeout_now": int(msgs.timeout_now[0]),
-                "msg_count": msgs.msg_count.cpu().numpy()[: self.sc["S"] * self.ps.stride: self.ps.stride],
-                "msg_index": msgs.msg_index.cpu().numpy().view(np.uint64)[
-                    : self.sc["S"] * self.ps.stride: self.ps.stride],
-                "bcast": int(msgs.bcast[0])}
+        out = {"sent": int(msgs.sent[0]), "snap": int(msgs.snap[0]),
+               "timeout_now": int(msgs.timeout_now[0]),
+               "msg_count": msgs.msg_count.cpu().numpy()[: self.sc["S"] * self.ps.stride: self.ps.stride],
+               "msg_index": msgs.msg_index.cpu().numpy().view(np.uint64)[
+                   : self.sc["S"] * self.ps.stride: self.ps.stride],
+               "bcast": int(msgs.bcast[0])}
+        if read is not None:
+            out["read_ok"] = int(msgs.read_ok[0])
+            out["acks"] = int(msgs.read_acks[0]) & ((1 << self.sc["S"]) - 1)
+        return out
 
-    def send(self, want, sei, me):
+    def send(self, want, sei):
         dt = torch.uint8 if self.sc["S"] <= 8 else torch.int16
         w = torch.tensor([want], dtype=dt, device=DEV)
-        sent, snap = self.eng.progress_send(self.ps, w, sei, me)
+        sent, snap = self.eng.progress_send(self.ps, w, sei)
         return {"sent": int(sent[0]), "snap": int(snap[0])}
+
+    def last_index(self):
+        return int(self.ps.last_index[0])
+
+    def check_quorum(self):
+        qa = self.eng.check_quorum(self.ps)
+        w = self.ps.host()["peer"]
+        ra = sum(1 << s for s in range(self.sc["S"]) if w[s * self.ps.stride] & 8)
+        return int(qa[0]), ra
 
     def append(self):
         ps, s = self.ps, self.sc["self"]
@@ -262,6 +330,72 @@ def test_progress_scenarios_on_gpu(eng):
     raft_snap_test.go, ...) through qe_progress_step / qe_progress_send."""
     for sc in scenarios():
         run_scenario(sc, GpuBackend(eng))
+
+
+def test_readindex_and_checkquorum_scenarios_on_gpu(eng):
+    """TestReadOnlyOptionSafe (raft_test.go:2177), TestReadOnlyWithLearner
+    (:2231) and the learner-ack rule through qe_progress_step's heartbeat
+    ReadIndex acks; TestLeaderStepdownWhenQuorumActive / ...Lost
+    (:1748-1781) through qe_progress_step heartbeats chained into
+    qe_check_quorum (tests/leader_round_scenarios.py)."""
+    from tests.leader_round_scenarios import SCENARIOS
+    for sc in SCENARIOS:
+        sc(GpuBackend(eng))
+
+
+@pytest.mark.parametrize("S,masks,extras", [(3, (), ()), (5, ("inc",), EXTRAS),
+                                            (9, ("inc", "out"), EXTRAS), (16, (), EXTRAS)])
+def test_check_quorum_matches_oracle(eng, S, masks, extras):
+    """qe_check_quorum against the oracle on random Progress words, voter
+    masks, tracked sets (voters without a Progress are missing) and leader
+    slots (>= S: the leader removed itself), twice in a row (the second sees
+    the reset RecentActive bits)."""
+    rng = np.random.default_rng(900 + S)
+    G = 5003
+    pb = random_state(rng, G, S, 8, 2, masks, extras)
+    ps = to_device(eng, pb, masks, extras)
+    for _ in range(2):
+        st = eng.stats_buffer(DEV)
+        qa = eng.check_quorum(ps, stats=st)
+        got = eng.stats_reduce(st).cpu().numpy().view(np.uint64)
+        o_qa, o_st = orc.check_quorum(pb)
+        np.testing.assert_array_equal(qa.cpu().numpy(), o_qa)
+        np.testing.assert_array_equal(got, o_st)
+        assert_same(ps, pb)
+        assert 0 < int(o_qa.sum()) < G or S == 16
+
+
+def test_bytes_requested_equal_oracle_on_bench_state(eng):
+    """The Progress step's roofline denominator (bench.py progress_step: the
+    instrumented kernel's byte count per group) equals the oracle's
+    independent count on the bench workload's own state and messages
+    (bench.progress_round_state), here at 64K groups."""
+    import bench
+    bench.engine = eng
+    G, S, F, R = 1 << 16, 5, 8, 4
+    ps = eng.ProgressState(G, S, F, R, DEV, extras=("self_slot",), max_ents=16)
+    msgs = eng.PeerMsgs(ps)
+    msgs.snap = msgs.timeout_now = None
+    bench.progress_round_state(ps, msgs)
+    h = ps.host()
+    pb = orc.ProgressBatch(G, S, F, R, stride=ps.stride, max_ents=16)
+    for k in ("match", "next", "pending", "ibuf", "committed", "term_start", "first_index",
+              "last_index", "run_first", "run_term", "run_count", "self_slot"):
+        setattr(pb, k, h[k].copy())
+    pb.pw = h["peer"].copy()
+    mtype = msgs.type.cpu().numpy()
+    mix = [msgs.index, msgs.reject_hint, msgs.log_term]
+    mindex, mhint, mlogterm = (t.cpu().numpy().view(np.uint64) for t in mix)
+    b = eng.progress_bytes_requested(ps, msgs)
+    o = orc.StepOut(pb)
+    m = orc.OrcMsgs(orc.P(mtype), orc.P(mindex), orc.P(mhint), orc.P(mlogterm), orc.P(o.sent),
+                    orc.P(o.bcast), None, None, orc.P(o.msg_count), orc.P(o.msg_index), None,
+                    None, None, orc.P(o.bytes))
+    import ctypes as C
+    orc.lib().orc_progress_step_batch(C.byref(pb.struct()), C.byref(m), orc.P(o.stats), 0)
+    assert_same(ps, pb)
+    assert b == int(o.bytes[0]), (b / G, int(o.bytes[0]) / G)
+    assert 300 * G < b < 700 * G  # the ~0.5 KB per group-round DESIGN.md quotes
 
 
 def test_fast_log_rejection_on_gpu(eng):
@@ -337,27 +471,28 @@ def test_send_if_empty_precedes_snapshot_on_gpu(eng):
     ps.last_index.fill_(20)
     ps.next.fill_(5)
     ps.match.fill_(4)
-    ps.flags.fill_(8)  # Probe, RecentActive
+    ps.peer.fill_(8)  # Probe, RecentActive
     want = torch.ones(G, dtype=torch.uint8, device=DEV)
-    sent, snap = eng.progress_send(ps, want, False, 0)
+    sent, snap = eng.progress_send(ps, want, False)
     assert int(sent.sum()) == 0 and int(snap.sum()) == 0
-    assert int((ps.flags[:G] & 3).sum()) == 0 and int(ps.pending[:G].sum()) == 0
-    sent, snap = eng.progress_send(ps, want, True, 0)
+    assert int((ps.peer[:G] & 3).sum()) == 0 and int(ps.pending[:G].sum()) == 0
+    sent, snap = eng.progress_send(ps, want, True)
     assert int(sent.sum()) == G and int(snap.sum()) == G
-    assert bool(((ps.flags[:G] & 3) == 2).all()) and bool((ps.pending[:G] == 9).all())
+    assert bool(((ps.peer[:G] & 3) == 2).all()) and bool((ps.pending[:G] == 9).all())
 
 
 def test_bytes_requested_accounting(eng):
-    """The instrumented variant gives the same results and a byte count in
-    the expected range."""
+    """The instrumented variant gives the same results, and its byte count
+    equals the oracle's exactly (no outputs requested: only the state)."""
     rng = np.random.default_rng(5)
     G, S, F, R = 4096, 5, 8, 4
     pb = random_state(rng, G, S, F, R, ())
     ps = to_device(eng, pb, ())
     mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
     msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+    for k in ("sent", "bcast", "snap", "timeout_now", "msg_count", "msg_index"):
+        setattr(msgs, k, None)
     b = eng.progress_bytes_requested(ps, msgs)
-    o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm)
+    o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, outputs=False, count_bytes=True)
     assert_same(ps, pb)
-    assert_outputs(msgs, o, S)
-    assert 50 * G < b < 600 * G, b
+    assert b == int(o.bytes[0])

@@ -8,8 +8,8 @@ import numpy as np
 import pytest
 
 from etcd_amd import _lib
-from etcd_amd.packing import (ConfStates, pack, pack_confstates, pack_progress, pack_votes,
-                              slot_lookup)
+from etcd_amd.packing import (ConfStates, pack, pack_confstates, pack_order, pack_progress,
+                              pack_votes, slot_lookup)
 from oracle import quorum_ref as Q
 
 
@@ -120,7 +120,7 @@ def test_pack_conf_full_tracker_config():
         learners_next=[[], [6], [], [9]],
         auto_leave=[0, 1, 0, 1])
     arr, flags = pack_conf(cs, 8)
-    ids = arr["slot_ids"].reshape(4, 8)
+    ids = arr["slot_ids"].reshape(8, 4).T  # ID-major [S][G] (ABI 3)
     # group 0: voters 1,2,3 then learner 10
     assert ids[0].tolist() == [1, 2, 3, 10, 0, 0, 0, 0]
     assert int(arr["inc"][0]) == 0b0111 and int(arr["out"][0]) == 0
@@ -145,3 +145,85 @@ def test_zero_id_learner_flagged_by_pack_confstate():
     p = pack_confstates(cs, 4)
     assert p.flags[0] & _lib.QE_PACK_ZERO_ID
     assert not p.slot_ids.any() and int(p.learner[0]) == 0
+
+
+def test_non_joint_auto_leave_restores_false():
+    """restore.go:118-155: AutoLeave only takes effect through EnterJoint, so
+    a non-joint ConfState restores AutoLeave = false (checkInvariants would
+    reject AutoLeave without Voters[1]); a joint one keeps it."""
+    from etcd_amd.packing import pack_conf
+    cs = ConfStates(voters=[[1, 2, 3], [1, 2]], voters_outgoing=[[], [2, 3]],
+                    auto_leave=[1, 1])
+    arr, flags = pack_conf(cs, 4)
+    assert not flags.any()
+    assert arr["auto_leave"].tolist() == [0, 1]
+
+
+def shape_key(c):
+    v0, v1, lrn = set(c[0]), set(c[1]), set(c[2]) - set(c[0]) - set(c[1])
+    return (len(v0 | v1), len(v0), len(v1), len(lrn))
+
+
+def test_pack_order_buckets_by_shape():
+    """qe_pack_order (ABI 3): a stable sort of the groups by configuration
+    shape; packing in that order gives, at packed position i, exactly the
+    identity packing of the caller's group perm[i] (masks, ID-major slot
+    ids, flags, Match, votes)."""
+    rng = random.Random(11)
+    G, S = 5000, 16
+    confs = [random_confstate(rng) for _ in range(G)]
+    confs[7] = ([1, 2], [], [0], [])  # flagged (ID 0): sorts last
+    lists = [[c[k] for c in confs] for k in range(4)]
+    cs = ConfStates(*lists)
+    perm, nshape = pack_order(cs, S)
+    assert sorted(perm.tolist()) == list(range(G))
+    keys = [shape_key(confs[int(g)]) for g in perm]
+    assert int(perm[-1]) == 7
+    assert keys[:-1] == sorted(keys[:-1])  # shape-ascending
+    assert nshape == len(set(keys[:-1])) + 1
+    for a, b in zip(range(G - 2), range(1, G - 1)):  # stable within a shape
+        if keys[a] == keys[b]:
+            assert perm[a] < perm[b]
+    ident = pack_confstates(ConfStates(*lists), S)
+    cs.perm = perm
+    buck = pack_confstates(cs, S)
+    np.testing.assert_array_equal(buck.perm, perm)
+    for k in ("inc", "out", "learner", "flags"):
+        np.testing.assert_array_equal(getattr(buck, k), getattr(ident, k)[perm], err_msg=k)
+    np.testing.assert_array_equal(buck.slot_ids_sg, ident.slot_ids_sg[:, perm])
+    progress = [{i: rng.randrange(1 << 62) for i in dict.fromkeys(c[0] + c[1] + c[2])}
+                for c in confs]
+    votes = [[(i, rng.random() < 0.5) for i in dict.fromkeys(c[0] + c[1])] for c in confs]
+    assert pack_progress(ident, progress) == pack_progress(buck, progress)
+    np.testing.assert_array_equal(buck.match, ident.match[:, perm])
+    pack_votes(ident, votes)
+    pack_votes(buck, votes)
+    np.testing.assert_array_equal(buck.voted, ident.voted[perm])
+    np.testing.assert_array_equal(buck.granted, ident.granted[perm])
+    # packed voters sit in the low slots, so within a shape bucket the union
+    # occupies the same slots in every group
+    for i in range(G - 1):
+        u, mask = keys[i][0], int(buck.inc[i]) | int(buck.out[i])
+        assert mask == (1 << u) - 1
+    # a perm entry out of range is refused
+    bad = perm.copy()
+    bad[3] = G
+    cs.perm = bad
+    with pytest.raises(_lib.QuorumEngineError):
+        pack_confstates(cs, S)
+
+
+def test_pack_order_threads_agree():
+    rng = random.Random(5)
+    confs = [random_confstate(rng) for _ in range(30000)]
+    cs = ConfStates([c[0] for c in confs], [c[1] for c in confs], [c[2] for c in confs])
+    L = _lib.lib()
+    try:
+        L.qe_pack_threads(1)
+        a, na = pack_order(cs, 16)
+        L.qe_pack_threads(7)
+        b, nb = pack_order(cs, 16)
+    finally:
+        L.qe_pack_threads(0)
+    np.testing.assert_array_equal(a, b)
+    assert na == nb

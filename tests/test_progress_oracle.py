@@ -115,7 +115,7 @@ def test_send_if_empty_precedes_snapshot(orc):
     pb = orc.ProgressBatch(1, 1, 8, 1)
     pb.first_index[0], pb.last_index[0] = 10, 20
     pb.next[0], pb.match[0] = 5, 4
-    pb.flags[0] = 0 | PF_RECENT_ACTIVE  # Probe, recently active
+    pb.set_peer(flags=0 | PF_RECENT_ACTIVE)  # Probe, recently active
     w = np.array([1], np.uint8)
     sent, snap = orc.progress_send(pb, w, 0, 0)
     assert sent[0] == 0 and snap[0] == 0 and pb.flags[0] & 3 == 0 and pb.pending[0] == 0
@@ -153,3 +153,40 @@ def test_find_conflict_by_term_jump_equals_walk(orc):
             if jump is None:
                 jump = index
         assert walk == jump
+
+
+def test_readindex_and_checkquorum_scenarios_on_oracle(orc):
+    """TestReadOnlyOptionSafe, TestReadOnlyWithLearner (+ the learner-ack
+    rule), TestLeaderStepdownWhenQuorumActive / ...Lost, leader side,
+    through the oracle's ReadIndex ack and CheckQuorum
+    (tests/leader_round_scenarios.py)."""
+    from tests.leader_round_scenarios import SCENARIOS, OracleRoundBackend
+    for sc in SCENARIOS:
+        sc(OracleRoundBackend(orc))
+
+
+def test_byte_accounting_rules_on_oracle(orc):
+    """The oracle's algorithmic byte count of a round on a hand-checked
+    state: one group, S = 2 (leader slot 0, one follower in StateReplicate
+    with an empty ring), the follower acks index 5 of a 5-entry log in the
+    leader's term.  Reads: self_slot 1 + the log model and commit 32, per
+    slot Match 8 + message kind 1 (both tracked), the follower's m.Index 8
+    and its Next + packed word 12; writes: its Match 8 (Next stays 6, the
+    word stays Replicate|RecentActive with an empty ring) and the commit 8;
+    no optional outputs."""
+    pb = orc.ProgressBatch(1, 2, 8, 1, max_ents=0)
+    pb.first_index[0], pb.last_index[0], pb.term_start[0] = 1, 5, 1
+    pb.run_count[0] = 1
+    pb.match[:] = [5, 3]
+    pb.next[:] = [6, 6]
+    pb.set_peer(flags=np.array([1 | 8, 1 | 8], np.uint8), istart=0, icount=np.array([0, 0]))
+    pb.self_slot = np.array([0], np.uint8)
+    z = np.zeros(2, np.uint64)
+    o = orc.progress_step(pb, np.array([0, 1], np.uint8), np.array([0, 5], np.uint64), z, z,
+                          outputs=False, count_bytes=True)
+    # commit advanced 0 -> 5: bcastAppend to slot 1 (Next 6 > lastIndex: an
+    # empty MsgApp, nothing appended); the ack's FreeLE on an empty ring
+    # reads nothing; the word is unchanged (Replicate, RecentActive, empty)
+    want = (1 + 32) + (8 + 1) + (8 + 1 + 8) + 12 + 8 + 8
+    assert int(pb.committed[0]) == 5 and int(pb.match[1]) == 5
+    assert int(o.bytes[0]) == want, (int(o.bytes[0]), want)
