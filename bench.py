@@ -225,7 +225,8 @@ def progress_round_state(ps, msgs, seed=0x5EED):
     G, S, F, R = ps.G, ps.S, ps.F, ps.R
     goff, dev, st = ps.group_offset, ps.device, ps.stride
     u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev)  # noqa: E731
-    base = (1 << 20) + u(1, 1)[:st] % ((1 << 40) - (1 << 20))
+    top = 1 << int(os.environ.get("QE_BENCH_INDEX_BITS", "40"))  # A/B knob only
+    base = (1 << 20) + u(1, 1)[:st] % (top - (1 << 20))
     ps.match.copy_(base.repeat(S) + u(2) % 64)
     ps.next.copy_(ps.match + 1 + u(3) % 4)
     cnt = (u(4) % (F + 1)).to(torch.int32)

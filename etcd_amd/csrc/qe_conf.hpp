@@ -243,12 +243,14 @@ __device__ __forceinline__ void cc_group(const CCArgs &a, uint64_t g) {
   st(a.isl, c.isl & c.trk, r_isl);
   st(a.trk, c.trk, r_trk);
   if (c.al != r_al) a.auto_leave[g] = static_cast<uint8_t>(c.al);
-  // a slot the change tracks or untracks: its new ID (0 when removed)
-  const uint32_t flip = (c.trk ^ trk0) & full;
+  // a slot the change untracks: 0; a slot tracked afterwards whose ID is
+  // new (created, or freed and reused within the change list): the new ID
 #pragma unroll
-  for (int s = 0; s < S; s++)
-    if ((flip >> s) & 1u)
-      a.ids[static_cast<uint64_t>(s) * a.G + g] = ((c.trk >> s) & 1u) ? id[s] : 0ull;
+  for (int s = 0; s < S; s++) {
+    const bool was = (trk0 >> s) & 1u, now = (c.trk >> s) & 1u;
+    if ((was && !now) || (now && (!was || id[s] != id0[s])))
+      a.ids[static_cast<uint64_t>(s) * a.G + g] = now ? id[s] : 0ull;
+  }
   if (a.p_match && created) {
     const uint64_t li = a.last_index[g];
     for (int s = 0; s < S; s++) {

@@ -42,6 +42,15 @@ namespace qe {
 
 constexpr int kRingChunk = 8;  // F <= kRingChunk: closed-form ring writes
 
+// Timing probe only (never the product build): QE_RING32_PROBE stores ring
+// entries as 32-bit words in the same entry-major layout (values truncated),
+// to price what halving the ring's bytes would buy.
+#ifdef QE_RING32_PROBE
+typedef uint32_t ring_t;
+#else
+typedef uint64_t ring_t;
+#endif
+
 __device__ __forceinline__ uint64_t bld64(rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
@@ -114,7 +123,7 @@ struct PRun {
 };
 
 struct PSend {
-  uint64_t *rb;  // entry 0 of this slot's rings for the tile: entry k at rb[k*rs + lane]
+  ring_t *rb;  // entry 0 of this slot's rings for the tile: entry k at rb[k*rs + lane]
   uint64_t rs;   // stride
   uint32_t lane;
   bool row;      // F <= kRingChunk: the runs are written by ring_flush
@@ -206,7 +215,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
       const uint64_t last = run_val(here, 0, x.me, x.li);
       const uint32_t pos = ring_pos(p.start, p.count, x.F);
       if (on) {
-        x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] = last;
+        x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] = static_cast<ring_t>(last);
         if (run.n == 0) {
           run.p = pos;
           run.b = p.next;
@@ -243,7 +252,11 @@ __device__ __forceinline__ void ring_flush(const PSend &x, const PRun &r1, const
     const bool on1 = j1 < r1.n, on2 = j2 < r2.n;
     if (__builtin_amdgcn_ballot_w64(on1 || on2)) {
       const uint64_t v = on2 ? run_val(r2, j2, x.me, x.li) : run_val(r1, j1, x.me, x.li);
+#ifdef QE_RING32_PROBE
+      bst32(static_cast<uint32_t>(v), mk_rsrc(x.rb + k * x.rs, n * 4), (on1 || on2) ? x.lane * 4 : kOOB);
+#else
       bst64(v, mk_rsrc(x.rb + k * x.rs, n * 8), (on1 || on2) ? x.lane * 8 : kOOB);
+#endif
     }
   }
 }
@@ -360,7 +373,7 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 // slot's Progress loads are issued, not with that prefetch: one ring in
 // registers instead of two keeps the kernel at 3 waves/SIMD without scratch
 // (A/B: 3.51 vs 3.56 ms, 4 waves/SIMD spills and is slower).
-__device__ __forceinline__ void pb_ring(const PArgs &a, const uint64_t *rb, uint32_t lane,
+__device__ __forceinline__ void pb_ring(const PArgs &a, const ring_t *rb, uint32_t lane,
                                         bool ring, PB &b) {
   if (ring) {
 #pragma unroll
@@ -536,7 +549,9 @@ k_progress_step(PArgs a) {
       if (s + 1 < static_cast<uint32_t>(S))
         pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
                 ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt);
-      if (row_ring) pb_ring(a, a.ibuf + static_cast<uint64_t>(s) * F * a.stride + g0, lane, ring_of(s), cur);
+      if (row_ring)
+        pb_ring(a, reinterpret_cast<const ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0,
+                lane, ring_of(s), cur);
       ac.add(touched, 12);  // Next + the packed word
       ac.add(touched && tt == QE_MSG_APP_RESP_REJECT, 16);  // RejectHint + LogTerm
       PR p;
@@ -553,7 +568,7 @@ k_progress_step(PArgs a) {
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
-      x.rb = a.ibuf + static_cast<uint64_t>(s) * F * a.stride + g0;
+      x.rb = reinterpret_cast<ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0;
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
       // F > kRingChunk: cur.rw (zero on that path) takes the first entries
@@ -828,7 +843,7 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
     pr_unpack(p, x.pw[s]);
     p.pending = 0;
     p.reset = 0;
-    xs.rb = a.ibuf + static_cast<uint64_t>(s) * a.F * a.stride + g0;
+    xs.rb = reinterpret_cast<ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * a.F * a.stride + g0;
     xs.count_msgs = 0;
     xs.first_index = 0;
     xs.snapped = false;

@@ -354,7 +354,7 @@ def test_check_quorum_matches_oracle(eng, S, masks, extras):
     G = 5003
     pb = random_state(rng, G, S, 8, 2, masks, extras)
     ps = to_device(eng, pb, masks, extras)
-    for _ in range(2):
+    for rnd in range(2):
         st = eng.stats_buffer(DEV)
         qa = eng.check_quorum(ps, stats=st)
         got = eng.stats_reduce(st).cpu().numpy().view(np.uint64)
@@ -362,7 +362,8 @@ def test_check_quorum_matches_oracle(eng, S, masks, extras):
         np.testing.assert_array_equal(qa.cpu().numpy(), o_qa)
         np.testing.assert_array_equal(got, o_st)
         assert_same(ps, pb)
-        assert 0 < int(o_qa.sum()) < G or S == 16
+        if rnd == 0 and S <= 5:  # random RecentActive bits: both outcomes occur
+            assert 0 < int(o_qa.sum()) < G
 
 
 def test_bytes_requested_equal_oracle_on_bench_state(eng):
