@@ -74,6 +74,9 @@ WORKLOADS = {
     "progress_send": ("16M groups x bcastAppend after a proposal (qe_progress_send to the 4 "
                       "followers, StateReplicate, Inflights F=8 with room): one MsgApp and one "
                       "ring entry per peer", 1 << 24, 5, "psend"),
+    "check_quorum": ("16M groups x 5 peers: MsgCheckQuorum on the leader over the resident "
+                     "Progress words (QuorumActive over RecentActive, step-down mask, "
+                     "RecentActive reset; each follower active with p = 0.7)", 1 << 24, 5, "cq"),
     "confchange": ("16M groups x Changer.Simple(AddNode(learner), AddLearnerNode(new)) on "
                    "slot masks: promote a learner, add a learner with initProgress "
                    "(3 voters + 1 learner + 1 free slot)", 1 << 24, 5, "confchange"),
@@ -554,6 +557,37 @@ def setup(name, G, S, kind, d, stats):
         bpg = 1 + 16 + 2 + nw * (12 + 20)
         return step, bpg, G, "group-bcasts", {"ps": ps, "prepare": prepare,
                                               "t": (want, sent, snap)}
+    if kind == "cq":
+        ps = engine.ProgressState(G, S, 1, 1, d.dev, group_offset=goff, extras=("self_slot",))
+        act = counter_rows(G, S, 0xC4EC, goff, d.dev) % 10 < 7  # heard from within the timeout
+        ps.peer.copy_(act.to(torch.int32) * 8 + 1)  # StateReplicate (+ RecentActive)
+        ps.self_slot.fill_(0)
+        del act
+        qa = torch.empty(G, dtype=torch.uint8, device=d.dev)
+        pristine = ps.peer.clone()
+
+        def prepare():
+            ps.peer.copy_(pristine)
+
+        import ctypes as C
+        p_ = ps.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            engine.check("qe_check_quorum", lib.qe_check_quorum(C.byref(p_), engine._ptr(qa), sp,
+                                                                  stream))
+
+        # per group: self_slot read and the quorum-active byte written; every
+        # slot's word read (all tracked) and the words whose RecentActive
+        # changes written (counted on this state)
+        step()
+        torch.cuda.synchronize(d.dev)
+        changed = int((ps.peer.view(S, ps.stride)[:, :G] != pristine.view(S, ps.stride)[:, :G]).sum())
+        prepare()
+        bpg = 1 + 4 * S + 1 + 4 * changed / G
+        return step, bpg, G, "group-checks", {"ps": ps, "prepare": prepare, "t": qa}
     if kind == "collect":
         gen = torch.Generator(device=d.dev).manual_seed(0xC011 + d.rank)
         flags = (torch.rand(G, device=d.dev, generator=gen) < 0.5).to(torch.uint8)

@@ -34,6 +34,10 @@ DOMINANT = {
     "config2_n7": ("void qe::k_cv_stream<7, 0,", 2),
     "config3_joint": ("void qe::k_cv_stream<10, 2,", 2),
     "config3_joint_rot": ("void qe::k_cv_stream<10, 2,", 2),
+    "config3_joint_packed": ("void qe::k_cv_stream<10, 2,", 2),
+    # check_quorum: dword rows of the peer words (256 B per row instruction)
+    # and byte rows: 64-B requests, FETCH_SIZE x 1
+    "check_quorum": ("void qe::k_check_quorum<5,", 1),
     "config4_repl": ("void qe::k_repl_stream<5,", 2),
     "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 1),
     "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
