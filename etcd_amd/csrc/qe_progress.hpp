@@ -334,10 +334,9 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
 // sequence at once, with the next slot's loads issued before this slot's
 // work.
 // ---------------------------------------------------------------------------
-struct PB {  // per-peer loads of one slot
+struct PB {  // per-peer loads of one slot (the ring is loaded separately, pb_ring)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
-  uint64_t rw[kRingChunk];  // F <= kRingChunk: the peer's whole ring (pb_ring)
 };
 
 // Loads of slot row `row` (= s*stride + tile0): Next and the packed word of
@@ -363,8 +362,6 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
   }
-#pragma unroll
-  for (int k = 0; k < kRingChunk; k++) b.rw[k] = 0;
 }
 
 // (F <= kRingChunk) the peer's ring entries when FreeLE may run (`ring`:
@@ -374,11 +371,13 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 // registers instead of two keeps the kernel at 3 waves/SIMD without scratch
 // (A/B: 3.51 vs 3.56 ms, 4 waves/SIMD spills and is slower).
 __device__ __forceinline__ void pb_ring(const PArgs &a, const ring_t *rb, uint32_t lane,
-                                        bool ring, PB &b) {
+                                        bool ring, uint64_t (&rw)[kRingChunk]) {
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) rw[k] = 0;
   if (ring) {
 #pragma unroll
     for (int k = 0; k < kRingChunk; k++)
-      if (static_cast<uint32_t>(k) < a.F) b.rw[k] = rb[k * a.stride + lane];
+      if (static_cast<uint32_t>(k) < a.F) rw[k] = rb[k * a.stride + lane];
   }
 }
 
@@ -549,9 +548,11 @@ k_progress_step(PArgs a) {
       if (s + 1 < static_cast<uint32_t>(S))
         pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
                 ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt);
-      if (row_ring)
-        pb_ring(a, reinterpret_cast<const ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0,
-                lane, ring_of(s), cur);
+      // the current peer's ring (F <= kRingChunk: every entry row; memory
+      // rings: the first entries from start, below)
+      uint64_t rw[kRingChunk];
+      pb_ring(a, reinterpret_cast<const ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0,
+              lane, row_ring && ring_of(s), rw);
       ac.add(touched, 12);  // Next + the packed word
       ac.add(touched && tt == QE_MSG_APP_RESP_REJECT, 16);  // RejectHint + LogTerm
       PR p;
@@ -571,7 +572,7 @@ k_progress_step(PArgs a) {
       x.rb = reinterpret_cast<ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0;
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
-      // F > kRingChunk: cur.rw (zero on that path) takes the first entries
+      // F > kRingChunk: rw (zero on that path) takes the first entries
       // from start, loaded after the Progress arrived
       uint32_t npre = 0;
       if (!row_ring) {
@@ -583,7 +584,7 @@ k_progress_step(PArgs a) {
             uint32_t pos = p.start + k;
             if (pos >= F) pos -= F;
             if (pos >= F) pos = 0;  // invalid Inflights.start: stay inside the ring
-            if (static_cast<uint32_t>(k) < npre) cur.rw[k] = x.rb[static_cast<uint64_t>(pos) * x.rs + lane];
+            if (static_cast<uint32_t>(k) < npre) rw[k] = x.rb[static_cast<uint64_t>(pos) * x.rs + lane];
           }
         }
       }
@@ -668,8 +669,8 @@ k_progress_step(PArgs a) {
               pr_become_probe(p);
               pr_become_replicate(p);
             } else if (p.state == QE_PR_REPLICATE) {
-              const uint32_t fo = row_ring ? row_prefix_le(cur.rw, F, p.start, c_old, idx)
-                                           : mem_prefix_le(cur.rw, npre, p.start, c_old, idx, x);
+              const uint32_t fo = row_ring ? row_prefix_le(rw, F, p.start, c_old, idx)
+                                           : mem_prefix_le(rw, npre, p.start, c_old, idx, x);
               free_le<ACCT>(p, idx, c_old, fo, r1, x, ac);
             }
             // bcastAppend of this accept (skips the leader) / sendAppend if
@@ -685,10 +686,10 @@ k_progress_step(PArgs a) {
             // FreeFirstOne = FreeLE(buffer[start])
             uint64_t first;
             if (c_old == 0) first = run_val(r1, 0, x.me, li);
-            else if (row_ring) first = row_at(cur.rw, p.start < F ? p.start : 0u);
-            else first = cur.rw[0];
-            const uint32_t fo = row_ring ? row_prefix_le(cur.rw, F, p.start, c_old, first)
-                                         : mem_prefix_le(cur.rw, npre, p.start, c_old, first, x);
+            else if (row_ring) first = row_at(rw, p.start < F ? p.start : 0u);
+            else first = rw[0];
+            const uint32_t fo = row_ring ? row_prefix_le(rw, F, p.start, c_old, first)
+                                         : mem_prefix_le(rw, npre, p.start, c_old, first, x);
             free_le<ACCT>(p, first, c_old, fo, r1, x, ac);
           }
           k2 = p.match < li ? 1u : 0u;

@@ -41,7 +41,7 @@ DOMINANT = {
     "config4_repl": ("void qe::k_repl_stream<5,", 2),
     "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 1),
     "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
-    "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false>", 1),
+    "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false,", 1),
     # confchange: its ID block and u64 rows are read 512 B per instruction
     # (128-B requests): 2 x FETCH_SIZE = 75.0 B/group = its algorithmic reads
     # (r02h); round-2 summaries before r02h used 1
