@@ -517,7 +517,19 @@ int qe_confchange(const qe_conf *c, const qe_conf_changes *ch, const qe_progress
     a.p_pending = p->pending_snapshot;
     a.p_pw = p->peer;
   }
-  const dim3 grid(static_cast<unsigned>((a.G + kBlock - 1) / kBlock));
+  // chunks of up to kCCTPW tiles per wave, >= 2 so the two register sets
+  // overlap; shorter chunks when the batch cannot give every CU 32 waves
+  const uint64_t tiles = (a.G + 63) / 64;
+  const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
+  uint64_t chunk = g_tiles_per_wave > 0 ? static_cast<uint64_t>(g_tiles_per_wave)
+                                        : (tiles + waves - 1) / waves;
+  if (chunk < 2) chunk = 2;
+  if (chunk > static_cast<uint64_t>(kCCTPW)) chunk = kCCTPW;
+  a.chunk = static_cast<uint32_t>(chunk);
+  const uint64_t per_block = (kBlock / 64) * chunk;
+  const uint64_t blocks = (tiles + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  const dim3 grid(static_cast<unsigned>(blocks));
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (c->num_slots) {
 #define QE_CC_CASE(n) \

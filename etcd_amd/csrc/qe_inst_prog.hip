@@ -52,8 +52,19 @@ static int launch_progress_send(PArgs a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
-static int launch_check_quorum(const PArgs &a, bool masked, bool joint, hipStream_t st) {
-  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+static int launch_check_quorum(PArgs a, bool masked, bool joint, hipStream_t st) {
+  // the chunking of qe_progress_send (kSendTPW tiles per wave at most)
+  const uint64_t tiles = (a.G + 63) / 64;
+  const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
+  uint64_t chunk = g_tiles_per_wave > 0 ? static_cast<uint64_t>(g_tiles_per_wave)
+                                        : (tiles + waves - 1) / waves;
+  if (chunk < 2) chunk = 2;
+  if (chunk > static_cast<uint64_t>(kSendTPW)) chunk = kSendTPW;
+  a.chunk = static_cast<uint32_t>(chunk);
+  const uint64_t per_block = (kBlock / 64) * chunk;
+  const uint64_t blocks = (tiles + per_block - 1) / per_block;
+  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  const dim3 grid(static_cast<unsigned>(blocks));
   if (joint) hipLaunchKernelGGL((k_check_quorum<S, MT, true, true>), grid, dim3(kBlock), 0, st, a);
   else if (masked) hipLaunchKernelGGL((k_check_quorum<S, MT, true, false>), grid, dim3(kBlock), 0, st, a);
   else hipLaunchKernelGGL((k_check_quorum<S, MT, false, false>), grid, dim3(kBlock), 0, st, a);

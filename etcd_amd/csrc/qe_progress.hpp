@@ -900,62 +900,124 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
 }
 
 // qe_check_quorum: MsgCheckQuorum (raft/raft.go:997-1018) over the resident
-// Progress words.  One lane per group, a wave per 64-group tile; only the
-// tracked slots' words are loaded, only changed words are stored.
+// Progress words.  One lane per group; each wave owns a chunk of up to
+// kSendTPW tiles (as qe_progress_send): the chunk's masks (Voters[0] |
+// Voters[1] << 16, tracked) are staged in LDS first, so a tile's word loads
+// depend on an LDS read, and two register sets keep tile k+1's words in
+// flight while tile k is decided and stored.  Only the tracked slots' words
+// are loaded, only changed words are stored.
+template <int S>
+struct CQTile {
+  uint32_t mio, trk, self;
+  uint32_t w[S];
+};
+
+template <int S>
+__device__ __forceinline__ void cq_issue(const PArgs &a, uint64_t t, uint32_t lane, uint32_t mio,
+                                         uint32_t trk, CQTile<S> &x) {
+  const uint64_t g0 = t * 64;
+  const uint32_t n = tile_n(a.G, t);
+  x.mio = mio;
+  x.trk = trk;
+  x.self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
+#pragma unroll
+  for (int s = 0; s < S; s++)
+    x.w[s] = bld32(mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
+                   bit_off(trk, s, lane * 4));
+}
+
+template <int S, bool JOINT>
+__device__ __forceinline__ void cq_finish(const PArgs &a, uint64_t t, uint32_t lane,
+                                          const CQTile<S> &x, uint64_t (&cnt)[3]) {
+  const uint64_t g0 = t * 64;
+  const uint32_t n = tile_n(a.G, t);
+  const uint32_t trk = x.trk, mi = x.mio & 0xFFFFu, mo = JOINT ? (x.mio >> 16) : 0u;
+  // the leader sees itself active (when it still has a Progress)
+  const uint32_t selfb = x.self < static_cast<uint32_t>(S) ? ((1u << x.self) & trk) : 0u;
+  uint32_t ra = 0;
+#pragma unroll
+  for (int s = 0; s < S; s++) ra |= ((x.w[s] >> 3) & 1u) << s;
+  ra = (ra & trk) | selfb;
+  // QuorumActive: every voter with a Progress votes its RecentActive
+  const uint32_t present = (mi | mo) & trk;
+  const bool qa = joint_vote(mi, mo, present, ra & present) == kVoteWon;
+  // Visit: RecentActive = false for every tracked peer but the leader
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const uint32_t nw =
+        (x.w[s] & ~QE_PF_RECENT_ACTIVE) | (((selfb >> s) & 1u) ? QE_PF_RECENT_ACTIVE : 0u);
+    const bool wr = ((trk >> s) & 1u) && nw != x.w[s];
+#ifdef QE_CQ_FULLROW  // A/B knob: a row some lane changes is stored for every tracked lane
+    const bool wf = (trk >> s) & 1u;
+#else
+    const bool wf = wr;
+#endif
+    if (__builtin_amdgcn_ballot_w64(wr))
+      bst32(nw, mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
+            wf ? lane * 4 : kOOB);
+  }
+  if (a.qactive) bst8(qa ? 1u : 0u, mk_rsrc(a.qactive + g0, n), lane);
+  if (lane < n) {
+    cnt[0] += 1;
+    cnt[1] += qa ? 0u : 1u;
+    cnt[2] += mix64(((a.goff + g0 + lane) * kPhi) ^ (static_cast<uint64_t>(ra) << 32) ^
+                    (qa ? kQuorumSalt : 0ull));
+  }
+}
+
 template <int S, typename MT, bool MASKED, bool JOINT>
 __global__ __launch_bounds__(kBlock) void k_check_quorum(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
+  __shared__ uint32_t lds_m[kBlock / 64][kSendTPW][64];
+  __shared__ uint32_t lds_t[kBlock / 64][kSendTPW][64];
   uint64_t cnt[3] = {0, 0, 0};
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wave =
-      static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ntiles = (a.G + 63) / 64;
-  for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    const uint64_t g0 = t * 64;
-    const uint32_t n = tile_n(a.G, t);
-    const uint32_t mi =
-        MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * sizeof(MT)), lane) &
-                  kFull)
-               : kFull;
-    const uint32_t mo =
-        JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * sizeof(MT)), lane) &
-                 kFull)
-              : 0u;
-    const uint32_t trk =
-        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0,
-                                           n * sizeof(MT)), lane) & kFull)
-                  : kFull;
-    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
-    uint32_t w[S];
+  const uint64_t t0 = (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv) * a.chunk;
+  const uint32_t nt =
+      t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < a.chunk ? ntiles - t0 : a.chunk) : 0u;
+  if (nt > 0) {
+    const bool staged = MASKED || a.tracked;
+    if (staged) {
+      uint32_t mv[kSendTPW], tv[kSendTPW];
 #pragma unroll
-    for (int s = 0; s < S; s++)
-      w[s] = bld32(mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
-                   bit_off(trk, s, lane * 4));
-    // the leader sees itself active (when it still has a Progress)
-    const uint32_t selfb = self < static_cast<uint32_t>(S) ? ((1u << self) & trk) : 0u;
-    uint32_t ra = 0;
+      for (int k = 0; k < kSendTPW; k++) {
+        const uint64_t g0 = (t0 + k) * 64;
+        const uint32_t n = static_cast<uint32_t>(k) < nt ? tile_n(a.G, t0 + k) : 0u;
+        const uint32_t mi =
+            MASKED ? ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * sizeof(MT)), lane)
+                   : kFull;
+        const uint32_t mo =
+            JOINT ? ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * sizeof(MT)), lane)
+                  : 0u;
+        mv[k] = (mi & kFull) | ((mo & kFull) << 16);
+        tv[k] = a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0,
+                                                   n * sizeof(MT)), lane) & kFull)
+                          : kFull;
+      }
 #pragma unroll
-    for (int s = 0; s < S; s++) ra |= ((w[s] >> 3) & 1u) << s;
-    ra = (ra & trk) | selfb;
-    // QuorumActive: every voter with a Progress votes its RecentActive
-    const uint32_t present = (mi | mo) & trk;
-    const bool qa = joint_vote(mi, mo, present, ra & present) == kVoteWon;
-    // Visit: RecentActive = false for every tracked peer but the leader
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint32_t nw = (w[s] & ~QE_PF_RECENT_ACTIVE) | (((selfb >> s) & 1u) ? QE_PF_RECENT_ACTIVE : 0u);
-      const bool wr = ((trk >> s) & 1u) && nw != w[s];
-      if (__builtin_amdgcn_ballot_w64(wr))
-        bst32(nw, mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
-              wr ? lane * 4 : kOOB);
+      for (int k = 0; k < kSendTPW; k++) {
+        lds_m[wv][k][lane] = mv[k];
+        lds_t[wv][k][lane] = tv[k];
+      }
     }
-    if (a.qactive) bst8(qa ? 1u : 0u, opt_rsrc(a.qactive, g0, n), lane);
-    if (lane < n) {
-      cnt[0] += 1;
-      cnt[1] += qa ? 0u : 1u;
-      cnt[2] += mix64(((a.goff + g0 + lane) * kPhi) ^ (static_cast<uint64_t>(ra) << 32) ^
-                      (qa ? kQuorumSalt : 0ull));
+    auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k : ntiles; };
+    auto mio_of = [&](uint32_t k) -> uint32_t {
+      return k < nt ? (staged ? lds_m[wv][k][lane] : kFull) : 0u;
+    };
+    auto trk_of = [&](uint32_t k) -> uint32_t {
+      return k < nt ? (staged ? lds_t[wv][k][lane] : kFull) : 0u;
+    };
+    CQTile<S> xa, xb;
+    cq_issue<S>(a, tix(0), lane, mio_of(0), trk_of(0), xa);
+    for (uint32_t k = 0; k < nt; k += 2) {
+      cq_issue<S>(a, tix(k + 1), lane, mio_of(k + 1), trk_of(k + 1), xb);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the decision
+      cq_finish<S, JOINT>(a, tix(k), lane, xa, cnt);
+      cq_issue<S>(a, tix(k + 2), lane, mio_of(k + 2), trk_of(k + 2), xa);
+      __builtin_amdgcn_sched_barrier(0);
+      cq_finish<S, JOINT>(a, tix(k + 1), lane, xb, cnt);
     }
   }
   if (a.stats) {
