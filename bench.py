@@ -234,8 +234,9 @@ def progress_round_state(ps, msgs, seed=0x5EED):
     ps.next.copy_(ps.match + 1 + u(3) % 4)
     cnt = (u(4) % (F + 1)).to(torch.int32)
     ps.peer.copy_(cnt * (1 << 16) + (1 | 8))  # StateReplicate, RecentActive, start 0
-    for k in range(F):  # entry-major rings: [S][F][stride]
-        ps.ibuf.view(S, F, st)[:, k, :] = ps.match.view(S, st) + 1 + 8 * k
+    ks = 8 * torch.arange(F, device=dev, dtype=torch.int64).view(1, F)
+    for s in range(S):  # ring entry k = Match + 1 + 8k (start 0: the live ones are k < count)
+        ps.set_ring_slot(s, ps.match[s * st:(s + 1) * st].view(st, 1) + 1 + ks)
     ps.last_index.copy_(base[:G] + 128)
     ps.term_start.copy_(base[:G])
     ps.first_index.copy_(base[:G] - 64)
@@ -269,6 +270,13 @@ def psend_state(ps, seed=0x5E4D):
     start = (u(4) % F).to(torch.int32)
     cnt = (u(5) % F).to(torch.int32)
     ps.peer.copy_(cnt * (1 << 16) + start * (1 << 8) + (1 | 8))  # Replicate, RecentActive
+    # in-flight entries in ring order: the entry at position (start + j) % F
+    # is Match + 1 + j (the live ones j < count lie just above Match)
+    k = torch.arange(F, device=dev, dtype=torch.int64).view(1, F)
+    for s in range(S):
+        r = slice(s * st, (s + 1) * st)
+        j = torch.remainder(k - start[r].view(st, 1).to(torch.int64), F)
+        ps.set_ring_slot(s, ps.match[r].view(st, 1) + 1 + j)
     ps.last_index.copy_(base[:G] + 128)
     ps.first_index.copy_(base[:G] - 64)
 
@@ -489,9 +497,10 @@ def setup(name, G, S, kind, d, stats):
         # Every timed launch steps the SAME fresh state with the same round
         # of messages: the mutable state is restored from a pristine copy
         # before each launch (outside the kernel's HIP events), so no launch
-        # sees stale, already-applied duplicates.  The Inflights buffer needs
-        # no restore: a round appends only into free ring entries, and the
-        # live entries it reads are the restored (start, count) window.
+        # sees stale, already-applied duplicates.  The Inflights rings need
+        # no restore: a round writes free positions (live ones are written
+        # back unchanged), and the live entries it reads are the restored
+        # (start, count) window.
         mutable = ("match", "next", "pending", "peer", "committed")
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
@@ -551,10 +560,10 @@ def setup(name, G, S, kind, d, stats):
 
         # per group: want mask, firstIndex/lastIndex read, sent/snap masks
         # written; per wanted peer Next and the packed word read, Next, the
-        # word (count changes) and the appended entry written:
-        # 1 + 16 + 2 + 4 * (12 + 20) = 147 B
+        # word (count changes) and the appended entry's 32-bit word (ABI 4)
+        # written: 1 + 16 + 2 + 4 * (12 + 16) = 131 B
         nw = bin(full & ~1).count("1")
-        bpg = 1 + 16 + 2 + nw * (12 + 20)
+        bpg = 1 + 16 + 2 + nw * (12 + 16)
         return step, bpg, G, "group-bcasts", {"ps": ps, "prepare": prepare,
                                               "t": (want, sent, snap)}
     if kind == "cq":

@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 3
+QE_ABI_VERSION = 4
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -100,7 +100,7 @@ class QeProgress(C.Structure):
     _fields_ = [
         ("num_groups", u64), ("group_offset", u64), ("num_slots", u32), ("inflight_cap", u32),
         ("stride", u64), ("match", vp), ("next", vp), ("pending_snapshot", vp), ("peer", vp),
-        ("infl_buf", vp), ("committed", vp),
+        ("infl_lo", vp), ("infl_hi", vp), ("committed", vp),
         ("term_start", vp), ("first_index", vp), ("last_index", vp), ("log_runs", u32),
         ("reserved", u32), ("run_first", vp), ("run_term", vp), ("run_count", vp),
         ("inc_mask", vp), ("out_mask", vp),
@@ -119,6 +119,13 @@ class QePeerMsgs(C.Structure):
 QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
 QE_PF_STATE, QE_PF_PROBE_SENT, QE_PF_RECENT_ACTIVE = 3, 4, 8
 QE_PW_START_SHIFT, QE_PW_COUNT_SHIFT = 8, 16
+QE_PF_RING_WIDE = 16
+QE_PW_RING_MASK = 0xFF0000F0  # ring representation bits (ABI 4), not Progress state
+QE_RING_EPOCH_MAX = 0x7FF
+
+
+def QE_RING_PITCH(F):
+    return (int(F) + 3) & ~3
 QE_MSG_NONE, QE_MSG_APP_RESP, QE_MSG_APP_RESP_REJECT, QE_MSG_HEARTBEAT_RESP = 0, 1, 2, 3
 QE_MSG_SNAP_STATUS, QE_MSG_SNAP_STATUS_REJECT, QE_MSG_UNREACHABLE = 4, 5, 6
 QE_MAX_INFLIGHT = 255
@@ -180,6 +187,8 @@ PROTOTYPES = {
     "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp]),
     "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
+    "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
+    "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),
                                 C.POINTER(QeProgress), vp]),
     "qe_comm_id_bytes": (C.c_size_t, []),

@@ -373,13 +373,13 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   if (p->num_groups && p->stride < p->num_groups) return QE_EINVAL;
   if (p->out_mask && !p->inc_mask) return QE_EINVAL;
   if (p->num_groups &&
-      (!p->match || !p->next || !p->pending_snapshot || !p->peer || !p->infl_buf ||
+      (!p->match || !p->next || !p->pending_snapshot || !p->peer || !p->infl_lo || !p->infl_hi ||
        !p->committed || !p->term_start || !p->first_index || !p->last_index))
     return QE_EINVAL;
   if (p->num_groups && p->log_runs && (!p->run_first || !p->run_term || !p->run_count))
     return QE_EINVAL;
-  // ring rows are addressed with 32-bit offsets per 64-group tile
-  if (static_cast<uint64_t>(p->inflight_cap) * 8 * 64 * QE_MAX_SLOTS > 0x7FFFFFFFull)
+  // a slot's ring block of a 64-group tile is addressed with 32-bit offsets
+  if (static_cast<uint64_t>(QE_RING_PITCH(p->inflight_cap)) * 4 * 64 > 0x7FFFFFFFull)
     return QE_ERANGE;
   a = PArgs{};
   a.G = p->num_groups;
@@ -391,7 +391,9 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.next = p->next;
   a.pending = p->pending_snapshot;
   a.pw = p->peer;
-  a.ibuf = p->infl_buf;
+  a.ilo = p->infl_lo;
+  a.ihi = p->infl_hi;
+  a.FP = QE_RING_PITCH(p->inflight_cap);
   a.committed = p->committed;
   a.term_start = p->term_start;
   a.first_index = p->first_index;

@@ -682,7 +682,8 @@ struct PArgs {
   uint32_t F, R;
   uint64_t *match, *next, *pending;
   uint32_t *pw;  // [S][stride] packed per-peer words (QE_PW_*)
-  uint64_t *ibuf;
+  uint32_t *ilo, *ihi;  // Inflights rings, lane-major [S][stride][FP] (ABI 4)
+  uint32_t FP;          // QE_RING_PITCH(F)
   uint64_t *committed;
   const uint64_t *term_start, *first_index, *last_index, *snap_index;
   const uint64_t *run_first, *run_term;
@@ -712,6 +713,7 @@ struct PR {
   uint64_t match, next, pending;
   uint32_t state, probe_sent, recent_active, start, count;
   uint32_t reset;  // ResetState ran: PendingSnapshot must be written back
+  uint32_t rep;    // the word's ring representation bits (QE_PW_RING_MASK)
 };
 
 // The packed per-peer word (include/etcd_quorum.h QE_PW_*).
@@ -721,11 +723,12 @@ __device__ __forceinline__ void pr_unpack(PR &p, uint32_t w) {
   p.recent_active = (w >> 3) & 1u;
   p.start = (w >> QE_PW_START_SHIFT) & 0xFFu;
   p.count = (w >> QE_PW_COUNT_SHIFT) & 0xFFu;
+  p.rep = w & QE_PW_RING_MASK;
 }
 __device__ __forceinline__ uint32_t pr_pack(const PR &p) {
   return p.state | (p.probe_sent ? QE_PF_PROBE_SENT : 0u) |
          (p.recent_active ? QE_PF_RECENT_ACTIVE : 0u) | (p.start << QE_PW_START_SHIFT) |
-         (p.count << QE_PW_COUNT_SHIFT);
+         (p.count << QE_PW_COUNT_SHIFT) | p.rep;
 }
 
 __device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:84-90
@@ -735,6 +738,7 @@ __device__ __forceinline__ void pr_reset(PR &p, uint32_t st) {  // progress.go:8
   p.state = st;
   p.count = 0;
   p.start = 0;
+  p.rep = 0;  // an empty ring: epoch 0, not wide (canonical)
 }
 __device__ __forceinline__ void pr_become_probe(PR &p) {  // progress.go:112-125
   if (p.state == QE_PR_SNAPSHOT) {

@@ -441,4 +441,74 @@ int qe_slot_lookup(uint64_t num_groups, uint32_t num_slots, const uint64_t *slot
   return QE_OK;
 }
 
+// ---- Inflights rings: plain uint64 <-> infl_lo / infl_hi (ABI 4) ----------
+// The canonical representation (include/etcd_quorum.h): a peer with no live
+// entry has epoch 0 and is not wide; otherwise it is not wide iff every live
+// entry (positions start .. start+count-1 mod F, inflights.go:25-37) has the
+// same upper word h <= QE_RING_EPOCH_MAX, and then its epoch is h.  Both
+// words of every position are stored (infl_hi too), so unpacking a wide peer
+// returns every position exactly.
+int qe_ring_pack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                 uint64_t stride, const uint64_t *entries, uint32_t *peer,
+                 uint32_t *infl_lo, uint32_t *infl_hi) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (inflight_cap == 0 || inflight_cap > QE_MAX_INFLIGHT) return QE_ERANGE;
+  if (num_groups == 0) return QE_OK;
+  if (stride < num_groups || !entries || !peer || !infl_lo || !infl_hi) return QE_EINVAL;
+  const uint32_t F = inflight_cap, FP = QE_RING_PITCH(F);
+  for (uint32_t s = 0; s < num_slots; s++) {
+    parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
+      for (uint64_t g = b; g < e; g++) {
+        const uint64_t row = s * stride + g;
+        const uint64_t *src = entries + row * F;
+        uint32_t *lo = infl_lo + row * FP, *hi = infl_hi + row * FP;
+        for (uint32_t k = 0; k < FP; k++) {
+          const uint64_t v = k < F ? src[k] : 0;
+          lo[k] = static_cast<uint32_t>(v);
+          hi[k] = static_cast<uint32_t>(v >> 32);
+        }
+        uint32_t w = peer[row] & ~QE_PW_RING_MASK;
+        const uint32_t start = (w >> QE_PW_START_SHIFT) & 0xFFu;
+        const uint32_t count = (w >> QE_PW_COUNT_SHIFT) & 0xFFu;
+        if (count > 0) {
+          const uint32_t st = start < F ? start : 0;  // as the kernels read an invalid start
+          const uint32_t h = hi[st];
+          bool wide = h > QE_RING_EPOCH_MAX;
+          for (uint32_t j = 0; j < count && j < F && !wide; j++) {
+            uint32_t pos = st + j;
+            if (pos >= F) pos -= F;
+            wide = hi[pos] != h;
+          }
+          w |= wide ? QE_PF_RING_WIDE : QE_PW_EPOCH_BITS(h);
+        }
+        peer[row] = w;
+      }
+    });
+  }
+  return QE_OK;
+}
+
+int qe_ring_unpack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                   uint64_t stride, const uint32_t *infl_lo, const uint32_t *infl_hi,
+                   const uint32_t *peer, uint64_t *entries) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (inflight_cap == 0 || inflight_cap > QE_MAX_INFLIGHT) return QE_ERANGE;
+  if (num_groups == 0) return QE_OK;
+  if (stride < num_groups || !entries || !peer || !infl_lo || !infl_hi) return QE_EINVAL;
+  const uint32_t F = inflight_cap, FP = QE_RING_PITCH(F);
+  for (uint32_t s = 0; s < num_slots; s++) {
+    parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
+      for (uint64_t g = b; g < e; g++) {
+        const uint64_t row = s * stride + g;
+        const uint32_t w = peer[row];
+        const bool wide = (w & QE_PF_RING_WIDE) != 0;
+        const uint64_t h = QE_PW_EPOCH(w);
+        for (uint32_t k = 0; k < F; k++)
+          entries[row * F + k] = ((wide ? infl_hi[row * FP + k] : h) << 32) | infl_lo[row * FP + k];
+      }
+    });
+  }
+  return QE_OK;
+}
+
 }  // extern "C"

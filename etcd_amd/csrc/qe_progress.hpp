@@ -40,16 +40,7 @@
 
 namespace qe {
 
-constexpr int kRingChunk = 8;  // F <= kRingChunk: closed-form ring writes
-
-// Timing probe only (never the product build): QE_RING32_PROBE stores ring
-// entries as 32-bit words in the same entry-major layout (values truncated),
-// to price what halving the ring's bytes would buy.
-#ifdef QE_RING32_PROBE
-typedef uint32_t ring_t;
-#else
-typedef uint64_t ring_t;
-#endif
+constexpr int kRingChunk = 8;  // F <= kRingChunk: the ring lives in registers (row form)
 
 __device__ __forceinline__ uint64_t bld64(rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -69,6 +60,13 @@ __device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
 }
 __device__ __forceinline__ void bst32(uint32_t v, rsrc_t r, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 bld128(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst128(u32x4 v, rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 template <typename MT>
 __device__ __forceinline__ void bst_mask(uint32_t v, rsrc_t r, uint32_t lane, bool on = true) {
@@ -110,6 +108,24 @@ constexpr uint64_t kReadSalt = 0x8CB92BA72F3D8DD7ull;   // a released ReadIndex 
 constexpr uint64_t kQuorumSalt = 0xA0761D6478BD642Full; // CheckQuorum: quorum active
 
 // ---------------------------------------------------------------------------
+// Inflights rings (ABI 4, include/etcd_quorum.h): 32-bit entry words,
+// lane-major [S][stride][FP], the upper words given by the peer word's epoch
+// (or, for a "wide" peer, by infl_hi).  A tile's ring block for one slot is
+// 64 x FP words; lane l's ring starts at byte l*FP*4 of it, so a ring of
+// F <= 8 entries is one or two 16-byte accesses and one 32-byte HBM sector.
+// The partial-sector write of a single appended entry is what an Inflights.
+// Add costs the memory system (scripts/append_probe.hip: ~990 cycles per
+// wave for an 8-byte entry, ~505 for a 4-byte one, ~460 for rewriting the
+// whole 32-byte ring), hence 32-bit words and whole-ring writes where the
+// ring is in registers anyway.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool rep_wide(uint32_t rep) { return (rep & QE_PF_RING_WIDE) != 0; }
+__device__ __forceinline__ uint32_t rep_epoch(uint32_t rep) { return QE_PW_EPOCH(rep); }
+__device__ __forceinline__ uint64_t ent64(uint32_t hi, uint32_t lo) {
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------
 // Sends: raft.maybeSendAppend (raft/raft.go:432-492) in closed form.
 // ---------------------------------------------------------------------------
 // A run of Inflights entries appended by consecutive sends: n entries from
@@ -123,10 +139,9 @@ struct PRun {
 };
 
 struct PSend {
-  ring_t *rb;  // entry 0 of this slot's rings for the tile: entry k at rb[k*rs + lane]
-  uint64_t rs;   // stride
-  uint32_t lane;
-  bool row;      // F <= kRingChunk: the runs are written by ring_flush
+  rsrc_t rlo, rhi;  // this slot's ring block of the tile (infl_lo / infl_hi)
+  uint32_t lb;      // lane * FP * 4: the lane's ring in the block
+  bool row;         // F <= kRingChunk: the runs are written by ring_store_row
   uint32_t F, me;
   uint64_t fi, li, snap;
   uint32_t count_msgs;   // messages sent to this peer this round (saturating)
@@ -150,8 +165,48 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t start, uint32_t count, uin
   return pos;
 }
 
-constexpr uint32_t kLoop = 0xFFFFFFFFu;
+// Inflights.Add(v) at ring position pos, memory form (F > kRingChunk, and
+// the single appends of qe_progress_send): the entry's low word always; the
+// first entry of an empty ring sets the epoch (or, above QE_RING_EPOCH_MAX,
+// makes the ring wide); an entry whose upper word differs from the epoch of
+// a non-empty ring turns it wide -- every live entry's upper word (the
+// epoch) is written first, a rare path; a wide ring also gets the entry's
+// upper word.
+__device__ __forceinline__ void ring_add_mem(PR &p, const PSend &x, bool on, uint32_t pos,
+                                             uint64_t v) {
+  const uint32_t h = static_cast<uint32_t>(v >> 32);
+  bst32(static_cast<uint32_t>(v), x.rlo, on ? x.lb + pos * 4 : kOOB);
+  const bool first = p.count == 0;
+  const bool conv = on && !first && !rep_wide(p.rep) && h != rep_epoch(p.rep);
+  if (__builtin_amdgcn_ballot_w64(conv)) {
+    const uint32_t ep = rep_epoch(p.rep);
+    uint32_t q = p.start;
+    while (q >= x.F) q -= x.F;
+    for (uint32_t j = 0; __builtin_amdgcn_ballot_w64(conv && j < p.count); j++) {
+      bst32(ep, x.rhi, (conv && j < p.count) ? x.lb + q * 4 : kOOB);
+      if (++q >= x.F) q = 0;
+    }
+  }
+  if (on) {
+    if (first)
+      p.rep = h <= QE_RING_EPOCH_MAX ? QE_PW_EPOCH_BITS(h) : QE_PF_RING_WIDE;
+    else if (conv)
+      p.rep = QE_PF_RING_WIDE;
+  }
+  const bool whi = on && rep_wide(p.rep);
+  if (__builtin_amdgcn_ballot_w64(whi)) bst32(h, x.rhi, whi ? x.lb + pos * 4 : kOOB);
+}
 
+// Entry at ring position pos, memory form, decoded with the representation
+// `rep` the ring had when the round began.
+__device__ __forceinline__ uint64_t ring_get_mem(const PSend &x, uint32_t rep, bool on, uint32_t pos) {
+  const uint32_t off = on ? x.lb + pos * 4 : kOOB;
+  const uint32_t lo = bld32(x.rlo, off);
+  const uint32_t hi = rep_wide(rep) ? bld32(x.rhi, off) : rep_epoch(rep);
+  return ent64(hi, lo);
+}
+
+constexpr uint32_t kLoop = 0xFFFFFFFFu;
 
 // `k` consecutive raft.maybeSendAppend(to, sei) calls on one peer, or with
 // k = kLoop one call with `sei` followed by `for maybeSendAppend(to, false)
@@ -206,16 +261,16 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
       const PRun here{0, 0, p.next};
       p.next = run_val(here, added - 1, x.me, x.li) + 1;
       p.count += added;
-      ac.add(true, 8 * added);
+      ac.add(true, 4 * added);
     }
-  } else {  // F > kRingChunk: append entry by entry, straight to memory
+  } else {  // memory form: append entry by entry, straight to memory
     while (__builtin_amdgcn_ballot_w64(added < lim && p.next <= x.li)) {
       const bool on = added < lim && p.next <= x.li;
       const PRun here{0, 0, p.next};
       const uint64_t last = run_val(here, 0, x.me, x.li);
       const uint32_t pos = ring_pos(p.start, p.count, x.F);
+      ring_add_mem(p, x, on, pos, last);
       if (on) {
-        x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] = static_cast<ring_t>(last);
         if (run.n == 0) {
           run.p = pos;
           run.b = p.next;
@@ -225,7 +280,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
         p.count += 1;
         added += 1;
       }
-      ac.add(on, 8);
+      ac.add(on, 4);
     }
   }
   if (repl) {
@@ -239,25 +294,81 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
   }
 }
 
-// Row mode: entry row k is stored once, for the lanes whose runs cover
-// position k (the later run wins: it was appended after the earlier one).
-__device__ __forceinline__ void ring_flush(const PSend &x, const PRun &r1, const PRun &r2,
-                                           uint32_t n) {
-  if (!__builtin_amdgcn_ballot_w64((r1.n | r2.n) != 0)) return;
+// Row form (F <= kRingChunk): the whole ring of a peer whose ring may be
+// read or rewritten (`ld`: touched, with live entries) in registers, one or
+// two 16-byte loads per lane; hi[] holds every position's upper word (the
+// epoch unless the peer is wide).
+__device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
+                                              uint32_t (&lo)[kRingChunk],
+                                              uint32_t (&hi)[kRingChunk]) {
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) lo[k] = 0;
+  if (__builtin_amdgcn_ballot_w64(ld)) {
+    const u32x4 a = bld128(x.rlo, ld ? x.lb : kOOB);
+    lo[0] = a.x, lo[1] = a.y, lo[2] = a.z, lo[3] = a.w;
+    if (FP > 4) {
+      const u32x4 b = bld128(x.rlo, ld ? x.lb + 16 : kOOB);
+      lo[4] = b.x, lo[5] = b.y, lo[6] = b.z, lo[7] = b.w;
+    }
+  }
+  const uint32_t ep = rep_epoch(rep);
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) hi[k] = ep;
+  const bool w = ld && rep_wide(rep);
+  if (__builtin_amdgcn_ballot_w64(w)) {  // rare: entries straddling epochs
+    const u32x4 a = bld128(x.rhi, w ? x.lb : kOOB);
+    u32x4 b = {0, 0, 0, 0};
+    if (FP > 4) b = bld128(x.rhi, w ? x.lb + 16 : kOOB);
+    if (w) hi[0] = a.x, hi[1] = a.y, hi[2] = a.z, hi[3] = a.w;
+    if (w) hi[4] = b.x, hi[5] = b.y, hi[6] = b.z, hi[7] = b.w;
+  }
+}
+
+// Row form: the peer's ring after the round, where a run appended.
+// Positions a run covers take the run's entry (the later run wins: it was
+// appended after the earlier one), the others keep what was loaded; the ring
+// is written back whole (full 32-byte sectors, no partial-sector writes) and
+// its representation recomputed canonically from the live entries (the
+// upper words written only when the peer is wide).  A ring nothing appended
+// to keeps its representation: FreeLE and ResetState keep it valid.
+__device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun &r1,
+                                               const PRun &r2, bool touched, uint32_t rep_in,
+                                               uint32_t FP, uint32_t (&lo)[kRingChunk],
+                                               uint32_t (&hi)[kRingChunk]) {
+  const bool any = (r1.n | r2.n) != 0;
+  if (!__builtin_amdgcn_ballot_w64(touched && any)) return;  // the ring stands as loaded
+  uint32_t h0 = 0;
+  bool seen = false, uni = true;
+  const uint32_t st = p.start;
 #pragma unroll
   for (int k = 0; k < kRingChunk; k++) {
     if (static_cast<uint32_t>(k) >= x.F) break;
     const uint32_t j1 = static_cast<uint32_t>(k) >= r1.p ? k - r1.p : k + x.F - r1.p;
     const uint32_t j2 = static_cast<uint32_t>(k) >= r2.p ? k - r2.p : k + x.F - r2.p;
     const bool on1 = j1 < r1.n, on2 = j2 < r2.n;
-    if (__builtin_amdgcn_ballot_w64(on1 || on2)) {
+    if (on1 || on2) {
       const uint64_t v = on2 ? run_val(r2, j2, x.me, x.li) : run_val(r1, j1, x.me, x.li);
-#ifdef QE_RING32_PROBE
-      bst32(static_cast<uint32_t>(v), mk_rsrc(x.rb + k * x.rs, n * 4), (on1 || on2) ? x.lane * 4 : kOOB);
-#else
-      bst64(v, mk_rsrc(x.rb + k * x.rs, n * 8), (on1 || on2) ? x.lane * 8 : kOOB);
-#endif
+      lo[k] = static_cast<uint32_t>(v);
+      hi[k] = static_cast<uint32_t>(v >> 32);
     }
+    const uint32_t rel = static_cast<uint32_t>(k) >= st ? k - st : k + x.F - st;
+    if (rel < p.count) {
+      uni = uni && (!seen || hi[k] == h0);
+      h0 = seen ? h0 : hi[k];
+      seen = true;
+    }
+  }
+  const bool wide = seen && (!uni || h0 > QE_RING_EPOCH_MAX);
+  const bool wl = touched && any;
+  if (wl) p.rep = !seen ? 0u : (wide ? QE_PF_RING_WIDE : QE_PW_EPOCH_BITS(h0));
+  if (__builtin_amdgcn_ballot_w64(wl)) {
+    bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, wl ? x.lb : kOOB);
+    if (FP > 4) bst128(u32x4{lo[4], lo[5], lo[6], lo[7]}, x.rlo, wl ? x.lb + 16 : kOOB);
+  }
+  const bool wh = wl && wide;
+  if (__builtin_amdgcn_ballot_w64(wh)) {
+    bst128(u32x4{hi[0], hi[1], hi[2], hi[3]}, x.rhi, wh ? x.lb : kOOB);
+    if (FP > 4) bst128(u32x4{hi[4], hi[5], hi[6], hi[7]}, x.rhi, wh ? x.lb + 16 : kOOB);
   }
 }
 
@@ -273,53 +384,61 @@ __device__ __forceinline__ void free_le(PR &p, uint64_t to, uint32_t c_old, uint
   if (fr == c_old) {
     for (uint32_t j = 0; j < r1.n && run_val(r1, j, x.me, x.li) <= to; j++) fr++;
   }
-  ac.add(p.count > 0, 8 * (fr + 1 < p.count ? fr + 1 : p.count));
+  ac.add(p.count > 0, 4 * (fr + 1 < p.count ? fr + 1 : p.count));
   if (fr > 0) {
     p.count -= fr;
     uint32_t st2 = p.start + fr;
     while (st2 >= x.F) st2 -= x.F;
     p.start = p.count == 0 ? 0 : st2;
+    if (p.count == 0) p.rep = 0;  // empty ring: canonical representation
   }
 }
 
-// Initial ring entries <= to, from start: row-resident form (F <= kRingChunk).
-__device__ __forceinline__ uint32_t row_prefix_le(const uint64_t (&rw)[kRingChunk], uint32_t F,
+// Initial ring entries <= to, from start: row form (F <= kRingChunk).
+__device__ __forceinline__ uint32_t row_prefix_le(const uint32_t (&lo)[kRingChunk],
+                                                  const uint32_t (&hi)[kRingChunk], uint32_t F,
                                                   uint32_t start, uint32_t c_old, uint64_t to) {
   uint32_t pm = 0;
 #pragma unroll
   for (int k = 0; k < kRingChunk; k++)
-    pm |= (static_cast<uint32_t>(k) < F && rw[k] <= to) ? (1u << k) : 0u;
+    pm |= (static_cast<uint32_t>(k) < F && ent64(hi[k], lo[k]) <= to) ? (1u << k) : 0u;
   const uint32_t full = (1u << F) - 1u;
   const uint32_t st = start < F ? start : 0u;
   const uint32_t rk = ((pm >> st) | (pm << (F - st))) & full;  // bit k: entry of rank k
   const uint32_t run = __builtin_ctz(~rk);                     // <= F
   return run < c_old ? run : c_old;
 }
-// rw[pos] as masked ORs: a select chain here is turned into an indexed load
-// by the compiler, which would move the whole row to scratch memory
-__device__ __forceinline__ uint64_t row_at(const uint64_t (&rw)[kRingChunk], uint32_t pos) {
-  uint64_t v = 0;
+// The entry at pos as masked ORs: a select chain here is turned into an
+// indexed load by the compiler, which would move the whole ring to scratch
+__device__ __forceinline__ uint64_t row_at(const uint32_t (&lo)[kRingChunk],
+                                           const uint32_t (&hi)[kRingChunk], uint32_t pos) {
+  uint32_t l = 0, h = 0;
 #pragma unroll
-  for (int k = 0; k < kRingChunk; k++)
-    v |= rw[k] & (0ull - static_cast<uint64_t>(pos == static_cast<uint32_t>(k)));
-  return v;
+  for (int k = 0; k < kRingChunk; k++) {
+    const uint32_t m = 0u - static_cast<uint32_t>(pos == static_cast<uint32_t>(k));
+    l |= lo[k] & m;
+    h |= hi[k] & m;
+  }
+  return ent64(h, l);
 }
-// The same from memory (F > kRingChunk): e[] holds the first min(CH, c_old)
-// entries from start.
-__device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk], uint32_t npre,
+// The same from memory (F > kRingChunk): lo/hi hold the first min(CH,
+// c_old) entries from start, decoded with the round's initial
+// representation rep.
+__device__ __forceinline__ uint32_t mem_prefix_le(const uint32_t (&lo)[kRingChunk],
+                                                  const uint32_t (&hi)[kRingChunk], uint32_t npre,
                                                   uint32_t start, uint32_t c_old, uint64_t to,
-                                                  const PSend &x) {
+                                                  uint32_t rep, const PSend &x) {
   uint32_t fr = 0;
   bool go = true;
 #pragma unroll
   for (int k = 0; k < kRingChunk; k++) {
-    go = go && static_cast<uint32_t>(k) < npre && e[k] <= to;
+    go = go && static_cast<uint32_t>(k) < npre && ent64(hi[k], lo[k]) <= to;
     fr += go ? 1u : 0u;
   }
   if (fr == npre && fr < c_old) {
     uint32_t pos = start + fr;
     while (pos >= x.F) pos -= x.F;
-    while (fr < c_old && x.rb[static_cast<uint64_t>(pos) * x.rs + x.lane] <= to) {
+    while (fr < c_old && ring_get_mem(x, rep, true, pos) <= to) {
       fr++;
       if (++pos >= x.F) pos -= x.F;
     }
@@ -334,7 +453,7 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint64_t (&e)[kRingChunk
 // sequence at once, with the next slot's loads issued before this slot's
 // work.
 // ---------------------------------------------------------------------------
-struct PB {  // per-peer loads of one slot (the ring is loaded separately, pb_ring)
+struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's turn)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
 };
@@ -361,23 +480,6 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
   if (__builtin_amdgcn_ballot_w64(rej)) {
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
-  }
-}
-
-// (F <= kRingChunk) the peer's ring entries when FreeLE may run (`ring`:
-// lanes < n only), one coalesced entry row each (rb: entry 0 of this slot's
-// rings for the tile).  Loaded when the slot's turn comes, after the next
-// slot's Progress loads are issued, not with that prefetch: one ring in
-// registers instead of two keeps the kernel at 3 waves/SIMD without scratch
-// (A/B: 3.51 vs 3.56 ms, 4 waves/SIMD spills and is slower).
-__device__ __forceinline__ void pb_ring(const PArgs &a, const ring_t *rb, uint32_t lane,
-                                        bool ring, uint64_t (&rw)[kRingChunk]) {
-#pragma unroll
-  for (int k = 0; k < kRingChunk; k++) rw[k] = 0;
-  if (ring) {
-#pragma unroll
-    for (int k = 0; k < kRingChunk; k++)
-      if (static_cast<uint32_t>(k) < a.F) rw[k] = rb[k * a.stride + lane];
   }
 }
 
@@ -520,8 +622,7 @@ k_progress_step(PArgs a) {
     x.fi = fi;
     x.li = li;
     x.snap = a.snap_index ? snap_ld : fi - 1;
-    x.rs = a.stride;
-    x.lane = lane;
+    x.lb = lane * a.FP * 4;
     x.row = row_ring;
     uint32_t sent = 0, snapm = 0, tnow = 0;
     uint32_t acks = acks0;
@@ -548,11 +649,14 @@ k_progress_step(PArgs a) {
       if (s + 1 < static_cast<uint32_t>(S))
         pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
                 ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt);
-      // the current peer's ring (F <= kRingChunk: every entry row; memory
-      // rings: the first entries from start, below)
-      uint64_t rw[kRingChunk];
-      pb_ring(a, reinterpret_cast<const ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0,
-              lane, row_ring && ring_of(s), rw);
+      if (!__builtin_amdgcn_ballot_w64(touched)) {
+        // no event for this slot in any group of the tile (e.g. the leader's
+        // own slot): only the per-peer output
+        if (a.msg_count) bst8(0u, mk_rsrc(a.msg_count + row, n), lane);
+        ac.add(live && a.msg_count, 1);
+        if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
+        continue;
+      }
       ac.add(touched, 12);  // Next + the packed word
       ac.add(touched && tt == QE_MSG_APP_RESP_REJECT, 16);  // RejectHint + LogTerm
       PR p;
@@ -560,6 +664,7 @@ k_progress_step(PArgs a) {
       p.next = cur.nx;
       pr_unpack(p, cur.w);
       p.reset = 0;
+      const uint32_t rep0 = p.rep;
       // PendingSnapshot is read only in StateSnapshot (every other state only
       // ever overwrites it)
       const bool need_pd = touched && p.state == QE_PR_SNAPSHOT;
@@ -569,13 +674,24 @@ k_progress_step(PArgs a) {
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
-      x.rb = reinterpret_cast<ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * F * a.stride + g0;
+      {
+        const uint64_t rb = (static_cast<uint64_t>(s) * a.stride + g0) * a.FP;
+        x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
+        x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+      }
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
-      // F > kRingChunk: rw (zero on that path) takes the first entries
-      // from start, loaded after the Progress arrived
+      // the peer's ring: row form, the whole ring of a touched peer with live
+      // entries (its appends rewrite it whole); memory form, the first
+      // entries from start when FreeLE may run (loaded after the Progress
+      // arrived, FreeLE continues from memory)
+      uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
-      if (!row_ring) {
+      if (row_ring) {
+        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi);
+      } else {
+#pragma unroll
+        for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
         const bool scan = ring_of(s) && p.state == QE_PR_REPLICATE;
         npre = scan ? (c_old < CH ? c_old : CH) : 0u;
         if (__builtin_amdgcn_ballot_w64(npre > 0)) {
@@ -584,7 +700,9 @@ k_progress_step(PArgs a) {
             uint32_t pos = p.start + k;
             if (pos >= F) pos -= F;
             if (pos >= F) pos = 0;  // invalid Inflights.start: stay inside the ring
-            if (static_cast<uint32_t>(k) < npre) rw[k] = x.rb[static_cast<uint64_t>(pos) * x.rs + lane];
+            const uint64_t v = ring_get_mem(x, rep0, static_cast<uint32_t>(k) < npre, pos);
+            rlo[k] = static_cast<uint32_t>(v);
+            rhi[k] = static_cast<uint32_t>(v >> 32);
           }
         }
       }
@@ -669,8 +787,8 @@ k_progress_step(PArgs a) {
               pr_become_probe(p);
               pr_become_replicate(p);
             } else if (p.state == QE_PR_REPLICATE) {
-              const uint32_t fo = row_ring ? row_prefix_le(rw, F, p.start, c_old, idx)
-                                           : mem_prefix_le(rw, npre, p.start, c_old, idx, x);
+              const uint32_t fo = row_ring ? row_prefix_le(rlo, rhi, F, p.start, c_old, idx)
+                                           : mem_prefix_le(rlo, rhi, npre, p.start, c_old, idx, rep0, x);
               free_le<ACCT>(p, idx, c_old, fo, r1, x, ac);
             }
             // bcastAppend of this accept (skips the leader) / sendAppend if
@@ -686,10 +804,10 @@ k_progress_step(PArgs a) {
             // FreeFirstOne = FreeLE(buffer[start])
             uint64_t first;
             if (c_old == 0) first = run_val(r1, 0, x.me, li);
-            else if (row_ring) first = row_at(rw, p.start < F ? p.start : 0u);
-            else first = rw[0];
-            const uint32_t fo = row_ring ? row_prefix_le(rw, F, p.start, c_old, first)
-                                         : mem_prefix_le(rw, npre, p.start, c_old, first, x);
+            else if (row_ring) first = row_at(rlo, rhi, p.start < F ? p.start : 0u);
+            else first = ent64(rhi[0], rlo[0]);
+            const uint32_t fo = row_ring ? row_prefix_le(rlo, rhi, F, p.start, c_old, first)
+                                         : mem_prefix_le(rlo, rhi, npre, p.start, c_old, first, rep0, x);
             free_le<ACCT>(p, first, c_old, fo, r1, x, ac);
           }
           k2 = p.match < li ? 1u : 0u;
@@ -716,12 +834,14 @@ k_progress_step(PArgs a) {
       const uint32_t km = lp ? kLoop : k2 + k3;
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      if (row_ring) ring_flush(x, r1, r2, n);
+      if (row_ring) ring_store_row(p, x, r1, r2, touched, rep0, a.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
       const bool wm = touched && up, wn = touched && p.next != cur.nx;
       const bool wp = touched && (p.pending != pd0 || p.reset);
       const bool ww = touched && nw != cur.w;
+      // the ring representation bits are not Progress state (not counted)
+      const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
       if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
       if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
       if (__builtin_amdgcn_ballot_w64(wp))
@@ -733,7 +853,7 @@ k_progress_step(PArgs a) {
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);
-      ac.add(ww, 4);
+      ac.add(wc, 4);
       ac.add(live && a.msg_count, 1);
       ac.add(x.count_msgs && a.msg_index, 8);
       sent |= x.count_msgs ? (1u << s) : 0u;
@@ -828,10 +948,9 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
   xs.fi = x.fi;
   xs.li = x.li;
   xs.snap = a.snap_index ? x.sn : x.fi - 1;
-  xs.rs = a.stride;
-  xs.lane = lane;
-  // one maybeSendAppend appends at most one entry: stored directly at its
-  // ring position (one instruction), not as F entry-row stores
+  xs.lb = lane * a.FP * 4;
+  // one maybeSendAppend appends at most one entry: its 32-bit word stored
+  // directly at its ring position (one instruction, memory form)
   xs.row = false;
   uint32_t sent = 0, snapm = 0;
 #pragma unroll
@@ -844,7 +963,11 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
     pr_unpack(p, x.pw[s]);
     p.pending = 0;
     p.reset = 0;
-    xs.rb = reinterpret_cast<ring_t *>(a.ibuf) + static_cast<uint64_t>(s) * a.F * a.stride + g0;
+    {
+      const uint64_t rb = (static_cast<uint64_t>(s) * a.stride + g0) * a.FP;
+      xs.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
+      xs.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+    }
     xs.count_msgs = 0;
     xs.first_index = 0;
     xs.snapped = false;

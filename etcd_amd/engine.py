@@ -297,8 +297,10 @@ def pack_peer_word(flags, start=0, count=0):
 class ProgressState:
     """Device-resident leader-side Progress of G groups (qe_progress):
     match/next/pending [S][stride], the packed per-peer words `peer` [S][stride]
-    (int32 storage of the u32 QE_PW_* words), Inflights rings [S][F][stride]
-    (entry-major), committed, and the leader-log model (term runs).  `extras`
+    (int32 storage of the u32 QE_PW_* words), Inflights rings as 32-bit entry
+    words `ilo` / `ihi` [S][stride][QE_RING_PITCH(F)] (lane-major, ABI 4: the
+    upper words come from the peer word's epoch unless QE_PF_RING_WIDE),
+    committed, and the leader-log model (term runs).  `extras`
     allocates the optional per-group arrays: "tracked" (slot mask),
     "self_slot", "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""
 
@@ -319,7 +321,9 @@ class ProgressState:
         self.next = torch.ones(n, dtype=i64, device=dev)
         self.pending = torch.zeros(n, dtype=i64, device=dev)
         self.peer = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.ibuf = torch.zeros(self.S * self.F * self.stride, dtype=i64, device=dev)
+        self.FP = _lib.QE_RING_PITCH(self.F)
+        self.ilo = torch.zeros(n * self.FP, dtype=torch.int32, device=dev)
+        self.ihi = torch.zeros(n * self.FP, dtype=torch.int32, device=dev)
         self.committed = torch.zeros(self.G, dtype=i64, device=dev)
         self.term_start = torch.zeros(self.G, dtype=i64, device=dev)
         self.first_index = torch.ones(self.G, dtype=i64, device=dev)
@@ -341,21 +345,25 @@ class ProgressState:
     def struct(self):
         return _lib.QeProgress(
             self.G, self.group_offset, self.S, self.F, self.stride, _ptr(self.match),
-            _ptr(self.next), _ptr(self.pending), _ptr(self.peer), _ptr(self.ibuf),
+            _ptr(self.next), _ptr(self.pending), _ptr(self.peer), _ptr(self.ilo), _ptr(self.ihi),
             _ptr(self.committed), _ptr(self.term_start),
             _ptr(self.first_index), _ptr(self.last_index), self.R, 0, _ptr(self.run_first),
             _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
             _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
             _ptr(self.snap_index), self.max_ents, 0)
 
-    ARRAYS = ("match", "next", "pending", "peer", "ibuf", "committed",
+    ARRAYS = ("match", "next", "pending", "peer", "ilo", "ihi", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
               "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
 
     def load_host(self, **arrays):
         """numpy arrays (uint64 as uint64, masks as uint8/uint16, peer words
         as uint32).  flags / istart / icount (uint8 arrays, any subset) are
-        packed into the peer words (absent fields 0)."""
+        packed into the peer words (absent fields 0).  `ibuf` takes plain
+        uint64 Inflights rings, entry-major [S][F][stride] (the oracle's
+        layout), converted through qe_ring_pack after the peer words are in
+        place (their ring representation bits are recomputed)."""
+        ibuf = arrays.pop("ibuf", None)
         fields = {k: arrays.pop(k) for k in ("flags", "istart", "icount") if k in arrays}
         if fields:
             n = max(np.asarray(v).size for v in fields.values())
@@ -375,7 +383,65 @@ class ProgressState:
                 a = a.view(np.int32)
             a = a.reshape(-1)[: dst.numel()]
             dst[: a.size].copy_(torch.from_numpy(a.copy()).to(self.device))
+        if ibuf is not None:
+            self.load_rings(ibuf)
         return self
+
+    def load_rings(self, ibuf):
+        """Plain uint64 rings, entry-major [S][F][stride] -> ilo / ihi and the
+        peer words' representation bits (qe_ring_pack, host side)."""
+        S, F, st = self.S, self.F, self.stride
+        e = np.zeros(S * F * st, np.uint64)
+        a = np.asarray(ibuf, np.uint64).reshape(-1)[: e.size]
+        e[: a.size] = a
+        ent = np.ascontiguousarray(e.reshape(S, F, st).transpose(0, 2, 1))  # [S][stride][F]
+        peer = self.peer.cpu().numpy().view(np.uint32).copy()
+        lo = np.zeros(S * st * self.FP, np.uint32)
+        hi = np.zeros_like(lo)
+        check("qe_ring_pack", _lib.lib().qe_ring_pack(
+            self.G, S, F, st, ent.ctypes.data, peer.ctypes.data, lo.ctypes.data, hi.ctypes.data))
+        for dst, v in ((self.peer, peer), (self.ilo, lo), (self.ihi, hi)):
+            dst.copy_(torch.from_numpy(v.view(np.int32)).to(self.device))
+
+    def set_ring_slot(self, s, ent):
+        """Slot s's rings from a device int64 tensor [stride][F] (uint64
+        entries), in place on the device: the 32-bit words, and the peer
+        words' representation bits in canonical form (the rule of
+        qe_ring_pack) from their Inflights.start / count."""
+        S, F, st, FP = self.S, self.F, self.stride, self.FP
+        ent = ent.view(st, F)
+        lo = ent & 0xFFFFFFFF
+        hi = (ent >> 32) & 0xFFFFFFFF
+        as_i32 = lambda v: torch.where(v >= (1 << 31), v - (1 << 32), v).to(torch.int32)  # noqa: E731
+        rows = slice(s * st, (s + 1) * st)
+        self.ilo.view(S * st, FP)[rows, :F] = as_i32(lo)
+        self.ihi.view(S * st, FP)[rows, :F] = as_i32(hi)
+        w = self.peer[rows].to(torch.int64) & 0xFFFFFFFF
+        start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
+        k = torch.arange(F, device=self.device).view(1, F)
+        live = torch.remainder(k - start.view(st, 1), F) < count.view(st, 1)
+        hmin = torch.where(live, hi, 1 << 40).amin(1)
+        hmax = torch.where(live, hi, -1).amax(1)
+        uni = (hmin == hmax) & (hmax <= _lib.QE_RING_EPOCH_MAX)
+        h = torch.where(uni, hmin, 0)
+        ep_bits = ((h & 7) << 5) | ((h & 0x7F8) << 21)
+        rep = torch.where(count == 0, 0, torch.where(uni, ep_bits, _lib.QE_PF_RING_WIDE))
+        w = (w & ~_lib.QE_PW_RING_MASK & 0xFFFFFFFF) | rep
+        self.peer[rows] = as_i32(w)
+
+    def rings(self, peer=None):
+        """Every ring position decoded to uint64 (qe_ring_unpack), entry-major
+        [S][F][stride] flattened (groups >= G are 0)."""
+        S, F, st = self.S, self.F, self.stride
+        if peer is None:
+            peer = self.peer.cpu().numpy().view(np.uint32)
+        lo = self.ilo.cpu().numpy().view(np.uint32)
+        hi = self.ihi.cpu().numpy().view(np.uint32)
+        ent = np.zeros(S * st * F, np.uint64)
+        check("qe_ring_unpack", _lib.lib().qe_ring_unpack(
+            self.G, S, F, st, lo.ctypes.data, hi.ctypes.data,
+            np.ascontiguousarray(peer).ctypes.data, ent.ctypes.data))
+        return np.ascontiguousarray(ent.reshape(S, st, F).transpose(0, 2, 1)).reshape(-1)
 
     def host(self):
         out = {}
@@ -389,7 +455,8 @@ class ProgressState:
                 a.view(np.uint16) if a.dtype == np.int16 else (
                     a.view(np.uint32) if a.dtype == np.int32 else a))
         w = out["peer"]
-        out["flags"] = (w & 0xFF).astype(np.uint8)
+        out["ibuf"] = self.rings(w)
+        out["flags"] = (w & 0xF).astype(np.uint8)
         out["istart"] = ((w >> 8) & 0xFF).astype(np.uint8)
         out["icount"] = ((w >> 16) & 0xFF).astype(np.uint8)
         return out

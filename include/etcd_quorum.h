@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 3  /* 3: see INTEGRATION.md "ABI 3" (layout changes listed there) */
+#define QE_ABI_VERSION 4  /* 4: see INTEGRATION.md "ABI 4" (layout changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -280,24 +280,42 @@ int qe_election_steps(const qe_election_state *st,
 /* tracker.StateType (raft/tracker/state.go) and the packed per-peer word
  * (ABI 3: one u32 per peer replaces the flags / Inflights.start /
  * Inflights.count byte rows of ABI 2, so a peer's small fields move in one
- * 4-byte access):
+ * 4-byte access; ABI 4 adds the ring representation bits):
  *   bits 0-1   StateType (QE_PR_*)          bit 2  Progress.ProbeSent
- *   bit 3      Progress.RecentActive        bits 4-7  reserved (0)
- *   bits 8-15  Inflights.start              bits 16-23  Inflights.count
- *   bits 24-31 reserved (0)
- * Reserved bits must be 0 on input; the kernels write them as 0. */
+ *   bit 3      Progress.RecentActive        bit 4  QE_PF_RING_WIDE
+ *   bits 5-7   ring epoch bits 0-2          bits 8-15  Inflights.start
+ *   bits 16-23 Inflights.count              bits 24-31 ring epoch bits 3-10
+ * Inflights entries are stored as 32-bit words (infl_lo); the upper 32 bits
+ * of an entry are the peer's 11-bit ring epoch H (QE_PW_EPOCH) unless
+ * QE_PF_RING_WIDE is set, in which case they are infl_hi's word:
+ *   entry k = ((wide ? infl_hi[k] : H) << 32) | infl_lo[k].
+ * The form is canonical when count == 0 -> H = 0, not wide; else not wide
+ * iff every live entry's upper word is the same value < 2^11 (entries below
+ * 2^43 within one 2^32-aligned window: every realistic in-flight window),
+ * which is then H.  qe_ring_pack produces it and the kernels restore it
+ * whenever they append (a ring they only free entries from may stay wide).
+ * qe_ring_pack / qe_ring_unpack convert plain uint64 rings.  Ring
+ * representation bits are not Progress state: QE_PW_RING_MASK selects them. */
 #define QE_PR_PROBE 0
 #define QE_PR_REPLICATE 1
 #define QE_PR_SNAPSHOT 2
 #define QE_PF_STATE 3u          /* word & QE_PF_STATE = StateType            */
 #define QE_PF_PROBE_SENT 4u     /* Progress.ProbeSent                        */
 #define QE_PF_RECENT_ACTIVE 8u  /* Progress.RecentActive                     */
+#define QE_PF_RING_WIDE 16u     /* ABI 4: entries' upper words in infl_hi     */
 #define QE_PW_START_SHIFT 8     /* Inflights.start = (word >> 8) & 0xFF       */
 #define QE_PW_COUNT_SHIFT 16    /* Inflights.count = (word >> 16) & 0xFF      */
+#define QE_PW_RING_MASK 0xFF0000F0u /* ABI 4: WIDE + epoch bits               */
+#define QE_RING_EPOCH_MAX 0x7FFu    /* largest epoch held in the word         */
+#define QE_PW_EPOCH(w) ((((w) >> 5) & 7u) | (((w) >> 21) & 0x7F8u))
+#define QE_PW_EPOCH_BITS(h) ((((uint32_t)(h) & 7u) << 5) | (((uint32_t)(h) & 0x7F8u) << 21))
 #define QE_PW_PACK(state, probe_sent, recent_active, start, count)                 \
   ((uint32_t)(state) | ((probe_sent) ? QE_PF_PROBE_SENT : 0u) |                   \
    ((recent_active) ? QE_PF_RECENT_ACTIVE : 0u) |                                 \
    ((uint32_t)(start) << QE_PW_START_SHIFT) | ((uint32_t)(count) << QE_PW_COUNT_SHIFT))
+/* ABI 4: words per peer ring in infl_lo / infl_hi (F rounded up to 4, so a
+ * ring of F <= 8 is one or two 16-byte accesses, one 32-byte HBM sector) */
+#define QE_RING_PITCH(F) (((uint32_t)(F) + 3u) & ~3u)
 #define QE_MAX_INFLIGHT 255     /* Inflights capacity (MaxInflightMsgs)      */
 #define QE_MAX_LOG_RUNS 16      /* term runs of the leader-log model          */
 
@@ -330,9 +348,12 @@ typedef struct qe_progress {
   uint32_t *peer;               /* [S][stride] packed per-peer word (ABI 3):
                                    StateType, ProbeSent, RecentActive,
                                    Inflights.start / count (QE_PW_*)         */
-  uint64_t *infl_buf;           /* [S][F][stride] Inflights.buffer, entry-
-                                   major: entry k of slot s of group g at
-                                   (s*F + k)*stride + g                      */
+  uint32_t *infl_lo;            /* ABI 4: [S][stride][QE_RING_PITCH(F)]
+                                   Inflights.buffer, low 32 bits, lane-major:
+                                   entry k of slot s of group g at
+                                   (s*stride + g)*QE_RING_PITCH(F) + k       */
+  uint32_t *infl_hi;            /* ABI 4: same shape, high 32 bits; read and
+                                   written only for QE_PF_RING_WIDE peers    */
   uint64_t *committed;          /* [G] raftLog.committed (rw)                */
   const uint64_t *term_start;   /* [G]                                       */
   const uint64_t *first_index;  /* [G] raftLog.firstIndex()                  */
@@ -448,6 +469,22 @@ int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stat
  * outcome. */
 int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
                      void *sent, void *snap, void *stream);
+
+/* ABI 4, HOST pointers: Inflights rings between plain uint64 buffers
+ * (Inflights.buffer of each peer, raft/tracker/inflights.go:25-37, peer-major
+ * [S][stride][F]: entry k of slot s of group g at (s*stride + g)*F + k) and
+ * the device form (infl_lo / infl_hi, pitch QE_RING_PITCH(F)).  qe_ring_pack
+ * also writes each peer word's ring representation bits (QE_PW_RING_MASK,
+ * canonical form; the other bits are kept: Inflights.start / count must be
+ * set).  qe_ring_unpack decodes all F entries of every peer (positions
+ * outside the live window decode like live ones; their values are whatever
+ * the ring holds there, as in the reference).  Groups [0, num_groups). */
+int qe_ring_pack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                 uint64_t stride, const uint64_t *entries, uint32_t *peer,
+                 uint32_t *infl_lo, uint32_t *infl_hi);
+int qe_ring_unpack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                   uint64_t stride, const uint32_t *infl_lo, const uint32_t *infl_hi,
+                   const uint32_t *peer, uint64_t *entries);
 
 /* ---- sparse MsgAppResp deltas ------------------------------------------ */
 

@@ -844,6 +844,9 @@ enum { PR_PROBE = 0, PR_REPLICATE = 1, PR_SNAPSHOT = 2 };
 #define PF_STATE 3u
 #define PF_PROBE_SENT 4u
 #define PF_RECENT_ACTIVE 8u
+/* bits of the device word that describe the ring's representation (ABI 4,
+ * QE_PW_RING_MASK), not Progress state: ignored here */
+#define PW_RING_MASK 0xFF0000F0u
 
 typedef struct orc_pr {
   uint64_t match, next, pending;
@@ -857,20 +860,23 @@ typedef struct orc_pr {
 
 static inline uint64_t *ib(orc_pr *p, uint32_t k) { return &p->buf[(uint64_t)k * p->bstride]; }
 
-/* inflights.go:55-71 Add (accounting: the 8-B entry written) */
+/* inflights.go:55-71 Add (accounting: the entry written, 4 B -- the 32-bit
+ * entry word of the device representation, ABI 4; the upper words of a
+ * ring straddling a 2^32 boundary are representation overhead, not
+ * counted) */
 static void infl_add(orc_pr *p, uint64_t x) {
   uint32_t nx = p->start + p->count;
   if (nx >= p->size) nx -= p->size;
   *ib(p, nx) = x;
   p->count++;
-  if (p->acct) *p->acct += 8;
+  if (p->acct) *p->acct += 4;
 }
 /* inflights.go:87-113 FreeLE (accounting: every entry the loop reads,
- * min(count, freed + 1) of them) */
+ * min(count, freed + 1) of them, 4 B each as in infl_add) */
 static void infl_free_le(orc_pr *p, uint64_t to) {
   if (p->count == 0) return;
   if (to < *ib(p, p->start)) {
-    if (p->acct) *p->acct += 8;
+    if (p->acct) *p->acct += 4;
     return;
   }
   uint32_t idx = p->start, i;
@@ -878,7 +884,7 @@ static void infl_free_le(orc_pr *p, uint64_t to) {
     if (to < *ib(p, idx)) break;
     if (++idx >= p->size) idx -= p->size;
   }
-  if (p->acct) *p->acct += 8 * (uint64_t)(i < p->count ? i + 1 : i);
+  if (p->acct) *p->acct += 4 * (uint64_t)(i < p->count ? i + 1 : i);
   p->count -= i;
   p->start = idx;
   if (p->count == 0) p->start = 0;
@@ -971,9 +977,11 @@ uint64_t orc_find_conflict_by_term(uint32_t nruns, const uint64_t *first, const 
 }
 
 /* The leader-side state of G groups (mirrors qe_progress of
- * include/etcd_quorum.h, ABI 3) and one round of peer messages (mirrors
- * qe_peer_msgs).  Slot s of group g lives at [s*stride + g]; entry k of
- * that peer's Inflights ring at ibuf[(s*F + k)*stride + g] (entry-major).
+ * include/etcd_quorum.h, except that the Inflights rings are plain uint64
+ * as in the reference, entry-major: entry k of slot s of group g at
+ * ibuf[(s*F + k)*stride + g]; tests convert through qe_ring_pack /
+ * qe_ring_unpack) and one round of peer messages (mirrors qe_peer_msgs).
+ * Slot s of group g lives at [s*stride + g].
  * pw is the packed per-peer word: StateType bits 0-1, ProbeSent bit 2,
  * RecentActive bit 3, Inflights.start bits 8-15, Inflights.count 16-23. */
 typedef struct orc_prog {
@@ -1186,7 +1194,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         match0[s] = prs[s].match;
         next0[s] = prs[s].next;
         pend0[s] = prs[s].pending;
-        word0[s] = a->pw[s * a->stride + g];
+        word0[s] = a->pw[s * a->stride + g] & ~PW_RING_MASK;
         state0[s] = prs[s].state;
         if (m->msg_count) m->msg_count[s * a->stride + g] = 0;
       }

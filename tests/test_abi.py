@@ -58,7 +58,7 @@ int main(void) {
   Z(qe_gen_params) F(qe_gen_params, dist) F(qe_gen_params, mask_mode)
   Z(qe_confstate_csr) F(qe_confstate_csr, learners_next_off) F(qe_confstate_csr, learners)
   F(qe_confstate_csr, auto_leave) F(qe_confstate_csr, perm)
-  Z(qe_progress) F(qe_progress, peer) F(qe_progress, infl_buf) F(qe_progress, log_runs)
+  Z(qe_progress) F(qe_progress, peer) F(qe_progress, infl_lo) F(qe_progress, infl_hi) F(qe_progress, log_runs)
   F(qe_progress, out_mask) F(qe_progress, tracked) F(qe_progress, snap_index)
   F(qe_progress, max_ents)
   Z(qe_peer_msgs) F(qe_peer_msgs, bcast) F(qe_peer_msgs, timeout_now) F(qe_peer_msgs, msg_index)
@@ -96,7 +96,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 3
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 4
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0
@@ -106,7 +106,7 @@ def test_constants_and_introspection():
     for name, val in [("QE_VOTE_PENDING", 1), ("QE_VOTE_LOST", 2), ("QE_VOTE_WON", 3),
                       ("QE_STATS_COUNTERS", 16), ("QE_STATS_SHARDS", 64), ("QE_EINVAL", -22),
                       ("QE_PF_RECENT_ACTIVE", 8), ("QE_PW_START_SHIFT", 8),
-                      ("QE_PW_COUNT_SHIFT", 16)]:
+                      ("QE_PW_COUNT_SHIFT", 16), ("QE_PF_RING_WIDE", 16)]:
         m = re.search(rf"#define {name} \(?(-?\d+)u?\)?", src)
         assert m and int(m.group(1)) == val, name
 
@@ -176,3 +176,67 @@ def test_missing_library_fails_loudly(tmp_path):
             "try:\n import etcd_amd\nexcept ImportError as e:\n print('IMPORTERROR', e)\n")
     out = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT)
     assert "IMPORTERROR" in out.stdout, out.stdout + out.stderr
+
+
+def _ring_case(rng, G, S, F):
+    """Random peer words (start < F, count <= F) and uint64 rings mixing
+    small indices, indices near 2^32 boundaries (rings that straddle one)
+    and indices past the 11-bit epoch (2^43)."""
+    import numpy as np
+    n = S * G
+    start = rng.integers(0, F, n)
+    count = rng.integers(0, F + 1, n)
+    w = (rng.integers(0, 16, n) | (start << 8) | (count << 16)).astype(np.uint32)
+    kind = rng.integers(0, 4, n)
+    base = np.where(kind == 0, rng.integers(0, 1 << 20, n),
+                    np.where(kind == 1, (rng.integers(1, 1 << 11, n) << 32) - rng.integers(0, 6, n),
+                             np.where(kind == 2, rng.integers(0, 1 << 43, n),
+                                      rng.integers(1 << 43, 1 << 62, n)))).astype(np.uint64)
+    ent = base.reshape(S, 1, G) + np.arange(F, dtype=np.uint64).reshape(1, F, 1)
+    return w, np.ascontiguousarray(ent.transpose(0, 2, 1)).reshape(-1)  # [S][G][F]
+
+
+@pytest.mark.parametrize("F", [1, 3, 8, 13, 255])
+def test_ring_pack_unpack_roundtrip(F):
+    """qe_ring_pack / qe_ring_unpack (host side, ABI 4): every live entry
+    round-trips exactly; the representation is canonical (empty -> epoch 0,
+    not wide; one upper word <= QE_RING_EPOCH_MAX -> that epoch; else wide);
+    Progress bits of the word are kept."""
+    import numpy as np
+    rng = np.random.default_rng(F)
+    G, S = 700, 3
+    w, ent = _ring_case(rng, G, S, F)
+    FP = _lib.QE_RING_PITCH(F)
+    lo = np.zeros(S * G * FP, np.uint32)
+    hi = np.zeros_like(lo)
+    peer = w.copy()
+    L = _lib.lib()
+    assert L.qe_ring_pack(G, S, F, G, ent.ctypes.data, peer.ctypes.data, lo.ctypes.data,
+                          hi.ctypes.data) == _lib.QE_OK
+    assert np.array_equal(peer & ~np.uint32(_lib.QE_PW_RING_MASK), w & ~np.uint32(_lib.QE_PW_RING_MASK))
+    back = np.zeros_like(ent)
+    assert L.qe_ring_unpack(G, S, F, G, lo.ctypes.data, hi.ctypes.data, peer.ctypes.data,
+                            back.ctypes.data) == _lib.QE_OK
+    e2, b2 = ent.reshape(S * G, F), back.reshape(S * G, F)
+    start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
+    wide = (peer & _lib.QE_PF_RING_WIDE) != 0
+    epoch = ((peer >> 5) & 7) | ((peer >> 21) & 0x7F8)
+    n_wide = 0
+    for i in range(S * G):
+        pos = [(int(start[i]) + j) % F for j in range(int(count[i]))]
+        assert np.array_equal(b2[i, pos], e2[i, pos]), i
+        his = {int(e2[i, q]) >> 32 for q in pos}
+        if not pos:
+            assert not wide[i] and epoch[i] == 0
+        elif len(his) == 1 and max(his) <= _lib.QE_RING_EPOCH_MAX:
+            assert not wide[i] and epoch[i] == his.pop()
+        else:
+            assert wide[i] and epoch[i] == 0
+            assert np.array_equal(b2[i], e2[i])  # wide: both words of every position
+            n_wide += 1
+    assert n_wide > 0
+    # argument checks
+    assert L.qe_ring_pack(G, 0, F, G, None, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_ring_pack(G, S, 256, G, None, None, None, None) == _lib.QE_ERANGE
+    assert L.qe_ring_unpack(G, S, F, G - 1, lo.ctypes.data, hi.ctypes.data, peer.ctypes.data,
+                            back.ctypes.data) == _lib.QE_EINVAL

@@ -28,8 +28,12 @@ def eng():
     return engine
 
 
-def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
+def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0, base=0):
+    """A random leader-side state.  `base` shifts every log index (ABI 4:
+    near a 2^32 boundary the Inflights rings straddle two epochs, past 2^43
+    every ring is wide)."""
     pb = orc.ProgressBatch(G, S, F, R, max_ents=max_ents)
+    pb.base = base
     # leader log: runs over [dummy, last]
     for g in range(G):
         nr = int(rng.integers(1, R + 1))
@@ -58,10 +62,10 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
                        (rng.integers(0, 2, n) * 8)).astype(np.uint8),
                 istart=rng.integers(0, F, n).astype(np.uint8),
                 icount=rng.integers(0, F + 1, n).astype(np.uint8))
-    base = pb.match.copy()
+    m0 = pb.match.copy()
     for k in range(F):  # entry-major rings: entry k of slot s at (s*F + k)*stride + g
         pb.ibuf[(np.arange(S)[:, None] * F + k) * pb.stride + np.arange(G)[None, :]] = \
-            (base.reshape(S, G) + 1 + 2 * ((k - pb.istart.reshape(S, G).astype(int)) % F)).astype(np.uint64)
+            (m0.reshape(S, G) + 1 + 2 * ((k - pb.istart.reshape(S, G).astype(int)) % F)).astype(np.uint64)
     md = orc.mask_dtype(S)
     if "inc" in masks:
         pb.inc = rng.integers(0, 1 << S, G).astype(md)
@@ -78,6 +82,13 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0):
                                       rng.integers(0, S, G)).astype(np.uint8)
     if "snap_index" in extras:
         pb.snap_index = (pb.first_index - 1 + rng.integers(0, 3, G)).astype(np.uint64)
+    if base:
+        b = np.uint64(base)
+        for k in ("match", "next", "pending", "ibuf", "committed", "term_start", "first_index",
+                  "last_index", "run_first"):
+            setattr(pb, k, (getattr(pb, k) + b).astype(np.uint64))
+        if pb.snap_index is not None:
+            pb.snap_index = (pb.snap_index + b).astype(np.uint64)
     return pb
 
 
@@ -85,9 +96,10 @@ def random_msgs(rng, pb):
     n = pb.S * pb.G
     mtype = rng.integers(0, 8, n).astype(np.uint8)  # 7 = unknown kind -> ignored
     li = np.tile(pb.last_index, pb.S)
+    lo = np.uint64(getattr(pb, "base", 0))
     mindex = np.where(rng.random(n) < 0.5, pb.next - 1,
-                      (rng.random(n) * (li + 3)).astype(np.uint64)).astype(np.uint64)
-    mhint = (rng.random(n) * (li + 2)).astype(np.uint64)
+                      lo + (rng.random(n) * (li - lo + 3)).astype(np.uint64)).astype(np.uint64)
+    mhint = (lo + (rng.random(n) * (li - lo + 2)).astype(np.uint64)).astype(np.uint64)
     mlogterm = np.where(rng.random(n) < 0.3, 0, rng.integers(1, 10, n)).astype(np.uint64)
     return mtype, mindex, mhint, mlogterm
 
@@ -104,12 +116,28 @@ def to_device(eng, pb, masks, extras=()):
     return ps
 
 
+RING_MASK = np.uint32(0xFF0000F0)  # QE_PW_RING_MASK: representation bits (ABI 4)
+
+
+def live_entries(pw, S, F, stride):
+    """Entry-major [S][F][stride] mask of the live Inflights positions
+    (start .. start+count-1 mod F, raft/tracker/inflights.go:25-37)."""
+    w = pw.reshape(S, 1, stride).astype(np.int64)
+    start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
+    k = np.arange(F).reshape(1, F, 1)
+    return (((k - start) % F) < count).reshape(-1)
+
+
 def assert_same(ps, pb):
+    """Progress state equal to the oracle's: every field, the peer words
+    without their ring representation bits, and every live ring entry
+    (decoded from the 32-bit form; dead positions are unobservable)."""
     h = ps.host()
     for k in ("match", "next", "pending", "committed"):
         np.testing.assert_array_equal(h[k], getattr(pb, k), err_msg=k)
-    np.testing.assert_array_equal(h["peer"], pb.pw, err_msg="packed peer words")
-    np.testing.assert_array_equal(h["ibuf"], pb.ibuf, err_msg="ibuf")
+    np.testing.assert_array_equal(h["peer"] & ~RING_MASK, pb.pw, err_msg="packed peer words")
+    live = live_entries(pb.pw, pb.S, pb.F, pb.stride)
+    np.testing.assert_array_equal(h["ibuf"][live], pb.ibuf[live], err_msg="live ring entries")
 
 
 def to_dev_mask(a, S):
@@ -206,6 +234,43 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
             np.testing.assert_array_equal(qa.cpu().numpy(), o_qa)
             np.testing.assert_array_equal(got2, o_st)
             assert_same(ps, pb)
+
+
+@pytest.mark.parametrize("F", [8, 32])
+@pytest.mark.parametrize("base", [(1 << 32) - 37, (1 << 43) - 29, 3 * (1 << 44) + 11])
+def test_progress_rings_across_epochs(eng, base, F):
+    """ABI 4's 32-bit ring words with every log index shifted by `base`:
+    rings straddling a 2^32 boundary (wide conversions on append, on the
+    whole-ring rewrite and in the memory form), and indices past the 11-bit
+    epoch (every ring wide), through the step, the send and CheckQuorum,
+    against the oracle's plain uint64 rings."""
+    rng = np.random.default_rng(base % 1000 + F)
+    G, S, R = 3001, 5, 3
+    pb = random_state(rng, G, S, F, R, (), EXTRAS, max_ents=int(rng.integers(0, 4)), base=base)
+    ps = to_device(eng, pb, (), EXTRAS)
+    md = orc.mask_dtype(S)
+    wide_seen = 0
+    for rnd in range(5):
+        mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
+        msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+        if rnd % 2:
+            msgs.bytes_requested = torch.zeros(1, dtype=torch.int64, device=DEV)
+        eng.progress_step(ps, msgs)
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, count_bytes=True)
+        assert_same(ps, pb)
+        assert_outputs(msgs, o, S)
+        if rnd % 2:
+            assert int(msgs.bytes_requested.item()) == int(o.bytes[0])
+        want = rng.integers(0, 1 << S, G).astype(md)
+        sei, me = int(rnd % 2), int(rng.integers(0, 5))
+        ps.max_ents = pb.max_ents = me
+        sent, snap = eng.progress_send(ps, to_dev_mask(want, S), sei)
+        o_sent, o_snap = orc.progress_send(pb, want, sei)
+        np.testing.assert_array_equal(sent.cpu().numpy().view(md), o_sent)
+        np.testing.assert_array_equal(snap.cpu().numpy().view(md), o_snap)
+        assert_same(ps, pb)
+        wide_seen += int(((ps.peer & 16) != 0).sum())
+    assert wide_seen > 0
 
 
 @pytest.mark.parametrize("R", [8, 9, 16])
@@ -383,7 +448,7 @@ def test_bytes_requested_equal_oracle_on_bench_state(eng):
     for k in ("match", "next", "pending", "ibuf", "committed", "term_start", "first_index",
               "last_index", "run_first", "run_term", "run_count", "self_slot"):
         setattr(pb, k, h[k].copy())
-    pb.pw = h["peer"].copy()
+    pb.pw = h["peer"] & ~RING_MASK
     mtype = msgs.type.cpu().numpy()
     mix = [msgs.index, msgs.reject_hint, msgs.log_term]
     mindex, mhint, mlogterm = (t.cpu().numpy().view(np.uint64) for t in mix)
