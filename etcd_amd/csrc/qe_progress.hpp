@@ -567,9 +567,19 @@ k_progress_step(PArgs a) {
     // message kinds, 4 bits per slot, for the rolled phase-2 loop (kinds
     // above QE_MSG_UNREACHABLE are "no message")
     uint64_t tys = 0;
+    // per-lane slot masks (bit s = slot s), so per-slot conditions below are
+    // bit tests, not short-circuit logic the compiler turns into branches
+    uint32_t msgm = 0, rejm = 0, appm = 0, hbm = 0;
 #pragma unroll
-    for (int s = 0; s < S; s++)
-      tys |= static_cast<uint64_t>(ty[s] <= QE_MSG_UNREACHABLE ? ty[s] : 15u) << (4 * s);
+    for (int s = 0; s < S; s++) {
+      const uint32_t t = ty[s];
+      tys |= static_cast<uint64_t>(t <= QE_MSG_UNREACHABLE ? t : 15u) << (4 * s);
+      msgm |= (t - 1u <= QE_MSG_UNREACHABLE - 1u ? 1u : 0u) << s;
+      rejm |= (t == QE_MSG_APP_RESP_REJECT ? 1u : 0u) << s;
+      appm |= (t == QE_MSG_APP_RESP ? 1u : 0u) << s;
+      hbm |= (t == QE_MSG_HEARTBEAT_RESP ? 1u : 0u) << s;
+    }
+    const uint32_t ixm = appm | rejm;  // slots whose message carries m.Index
     // ---- round trip 2: m.Index of every MsgAppResp and slot 0's peer loads ----
     uint64_t ix[S];
 #pragma unroll
@@ -583,17 +593,10 @@ k_progress_step(PArgs a) {
     }
     bool runs_counted = false;  // ACCT: the run table counts once, when first used
     auto ty_of = [&](uint32_t s) -> uint32_t { return static_cast<uint32_t>(tys >> (4 * s)) & 15u; };
-    auto has_ix_of = [&](uint32_t s) -> bool {
-      const uint32_t t = ty_of(s);
-      return t == QE_MSG_APP_RESP || t == QE_MSG_APP_RESP_REJECT;
-    };
     PB cur;
     {  // slot 0, before phase 1: every possible event
-      const uint32_t t0 = ty_of(0);
-      const bool msg = t0 >= QE_MSG_APP_RESP && t0 <= QE_MSG_UNREACHABLE;
-      const bool ld = (trk & 1u) && (msg || self != 0u);
-      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, t0 == QE_MSG_APP_RESP_REJECT,
-              has_ix_of(0), cur);
+      const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
+      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0, cur);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
@@ -627,28 +630,23 @@ k_progress_step(PArgs a) {
     uint32_t sent = 0, snapm = 0, tnow = 0;
     uint32_t acks = acks0;
     bool released = false;
-    auto touched_of = [&](uint32_t s) -> bool {
-      const bool tr = (trk >> s) & 1u;
-      const uint32_t t = ty_of(s);
-      const bool msg = t >= QE_MSG_APP_RESP && t <= QE_MSG_UNREACHABLE;
-      return tr && (msg || (bset != 0 && s != self));
-    };
-    auto ring_of = [&](uint32_t s) -> bool {  // FreeLE may run for this peer
-      const uint32_t t = ty_of(s);
-      return touched_of(s) && ((t == QE_MSG_APP_RESP && ((upd >> s) & 1u)) ||
-                               t == QE_MSG_HEARTBEAT_RESP);
-    };
+    // touched: a tracked peer with a message, or a bcast target (every
+    // tracked slot but the leader's when some accept advanced the commit);
+    // ringm: FreeLE may run for this peer
+    const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
+    const uint32_t tchm = trk & (msgm | (bset != 0 ? (kFull & ~selfb) : 0u));
+    const uint32_t ringm = tchm & ((appm & upd) | hbm);
     // rolled over the slots (one copy of the per-peer code; the next slot's
     // loads are issued before this slot's work)
 #pragma unroll 1
     for (uint32_t s = 0; s < static_cast<uint32_t>(S); s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const uint32_t tt = ty_of(s);
-      const bool touched = touched_of(s);
+      const bool touched = ((tchm >> s) & 1u) != 0;
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
-        pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, touched_of(s + 1),
-                ty_of(s + 1) == QE_MSG_APP_RESP_REJECT, has_ix_of(s + 1), nxt);
+        pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
+                ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0, nxt);
       if (!__builtin_amdgcn_ballot_w64(touched)) {
         // no event for this slot in any group of the tile (e.g. the leader's
         // own slot): only the per-peer output
@@ -692,7 +690,7 @@ k_progress_step(PArgs a) {
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
-        const bool scan = ring_of(s) && p.state == QE_PR_REPLICATE;
+        const bool scan = ((ringm >> s) & 1u) != 0 && p.state == QE_PR_REPLICATE;
         npre = scan ? (c_old < CH ? c_old : CH) : 0u;
         if (__builtin_amdgcn_ballot_w64(npre > 0)) {
 #pragma unroll
