@@ -240,3 +240,34 @@ def test_ring_pack_unpack_roundtrip(F):
     assert L.qe_ring_pack(G, S, 256, G, None, None, None, None) == _lib.QE_ERANGE
     assert L.qe_ring_unpack(G, S, F, G - 1, lo.ctypes.data, hi.ctypes.data, peer.ctypes.data,
                             back.ctypes.data) == _lib.QE_EINVAL
+
+
+@pytest.mark.parametrize("F", [5, 8])
+def test_set_ring_slot_matches_ring_pack(F):
+    """engine.ProgressState.set_ring_slot (the bench's device-side ring
+    builder, torch ops only -- run here on CPU tensors) writes the same
+    32-bit words and representation bits as the host packer qe_ring_pack."""
+    import numpy as np
+    import torch
+
+    from etcd_amd import engine
+    rng = np.random.default_rng(40 + F)
+    G, S = 300, 3
+    ps = engine.ProgressState(G, S, F, 1, device="cpu", stride=320)
+    st = ps.stride
+    w, ent = _ring_case(rng, st, S, F)  # [S][st][F] uint64
+    ps.peer.copy_(torch.from_numpy(w.view(np.int32)))
+    for s in range(S):
+        e = torch.from_numpy(ent.reshape(S, st, F)[s].copy().view(np.int64))
+        ps.set_ring_slot(s, e)
+    FP = _lib.QE_RING_PITCH(F)
+    lo = np.zeros(S * st * FP, np.uint32)
+    hi = np.zeros_like(lo)
+    peer = w.copy()
+    assert _lib.lib().qe_ring_pack(st, S, F, st, ent.ctypes.data, peer.ctypes.data,
+                                   lo.ctypes.data, hi.ctypes.data) == _lib.QE_OK
+    assert np.array_equal(ps.peer.numpy().view(np.uint32), peer)
+    got_lo = ps.ilo.numpy().view(np.uint32).reshape(S * st, FP)[:, :F]
+    got_hi = ps.ihi.numpy().view(np.uint32).reshape(S * st, FP)[:, :F]
+    assert np.array_equal(got_lo, lo.reshape(S * st, FP)[:, :F])
+    assert np.array_equal(got_hi, hi.reshape(S * st, FP)[:, :F])
