@@ -498,6 +498,49 @@ def progress_scenarios():
                          {"op": "step", "msgs": {"2": {"type": "accept", "index": 2}},
                           "expect": {"timeout_now": [2],
                                      "peers": {"2": {"state": 1, "match": 2, "next": 3}}}}]})
+    # TestProgressPaused (raft_test.go:97-109): two peers, becomeLeader
+    # appends 1:t1 (node 2: Probe, Next 1); three MsgProp -> appendEntry +
+    # bcastAppend each: one MsgApp in all (the probe pauses node 2).
+    base = {"S": 2, "self": 0, "max_ents": 0,
+            "log": {"first_index": 1, "last_index": 1, "term_start": 1, "committed": 0,
+                    "runs": [[0, 0], [1, 1]]}}
+    steps = []
+    for i in range(3):
+        steps += [{"op": "append"}, {"op": "send", "want": [1], "send_if_empty": 1,
+                                      "expect": {"sent": [1] if i == 0 else []}}]
+    sc.append(dict(base, name="TestProgressPaused", source="raft/raft_test.go:97-109",
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateProbe")], steps=steps))
+    # TestProgressResumeByHeartbeatResp (:78-95): node 2 ProbeSent = true
+    # stays so through MsgBeat (heartbeats only, no Progress change: the
+    # check); then BecomeReplicate (the state below) and MsgHeartbeatResp
+    # -> ProbeSent false.
+    sc.append(dict(base, name="TestProgressResumeByHeartbeatResp",
+                   source="raft/raft_test.go:78-95",
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateReplicate")],
+                   steps=[{"op": "step", "msgs": {"1": {"type": "heartbeat"}},
+                           "expect": {"peers": {"1": {"probe_sent": False}}}}]))
+    # TestProgressFlowControl (:111-177): MaxInflightMsgs 3 (inflight_cap),
+    # MaxSizePerMsg 2048 over 1000-byte entries = 2 entries per MsgApp
+    # (max_ents; the first MsgApp, [1:empty, 2], also carries 2).  Node 2
+    # BecomeProbe (Next 1); ten MsgProp: one MsgApp (probe).  Ack of 2 ->
+    # Replicate, commit 2, bcast + send loop: three MsgApps of 2 entries
+    # ([3,4] [5,6] [7,8]: Next 9, ring full).  Ack of 8: two MsgApps, of 2
+    # and 1 entries ([9,10] [11]: Next 12).
+    steps = []
+    for i in range(10):
+        steps += [{"op": "append"},
+                  {"op": "send", "want": [1], "send_if_empty": 1,
+                   "expect": {"sent": [1] if i == 0 else [],
+                              "peers": {"1": {"probe_sent": True, "next": 1}}}}]
+    steps += [{"op": "step", "msgs": {"1": {"type": "accept", "index": 2}},
+               "expect": {"messages": 3, "msg_index": {"1": 2}, "committed": 2,
+                          "peers": {"1": {"state": 1, "match": 2, "next": 9, "inflights": 3}}}},
+              {"op": "step", "msgs": {"1": {"type": "accept", "index": 8}},
+               "expect": {"messages": 2, "msg_index": {"1": 8}, "committed": 8,
+                          "peers": {"1": {"match": 8, "next": 12, "inflights": 2}}}}]
+    sc.append(dict(base, name="TestProgressFlowControl", source="raft/raft_test.go:111-177",
+                   max_ents=2, inflight_cap=3,
+                   peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateProbe")], steps=steps))
     return sc
 
 

@@ -22,6 +22,12 @@ from tests.golden_util import GOLDEN
 KIND = {"accept": 1, "reject": 2, "heartbeat": 3, "snap_status": 4, "snap_status_reject": 5,
         "unreachable": 6}
 F_CAP = 255  # the tests' MaxInflightMsgs is 256; the slot model caps it at 255
+
+
+def cap(sc):
+    """The scenario's Inflights capacity (MaxInflightMsgs): F_CAP unless the
+    test sets its own (TestProgressFlowControl: 3)."""
+    return int(sc.get("inflight_cap", F_CAP))
 PF_PROBE_SENT, PF_RECENT_ACTIVE = 4, 8
 
 
@@ -42,7 +48,7 @@ def initial_arrays(sc):
                            (PF_RECENT_ACTIVE if p["recent_active"] else 0)
                            for p in sc["peers"]], np.uint8),
         "icount": np.array([len(p["ring"]) for p in sc["peers"]], np.uint8),
-        "ibuf": np.zeros(S * F_CAP, np.uint64),
+        "ibuf": np.zeros(S * cap(sc), np.uint64),
         "committed": np.array([lg["committed"]], np.uint64),
         "term_start": np.array([lg["term_start"]], np.uint64),
         "first_index": np.array([lg["first_index"]], np.uint64),
@@ -57,7 +63,7 @@ def initial_arrays(sc):
         a["snap_index"] = np.array([lg["snap_index"]], np.uint64)
     for s, p in enumerate(sc["peers"]):
         for k, v in enumerate(p["ring"]):
-            a["ibuf"][s * F_CAP + k] = v
+            a["ibuf"][s * cap(sc) + k] = v
     return a
 
 
@@ -133,7 +139,7 @@ class OracleBackend:
 
     def load(self, sc, a):
         S = sc["S"]
-        pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
+        pb = self.orc.ProgressBatch(1, S, cap(sc), len(sc["log"]["runs"]), max_ents=sc["max_ents"])
         a = dict(a)
         pb.pw = self.orc.pack_word(a.pop("flags"), 0, a.pop("icount"))
         for k, v in a.items():

@@ -13,7 +13,7 @@ import torch
 
 from oracle import orc
 from tests.golden_util import raft_tables
-from tests.progress_scenarios import F_CAP, peer_view, run_scenario, scenarios
+from tests.progress_scenarios import cap, peer_view, run_scenario, scenarios
 from tests.test_progress_oracle import log_runs
 
 pytestmark = pytest.mark.gpu
@@ -327,7 +327,7 @@ class GpuBackend:
 
     def load(self, sc, a, inc=None):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
-        ps = self.eng.ProgressState(1, sc["S"], F_CAP, len(sc["log"]["runs"]), DEV, stride=1,
+        ps = self.eng.ProgressState(1, sc["S"], cap(sc), len(sc["log"]["runs"]), DEV, stride=1,
                                     extras=EXTRAS, max_ents=sc["max_ents"],
                                     masks=("inc",) if inc is not None else ())
         ps.tracked = None  # every slot holds a Progress (as the oracle backend)
