@@ -541,6 +541,24 @@ def progress_scenarios():
     sc.append(dict(base, name="TestProgressFlowControl", source="raft/raft_test.go:111-177",
                    max_ents=2, inflight_cap=3,
                    peers=[_peer(1, 2, "StateReplicate"), _peer(0, 1, "StateProbe")], steps=steps))
+    # TestHandleHeartbeatResp (:1312-1354): storage 1:t1 2:t2 3:t3, Term 1,
+    # becomeLeader appends 4:t1 (node 2: Probe, Next 4), commitTo(4).  Two
+    # heartbeat responses each re-send the probe MsgApp (Index 3); the ack of
+    # 4 (its sendAppend is consumed unchecked); then a heartbeat response
+    # sends nothing.  The log model's term_start is 4 (the commit never moves
+    # here, so index 1's term-1 entry plays no part).
+    sc.append({"name": "TestHandleHeartbeatResp", "source": "raft/raft_test.go:1312-1354",
+               "S": 2, "self": 0, "max_ents": 0,
+               "log": {"first_index": 1, "last_index": 4, "term_start": 4, "committed": 4,
+                       "runs": [[0, 0], [1, 1], [2, 2], [3, 3], [4, 1]]},
+               "peers": [_peer(4, 5, "StateReplicate"), _peer(0, 4, "StateProbe")],
+               "steps": [{"op": "step", "msgs": {"1": {"type": "heartbeat"}},
+                          "expect": {"messages": 1, "msg_index": {"1": 3}}},
+                         {"op": "step", "msgs": {"1": {"type": "heartbeat"}},
+                          "expect": {"messages": 1, "msg_index": {"1": 3}}},
+                         {"op": "step", "msgs": {"1": {"type": "accept", "index": 4}}},
+                         {"op": "step", "msgs": {"1": {"type": "heartbeat"}},
+                          "expect": {"messages": 0}}]})
     return sc
 
 

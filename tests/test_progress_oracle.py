@@ -105,7 +105,7 @@ def test_progress_scenarios_on_oracle(orc):
     for sc in scenarios():
         run_scenario(sc, OracleBackend(orc))
         names.append(sc["name"])
-    assert len(names) == 22
+    assert len(names) == 23
 
 
 def test_send_if_empty_precedes_snapshot(orc):
