@@ -167,8 +167,29 @@ def leader_stepdown_when_quorum_lost(be):
     assert _stepdown_run(be, heartbeats=False) is False
 
 
+def add_node_check_quorum(be):
+    """TestAddNodeCheckQuorum (raft/raft_test.go:3221-3251), from the conf
+    change on: a single-voter leader (checkQuorum, electionTimeout 10) adds
+    node 2 one tick before its quorum check.  initProgress gives the new
+    Progress RecentActive = true (confchange.go:240-262), so the check at
+    the next tick keeps the leader (and resets node 2's RecentActive); with
+    no word from node 2 the check electionTimeout ticks later steps it
+    down."""
+    S = 2
+    sc = {"name": "", "S": S, "self": 0, "max_ents": 0,
+          "log": {"runs": [[0, 0], [1, 1]], "committed": 1, "term_start": 1, "first_index": 1,
+                  "last_index": 1},
+          "peers": [_peer(1, 2, REPLICATE), _peer(0, 1, 0, recent_active=True)]}
+    be.load(sc, initial_arrays(sc))
+    qa, ra = be.check_quorum()
+    assert qa == 1 and ra == 0b01, (qa, ra)  # still the leader
+    qa, ra = be.check_quorum()
+    assert qa == 0, (qa, ra)  # steps down
+
+
 SCENARIOS = [read_only_option_safe, read_only_with_learner, learner_ack_does_not_count,
-             leader_stepdown_when_quorum_active, leader_stepdown_when_quorum_lost]
+             leader_stepdown_when_quorum_active, leader_stepdown_when_quorum_lost,
+             add_node_check_quorum]
 
 
 class OracleRoundBackend:
