@@ -756,9 +756,10 @@ __device__ __forceinline__ void pr_become_replicate(PR &p) {  // progress.go:127
   p.next = p.match + 1;
 }
 __device__ __forceinline__ bool pr_paused(const PR &p, uint32_t F) {  // progress.go:201-212
-  if (p.state == QE_PR_PROBE) return p.probe_sent;
-  if (p.state == QE_PR_REPLICATE) return p.count == F;
-  return true;
+  // Probe: ProbeSent; Replicate: Inflights.Full(); Snapshot: always (as
+  // selects, not a branch chain)
+  const bool probe = p.state == QE_PR_PROBE, repl = p.state == QE_PR_REPLICATE;
+  return probe ? p.probe_sent != 0 : (repl ? p.count == F : true);
 }
 
 // raftLog.findConflictByTerm (raft/log.go:147-168) on the term-run model,

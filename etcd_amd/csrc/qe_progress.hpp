@@ -245,11 +245,15 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
   const uint64_t d = x.li - p.next;  // valid when repl
   uint32_t added = 0;
   if (x.row) {  // lim <= F <= kRingChunk: count the appends directly
-    uint32_t fit = 1;  // MsgApps whose first entry is <= lastIndex
+    // MsgApps whose first entry is <= lastIndex: 1 + min(7, d / max_ents),
+    // by a 3-step binary search on the quotient (the multiples are uniform)
+    uint32_t fit = 1;
     if (x.me) {
-#pragma unroll
-      for (int j = 1; j < kRingChunk; j++)
-        fit += (static_cast<uint64_t>(j) * x.me <= d) ? 1u : 0u;
+      const uint64_t me = x.me;
+      uint32_t q = d >= 4 * me ? 4u : 0u;
+      q += d >= (q + 2) * me ? 2u : 0u;
+      q += d >= (q + 1) * me ? 1u : 0u;
+      fit += q;
     }
     added = x.me ? (lim < fit ? lim : fit) : (lim ? 1u : 0u);
     if (added) {
@@ -331,12 +335,69 @@ __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t 
 // its representation recomputed canonically from the live entries (the
 // upper words written only when the peer is wide).  A ring nothing appended
 // to keeps its representation: FreeLE and ResetState keep it valid.
+// Low words of a run's entries in 32-bit arithmetic: entry j is
+// b + min(d, (j+1)*me - 1) with d = lastIndex - b (run_val), so its low word
+// is lo(b) + lo(min) mod 2^32, and the min is the step for j < jcap =
+// min(8, floor(d / me)) (0 for noLimit: every entry is lastIndex), else d.
+struct RunLo {
+  uint32_t lob, lod, jcap;
+};
+__device__ __forceinline__ RunLo run_lo(const PRun &r, uint32_t me, uint64_t li) {
+  const uint64_t d = li - r.b;
+  uint32_t q = 0;
+  if (me) {  // wave-uniform
+    const uint64_t m = me;
+    q = d >= 4 * m ? 4u : 0u;
+    q += d >= (q + 2) * m ? 2u : 0u;
+    q += d >= (q + 1) * m ? 1u : 0u;
+    q = d >= 8 * m ? 8u : q;
+  }
+  return RunLo{static_cast<uint32_t>(r.b), static_cast<uint32_t>(d), q};
+}
+__device__ __forceinline__ uint32_t run_lo_at(const RunLo &L, uint32_t j, uint32_t me) {
+  return L.lob + (j < L.jcap ? (j + 1) * me - 1u : L.lod);
+}
+
 __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun &r1,
                                                const PRun &r2, bool touched, uint32_t rep_in,
-                                               uint32_t FP, uint32_t (&lo)[kRingChunk],
+                                               uint32_t c_old, uint32_t FP,
+                                               uint32_t (&lo)[kRingChunk],
                                                uint32_t (&hi)[kRingChunk]) {
   const bool any = (r1.n | r2.n) != 0;
   if (!__builtin_amdgcn_ballot_w64(touched && any)) return;  // the ring stands as loaded
+  const bool wl = touched && any;
+  {
+    // Common case: every appended entry and every old one share one upper
+    // word h <= QE_RING_EPOCH_MAX (runs are monotonic: their first and last
+    // entries decide), so the ring stays narrow and only low words change.
+    const uint32_t hb1 = static_cast<uint32_t>(r1.b >> 32), hb2 = static_cast<uint32_t>(r2.b >> 32);
+    const uint32_t h = r2.n ? hb2 : hb1;
+    const uint32_t hl1 =
+        static_cast<uint32_t>(run_val(r1, r1.n ? r1.n - 1 : 0, x.me, x.li) >> 32);
+    const uint32_t hl2 =
+        static_cast<uint32_t>(run_val(r2, r2.n ? r2.n - 1 : 0, x.me, x.li) >> 32);
+    const bool ok = h <= QE_RING_EPOCH_MAX && (r1.n == 0 || (hb1 == h && hl1 == h)) &&
+                    (r2.n == 0 || (hb2 == h && hl2 == h)) &&
+                    (c_old == 0 || (!rep_wide(rep_in) && rep_epoch(rep_in) == h));
+    if (!__builtin_amdgcn_ballot_w64(wl && !ok)) {
+      const RunLo L1 = run_lo(r1, x.me, x.li), L2 = run_lo(r2, x.me, x.li);
+#pragma unroll
+      for (int k = 0; k < kRingChunk; k++) {
+        if (static_cast<uint32_t>(k) >= x.F) break;
+        const uint32_t j1 = static_cast<uint32_t>(k) >= r1.p ? k - r1.p : k + x.F - r1.p;
+        const uint32_t j2 = static_cast<uint32_t>(k) >= r2.p ? k - r2.p : k + x.F - r2.p;
+        lo[k] = j2 < r2.n ? run_lo_at(L2, j2, x.me) : (j1 < r1.n ? run_lo_at(L1, j1, x.me) : lo[k]);
+      }
+      if (wl) p.rep = p.count ? QE_PW_EPOCH_BITS(h) : 0u;
+      if (__builtin_amdgcn_ballot_w64(wl)) {
+        bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, wl ? x.lb : kOOB);
+        if (FP > 4) bst128(u32x4{lo[4], lo[5], lo[6], lo[7]}, x.rlo, wl ? x.lb + 16 : kOOB);
+      }
+      return;
+    }
+  }
+  // General case (some lane's ring straddles upper words): every position's
+  // full value, the representation recomputed from the live entries.
   uint32_t h0 = 0;
   bool seen = false, uni = true;
   const uint32_t st = p.start;
@@ -359,7 +420,6 @@ __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun
     }
   }
   const bool wide = seen && (!uni || h0 > QE_RING_EPOCH_MAX);
-  const bool wl = touched && any;
   if (wl) p.rep = !seen ? 0u : (wide ? QE_PF_RING_WIDE : QE_PW_EPOCH_BITS(h0));
   if (__builtin_amdgcn_ballot_w64(wl)) {
     bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, wl ? x.lb : kOOB);
@@ -482,6 +542,10 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
   }
 }
+
+#ifndef QE_PSTEP_PROBE  // timing probes only (never the product build): bit 0 drops the
+#define QE_PSTEP_PROBE 0  // per-peer stores, bit 1 the ring loads, bit 2 the sends, bit 3
+#endif                    // the ring store, bit 4 the Progress stores, bit 5 the k1 burst
 
 #ifndef QE_PSTEP_WAVES
 #define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
@@ -686,7 +750,7 @@ k_progress_step(PArgs a) {
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
       if (row_ring) {
-        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi);
+        ring_load_row(x, touched && c_old > 0 && !(QE_PSTEP_PROBE & 2), rep0, a.FP, rlo, rhi);
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
@@ -738,7 +802,7 @@ k_progress_step(PArgs a) {
           }
         }
       }
-      if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
+      if (!(QE_PSTEP_PROBE & 36) && __builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
@@ -830,14 +894,17 @@ k_progress_step(PArgs a) {
       // later bcasts follow the loop.  Otherwise the message's sendAppend
       // and the later bcasts are consecutive sendIfEmpty sends: one burst.
       const uint32_t km = lp ? kLoop : k2 + k3;
+      if (!(QE_PSTEP_PROBE & 4)) {
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      if (row_ring) ring_store_row(p, x, r1, r2, touched, rep0, a.FP, rlo, rhi);
+      }
+      if (row_ring && !(QE_PSTEP_PROBE & 9)) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
-      const bool wm = touched && up, wn = touched && p.next != cur.nx;
-      const bool wp = touched && (p.pending != pd0 || p.reset);
-      const bool ww = touched && nw != cur.w;
+      const bool tw = touched && !(QE_PSTEP_PROBE & 17);
+      const bool wm = tw && up, wn = tw && p.next != cur.nx;
+      const bool wp = tw && (p.pending != pd0 || p.reset);
+      const bool ww = tw && nw != cur.w;
       // the ring representation bits are not Progress state (not counted)
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
       if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
