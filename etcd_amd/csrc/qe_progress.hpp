@@ -545,7 +545,8 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 
 #ifndef QE_PSTEP_PROBE  // timing probes only (never the product build): bit 0 drops the
 #define QE_PSTEP_PROBE 0  // per-peer stores, bit 1 the ring loads, bit 2 the sends, bit 3
-#endif                    // the ring store, bit 4 the Progress stores, bit 5 the k1 burst
+#endif                    // the ring store, bit 4 the Progress stores, bit 5 the k1 burst,
+                          // bit 6 the burst of the bcasts after an accept's send loop
 
 #ifndef QE_PSTEP_WAVES
 #define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
@@ -896,7 +897,7 @@ k_progress_step(PArgs a) {
       const uint32_t km = lp ? kLoop : k2 + k3;
       if (!(QE_PSTEP_PROBE & 4)) {
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
-      if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
+      if (!(QE_PSTEP_PROBE & 64) && __builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
       }
       if (row_ring && !(QE_PSTEP_PROBE & 9)) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
