@@ -906,13 +906,16 @@ k_progress_step(PArgs a) {
       const bool wm = tw && up, wn = tw && p.next != cur.nx;
       const bool wp = tw && (p.pending != pd0 || p.reset);
       const bool ww = tw && nw != cur.w;
+      // (storing a changed row for every touched lane, whole sectors, made
+      // no difference here: profiles/r03/cq_fullrow_ab.txt)
+      const bool fm = wm, fn = wn, fw = ww;
       // the ring representation bits are not Progress state (not counted)
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
-      if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), wm ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), fm ? o8 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), fn ? o8 : kOOB);
       if (__builtin_amdgcn_ballot_w64(wp))
         bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), ww ? lane * 4 : kOOB);
+      if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), fw ? lane * 4 : kOOB);
       if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
       if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
         bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
@@ -1136,10 +1139,13 @@ __device__ __forceinline__ void cq_finish(const PArgs &a, uint64_t t, uint32_t l
     const uint32_t nw =
         (x.w[s] & ~QE_PF_RECENT_ACTIVE) | (((selfb >> s) & 1u) ? QE_PF_RECENT_ACTIVE : 0u);
     const bool wr = ((trk >> s) & 1u) && nw != x.w[s];
-#ifdef QE_CQ_FULLROW  // A/B knob: a row some lane changes is stored for every tracked lane
-    const bool wf = (trk >> s) & 1u;
-#else
+    // a row some lane changes is stored for every tracked lane (unchanged
+    // words rewritten as loaded): whole 64-B sectors instead of the partial
+    // ones of changed words only, 0.137 -> 0.120 ms (profiles/r03/cq_fullrow_ab.txt)
+#ifdef QE_CQ_CHANGED_ONLY  // A/B knob: store only the changed words
     const bool wf = wr;
+#else
+    const bool wf = (trk >> s) & 1u;
 #endif
     if (__builtin_amdgcn_ballot_w64(wr))
       bst32(nw, mk_rsrc(a.pw + static_cast<uint64_t>(s) * a.stride + g0, n * 4),
