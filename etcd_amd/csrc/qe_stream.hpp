@@ -72,7 +72,7 @@ __device__ __forceinline__ uint32_t ld_mask_r(rsrc_t r, uint32_t lane) {
 
 template <int S, int MODE, typename MT, bool NTL>
 __device__ __forceinline__ void st_issue(const CVArgs &a, uint64_t t, uint32_t lane, uint32_t use,
-                                         uint64_t (&v)[S], STile &x) {
+                                         uint32_t top, uint64_t (&v)[S], STile &x) {
   const uint64_t tile0 = t * 64;
   const uint32_t n = tile_n(a.G, t);
   const uint32_t off = lane * 8;
@@ -80,6 +80,14 @@ __device__ __forceinline__ void st_issue(const CVArgs &a, uint64_t t, uint32_t l
   for (int s = 0; s < S; s++) {
     const rsrc_t r = mk_rsrc(a.match + s * a.stride + tile0, n * 8);
     const uint32_t o = MODE == 0 ? off : bit_off(use, s, off);
+#ifndef QE_STREAM_ALL_ROWS  // A/B knob: issue every slot row's load
+    // slots >= top (scalar) hold no voter of the chunk: no instruction at all
+    // (a fully dropped load still costs an issue slot of the memory path)
+    if (MODE != 0 && static_cast<uint32_t>(s) >= top) {
+      v[s] = 0;
+      continue;
+    }
+#endif
     v[s] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, NTL ? 2 : 0));
   }
   const MT *lp = static_cast<const MT *>(a.learner), *vp = static_cast<const MT *>(a.voted);
@@ -170,7 +178,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
         any |= mv[k];
       }
       // slots >= top hold no voter of any group in the chunk (wave-uniform)
-      top = 32u - __builtin_clz(wave_or((any | (any >> 16)) & 0xFFFFu) | 1u);
+      top = __builtin_amdgcn_readfirstlane(
+          32u - __builtin_clz(wave_or((any | (any >> 16)) & 0xFFFFu) | 1u));
     }
     auto use_of = [&](uint32_t k) -> uint32_t {
       if constexpr (MODE == 0) return 0u;
@@ -188,13 +197,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, kBlock),
     auto tix = [&](uint32_t k) -> uint64_t { return t0 + k < tend ? t0 + k : ntiles; };
     uint64_t va[S], vb[S];
     STile xa, xb;
-    st_issue<S, MODE, MT, NTL>(a, tix(0), lane, use_of(0), va, xa);
+    st_issue<S, MODE, MT, NTL>(a, tix(0), lane, use_of(0), top, va, xa);
     for (uint32_t k = 0; k < nt; k += 2) {
       // tile k from set A while tile k+1 streams into set B, then swap
-      st_issue<S, MODE, MT, NTL>(a, tix(k + 1), lane, use_of((k + 1) % TPW), vb, xb);
+      st_issue<S, MODE, MT, NTL>(a, tix(k + 1), lane, use_of((k + 1) % TPW), top, vb, xb);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compute
       st_finish<S, MODE, NTS>(a, tix(k), lane, want_stats, mio_of(k), top, va, xa, st);
-      st_issue<S, MODE, MT, NTL>(a, tix(k + 2), lane, use_of((k + 2) % TPW), va, xa);
+      st_issue<S, MODE, MT, NTL>(a, tix(k + 2), lane, use_of((k + 2) % TPW), top, va, xa);
       __builtin_amdgcn_sched_barrier(0);
       st_finish<S, MODE, NTS>(a, tix(k + 1), lane, want_stats, mio_of((k + 1) % TPW), top, vb,
                               xb, st);
