@@ -84,10 +84,23 @@ __global__ __launch_bounds__(1024) void k_collect_scan(const uint32_t *counts, u
                                                        uint64_t *offsets, uint64_t *out_count) {
   __shared__ uint64_t wtot[16];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint64_t per = (nb + 1023) / 1024;
+  // per: a multiple of 4, so a thread's range is 16-byte aligned and read
+  // as uint4 loads (the counts array starts 16-byte aligned: the scratch is
+  // 8-byte aligned and the counts follow nb u64 offsets -- see qe_collect)
+  const uint64_t per = ((nb + 1023) / 1024 + 3) & ~3ull;
   const uint64_t b0 = t * per < nb ? t * per : nb, b1 = b0 + per < nb ? b0 + per : nb;
+  const bool vec = (reinterpret_cast<uintptr_t>(counts) & 15u) == 0;
   uint64_t s = 0;
-  for (uint64_t b = b0; b < b1; b++) s += counts[b];
+  if (vec) {
+    uint64_t b = b0;
+    for (; b + 4 <= b1; b += 4) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(counts + b);
+      s += static_cast<uint64_t>(v.x) + v.y + v.z + v.w;
+    }
+    for (; b < b1; b++) s += counts[b];
+  } else {
+    for (uint64_t b = b0; b < b1; b++) s += counts[b];
+  }
   uint64_t inc = s;  // inclusive scan of the thread sums within the wave
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -103,7 +116,18 @@ __global__ __launch_bounds__(1024) void k_collect_scan(const uint32_t *counts, u
     all += wtot[k];
   }
   uint64_t run = before + inc - s;
-  for (uint64_t b = b0; b < b1; b++) {
+  uint64_t b = b0;
+  if (vec && (reinterpret_cast<uintptr_t>(offsets) & 15u) == 0) {
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    for (; b + 4 <= b1; b += 4) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(counts + b);
+      const uint64_t o1 = run + v.x, o2 = o1 + v.y, o3 = o2 + v.z;
+      *reinterpret_cast<u64x2 *>(offsets + b) = u64x2{run, o1};
+      *reinterpret_cast<u64x2 *>(offsets + b + 2) = u64x2{o2, o3};
+      run = o3 + v.w;
+    }
+  }
+  for (; b < b1; b++) {
     offsets[b] = run;
     run += counts[b];
   }
