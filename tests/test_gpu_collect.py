@@ -71,6 +71,22 @@ def test_collect_empty_and_no_values(eng):
     del C
 
 
+@pytest.mark.parametrize("G", [100, 4097, 3 * 4096 + 17])
+def test_collect_with_perm(eng, G):
+    """Packed batches (qe_pack_order): out_groups[i] = goff + perm[g] for the
+    i-th selected packed position g, values taken at g."""
+    rng = np.random.default_rng(G)
+    flags = (rng.random(G) < 0.4).astype(np.uint8)
+    values = rng.integers(0, 1 << 62, G, dtype=np.int64)
+    perm = rng.permutation(G).astype(np.int64)
+    groups, vals = eng.collect(torch.from_numpy(flags).to(DEV), torch.from_numpy(values).to(DEV),
+                               group_offset=77, perm=torch.from_numpy(perm).to(DEV))
+    torch.cuda.synchronize()
+    want = np.nonzero(flags)[0]
+    np.testing.assert_array_equal(groups.cpu().numpy(), perm[want] + 77)
+    np.testing.assert_array_equal(vals.cpu().numpy(), values[want])
+
+
 def test_collect_full_size(eng):
     """64M groups (config 2's batch) at half density, every entry compared."""
     G = 1 << 26
