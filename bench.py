@@ -96,6 +96,8 @@ def parse():
                     help="CPU baseline threads (0 = this process's CPU share: the affinity "
                          "set, capped by OMP_NUM_THREADS when the box sets it)")
     ap.add_argument("--cpu-groups", type=int, default=1 << 21)
+    ap.add_argument("--aux-groups-div", type=int, default=1,
+                    help="rehearsal only: divide every secondary workload's group count")
     return ap.parse_args()
 
 
@@ -493,6 +495,9 @@ def setup(name, G, S, kind, d, stats):
                                   max_ents=ME)
         msgs = engine.PeerMsgs(ps)
         msgs.snap = msgs.timeout_now = None  # no snapshots / transfers in this workload
+        # no ReadIndex in this workload (heartbeat rounds carry it); the
+        # round-3 output set, so the figures stay comparable
+        msgs.read_released = msgs.term_commit = msgs.term_commit_index = None
         progress_round_state(ps, msgs)
         # Every timed launch steps the SAME fresh state with the same round
         # of messages: the mutable state is restored from a pristine copy
@@ -726,6 +731,10 @@ def cpu_baseline(args, S=5):
         reps = max(1, int(10.0 / max(t1, 1e-6)))
         t = L.orc_gf_run(w, orc.P(commit), orc.P(vote), reps, threads)
         gf_rate = G * reps / t
+        # one thread, for the per-core rate and the scaling over the share
+        t1s = L.orc_gf_run(w, orc.P(commit), orc.P(vote), 1, 1)
+        reps1 = max(1, int(3.0 / max(t1s, 1e-6)))
+        gf_rate1 = G * reps1 / L.orc_gf_run(w, orc.P(commit), orc.P(vote), reps1, 1)
     finally:
         L.orc_gf_free(w)
     # the SoA restatement (strongest CPU variant)
@@ -747,6 +756,17 @@ def cpu_baseline(args, S=5):
                    f"{os.environ.get('OMP_NUM_THREADS', 'unset')}) of a {host_cpus}-CPU "
                    f"{cpu_model()} host"),
         "cpu_model": cpu_model(), "host_cpus": host_cpus,
+        "one_thread_value": gf_rate1,
+        "scaling_efficiency": gf_rate / (gf_rate1 * threads),
+        # the north star quotes the Go loop over the host's own cores; this
+        # box grants the process a CPU share (OMP_NUM_THREADS), so the whole
+        # host is not run here: the per-thread rate measured at the share,
+        # times every host CPU, is an upper bound (scaling is at most linear)
+        "full_host_value": gf_rate / threads * host_cpus,
+        "full_host_basis": (f"ESTIMATE, not measured: the {threads}-thread rate / {threads} x "
+                            f"{host_cpus} host CPUs (linear scaling, an upper bound; measured "
+                            f"scaling 1 -> {threads} threads: "
+                            f"{gf_rate / (gf_rate1 * threads):.2f} of linear)"),
         "soa_value": soa_rate,
         "soa_sample": f"{G} groups x {reps2} passes, SoA restatement (orc_soa_run), {threads} threads",
     }
@@ -810,6 +830,8 @@ def run_workload(name, args, d, steps, warmup):
     desc, G, S, kind = WORKLOADS[name]
     if args.groups and name == args.workload:
         G = args.groups
+    elif name != args.workload and args.aux_groups_div > 1:
+        G = max(1 << 16, G // args.aux_groups_div)
     stats = engine.stats_buffer(d.dev)
     step, bpu, units, unit_name, keep = setup(name, G, S, kind, d, stats)
     torch.cuda.synchronize(d.dev)
@@ -964,6 +986,11 @@ def main():
     if d.world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={d.world}", file=sys.stderr)
         sys.exit(2)
+    if d.world > 1:
+        # the host packer (config3_joint_packed) runs in every rank at once:
+        # each gets its share of this process's CPUs, not all of them
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", str(d.world)))
+        engine._lib.lib().qe_pack_threads(max(1, cpu_share() // max(1, local)))
     main_res = run_workload(args.workload, args, d, args.steps, args.warmup)
     aux = {}
     if not args.no_aux:

@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 4
+QE_ABI_VERSION = 5
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -106,6 +106,7 @@ class QeProgress(C.Structure):
         ("inc_mask", vp), ("out_mask", vp),
         ("tracked", vp), ("self_slot", vp), ("lead_transferee", vp), ("snap_index", vp),
         ("max_ents", u32), ("reserved2", u32),
+        ("read_acks", vp), ("read_head", vp), ("read_count", vp),  # ABI 5
     ]
 
 
@@ -113,7 +114,8 @@ class QePeerMsgs(C.Structure):
     _fields_ = [("type", vp), ("index", vp), ("reject_hint", vp), ("log_term", vp),
                 ("sent", vp), ("bcast", vp), ("snap", vp), ("timeout_now", vp),
                 ("msg_count", vp), ("msg_index", vp), ("bytes_requested", vp),
-                ("read_acks", vp), ("read_ctx", vp), ("read_ok", vp)]
+                ("read_ctx", vp), ("read_released", vp), ("term_commit", vp),  # ABI 5
+                ("term_commit_index", vp)]
 
 
 QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
@@ -128,6 +130,9 @@ def QE_RING_PITCH(F):
     return (int(F) + 3) & ~3
 QE_MSG_NONE, QE_MSG_APP_RESP, QE_MSG_APP_RESP_REJECT, QE_MSG_HEARTBEAT_RESP = 0, 1, 2, 3
 QE_MSG_SNAP_STATUS, QE_MSG_SNAP_STATUS_REJECT, QE_MSG_UNREACHABLE = 4, 5, 6
+QE_MSG_TRANSFER_LEADER = 7  # ABI 5
+QE_READ_QUEUE = 4           # ABI 5: ReadIndex requests pending per group
+QE_RI_NONE, QE_RI_RESPOND, QE_RI_POSTPONED, QE_RI_QUEUED, QE_RI_FULL = 0, 1, 2, 3, 4
 QE_MAX_INFLIGHT = 255
 QE_MAX_LOG_RUNS = 16
 
@@ -187,6 +192,7 @@ PROTOTYPES = {
     "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp]),
     "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
+    "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),

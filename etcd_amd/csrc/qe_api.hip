@@ -408,6 +408,9 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.self_slot = p->self_slot;
   a.transferee = p->lead_transferee;
   a.max_ents = p->max_ents;
+  a.read_acks = p->read_acks;
+  a.read_head = p->read_head;
+  a.read_count = p->read_count;
   return QE_OK;
 }
 
@@ -431,9 +434,12 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
   a.msg_count = m->msg_count;
   a.msg_index = m->msg_index;
   a.acct = m->bytes_requested;
-  a.read_acks = m->read_acks;
-  a.read_ctx = m->read_ctx;
-  a.read_ok = m->read_ok;
+  // ABI 5: the ReadIndex queue comes whole or not at all
+  if (p->read_acks && (!p->read_head || !p->read_count)) return QE_EINVAL;
+  a.read_ctx = p->read_acks ? m->read_ctx : nullptr;
+  a.read_released = m->read_released;
+  a.term_commit = m->term_commit;
+  a.term_commit_index = m->term_commit_index;
   a.stats = stats;
   const int kind = m->bytes_requested ? 2 : 0;
   return dispatch_progress(p->num_slots, a, kind, p->inc_mask != nullptr, p->out_mask != nullptr,
@@ -452,6 +458,39 @@ int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_em
   a.sent = sent;
   a.snap = snap;
   return dispatch_progress(p->num_slots, a, 1, false, false, static_cast<hipStream_t>(stream));
+}
+
+int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
+                  uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream) {
+  if (!p) return QE_EINVAL;
+  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
+    return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (p->stride < p->num_groups || !request || !result) return QE_EINVAL;
+  if (!p->committed || !p->term_start || !p->last_index) return QE_EINVAL;
+  if (p->out_mask && !p->inc_mask) return QE_EINVAL;
+  // ReadOnlySafe queues: the queue must be there
+  if (!lease_based && (!p->read_acks || !p->read_head || !p->read_count)) return QE_EINVAL;
+  PArgs a{};
+  a.G = p->num_groups;
+  a.goff = p->group_offset;
+  a.stride = p->stride;
+  a.committed = p->committed;
+  a.term_start = p->term_start;
+  a.last_index = p->last_index;
+  a.inc = p->inc_mask;
+  a.out = p->out_mask;
+  a.self_slot = p->self_slot;
+  a.read_acks = p->read_acks;
+  a.read_head = p->read_head;
+  a.read_count = p->read_count;
+  a.ri_request = request;
+  a.ri_result = result;
+  a.ri_ctx = ctx;
+  a.ri_index = index;
+  a.lease_based = lease_based ? 1u : 0u;
+  return dispatch_progress(p->num_slots, a, 4, p->inc_mask != nullptr, p->out_mask != nullptr,
+                           static_cast<hipStream_t>(stream));
 }
 
 int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stats,

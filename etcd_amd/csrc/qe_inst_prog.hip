@@ -18,18 +18,18 @@ using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
 #define QE_CAT2(a, b) a##b
 #define QE_CAT(a, b) QE_CAT2(a, b)
 
-template <int RM, bool ACCT, int WPB = kBlock / 64>
+template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64>
 static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
   // the same waves as the 4-wave grid, in blocks of WPB waves
   const uint64_t nb = static_cast<uint64_t>(grid_for((a.G + 63) / 64, 0, 1)) * ((kBlock / 64) / WPB);
   const dim3 grid(static_cast<unsigned>(nb < 0x7FFFFFFFull ? nb : 0x7FFFFFFFull));
   const dim3 blk(64 * WPB);
   if (joint)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
   else if (masked)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -71,27 +71,44 @@ static int launch_check_quorum(PArgs a, bool masked, bool joint, hipStream_t st)
   return hip_status(hipGetLastError());
 }
 
+template <bool RD>
+static int step_runs(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  if (a.R <= 4) return launch_progress_step<4, false, RD>(a, masked, joint, st);
+#ifndef QE_NO_RM8  // A/B knob: without the 8-run kernel
+  if (a.R <= 8) return launch_progress_step<8, false, RD>(a, masked, joint, st);
+#endif
+#ifdef QE_RM16_WPB  // A/B knob: waves per block of the 16-run kernel
+  return launch_progress_step<QE_MAX_LOG_RUNS, false, RD, QE_RM16_WPB>(a, masked, joint, st);
+#else
+  return launch_progress_step<QE_MAX_LOG_RUNS, false, RD, 1>(a, masked, joint, st);
+#endif
+}
+
+static int launch_read_index(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  if (joint) hipLaunchKernelGGL((k_read_index<S, MT, true, true>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_read_index<S, MT, true, false>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_read_index<S, MT, false, false>), grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 // kind 0: qe_progress_step, 1: qe_progress_send, 2: qe_progress_step with
 // byte accounting (instrumented variant, measurement only), 3:
-// qe_check_quorum
+// qe_check_quorum, 4: qe_read_index
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
   if (kind == 1) return launch_progress_send(a, st);
   if (kind == 3) return launch_check_quorum(a, masked, joint, st);
+  if (kind == 4) return launch_read_index(a, masked, joint, st);
   // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
   // or two older terms before the current one); 8 keep the block's LDS at
   // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);
   // up to QE_MAX_LOG_RUNS otherwise
-  if (kind == 2) return launch_progress_step<QE_MAX_LOG_RUNS, true>(a, masked, joint, st);
-  if (a.R <= 4) return launch_progress_step<4, false>(a, masked, joint, st);
-#ifndef QE_NO_RM8  // A/B knob: without the 8-run kernel
-  if (a.R <= 8) return launch_progress_step<8, false>(a, masked, joint, st);
-#endif
-#ifdef QE_RM16_WPB  // A/B knob: waves per block of the 16-run kernel
-  return launch_progress_step<QE_MAX_LOG_RUNS, false, QE_RM16_WPB>(a, masked, joint, st);
-#else
-  return launch_progress_step<QE_MAX_LOG_RUNS, false, 1>(a, masked, joint, st);
-#endif
+  // ReadIndex tracking (a.read_acks) takes a variant of its own: its queue
+  // state costs registers the rounds without reads should not pay
+  if (kind == 2) return launch_progress_step<QE_MAX_LOG_RUNS, true, true>(a, masked, joint, st);
+  if (a.read_acks) return step_runs<true>(a, masked, joint, st);
+  return step_runs<false>(a, masked, joint, st);
 }
 
 }  // namespace qe

@@ -6,6 +6,18 @@
 // A wave iterates over tiles of 64*PAIRS pairs; the grid is persistent
 // (a few workgroups per CU) and strides over tiles.  See DESIGN.md §2-§3.
 #pragma once
+// A/B knobs are for variant libraries built by
+// scripts/build_variant*.sh, which define QE_VARIANT_BUILD.  QE_PSTEP_PROBE
+// drops work (results change); the others only change code paths or launch
+// shapes.  A product build with any of them set is refused, so a stray -D can
+// never ship a library that computes something else.
+#if !defined(QE_VARIANT_BUILD) &&                                                  \
+    (defined(QE_PSTEP_PROBE) || defined(QE_CQ_CHANGED_ONLY) ||                     \
+     defined(QE_STREAM_ALL_ROWS) || defined(QE_NO_RM8) || defined(QE_RM16_WPB) ||  \
+     defined(QE_PSTEP_WAVES) || defined(QE_STREAM_TPW) || defined(QE_STREAM_WAVES) || \
+     defined(QE_JOINT_MIN_WAVES))
+#error "A/B knob set in a product build: use scripts/build_variant*.sh (QE_VARIANT_BUILD)"
+#endif
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -689,18 +701,29 @@ struct PArgs {
   const uint64_t *run_first, *run_term;
   const uint8_t *run_count;
   const void *inc, *out, *tracked;
-  const uint8_t *self_slot, *transferee;
+  const uint8_t *self_slot;
+  uint8_t *transferee;  // rw (ABI 5: MsgTransferLeader)
   uint32_t max_ents;
+  // ReadIndex queue (ABI 5): acks [G][QE_READ_QUEUE] mask-typed, head, count
+  void *read_acks;
+  uint32_t *read_head;
+  uint8_t *read_count;
   // step messages and outputs
   const uint8_t *mtype;
   const uint64_t *mindex, *mhint, *mlogterm;
   void *sent, *snap, *tnow;
   uint8_t *bcast, *msg_count;
   uint64_t *msg_index, *acct;
-  void *read_acks;
-  const void *read_ctx;
-  uint8_t *read_ok;
+  const uint32_t *read_ctx;
+  uint8_t *read_released, *term_commit;
+  uint64_t *term_commit_index;
   uint64_t *stats;
+  // read index (qe_read_index)
+  const uint8_t *ri_request;
+  uint8_t *ri_result;
+  uint32_t *ri_ctx;
+  uint64_t *ri_index;
+  uint32_t lease_based;
   // send
   const void *want;
   uint32_t send_if_empty;

@@ -104,7 +104,9 @@ __device__ __forceinline__ void acct_flush(const Acct<ACCT> &ac, uint64_t *acct)
 // Checksum of the round: a per-group part from the commit pass and a
 // per-group part from the peer pass (oracle/quorum_oracle.c orc_checksum_step).
 constexpr uint64_t kSentSalt = 0xD1B54A32D192ED03ull;
-constexpr uint64_t kReadSalt = 0x8CB92BA72F3D8DD7ull;   // a released ReadIndex request
+constexpr uint64_t kReadSalt = 0x8CB92BA72F3D8DD7ull;   // released ReadIndex requests
+constexpr uint64_t kTermSalt = 0x589965CC75374CC3ull;   // first commit in the leader's term
+constexpr uint64_t kTransferSalt = 0x1D8E4E27C47D124Full; // lead_transferee changed
 constexpr uint64_t kQuorumSalt = 0xA0761D6478BD642Full; // CheckQuorum: quorum active
 
 // ---------------------------------------------------------------------------
@@ -516,18 +518,20 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint32_t (&lo)[kRingChun
 struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's turn)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
+  uint32_t rc;                  // the context number a MsgHeartbeatResp carries
 };
 
 // Loads of slot row `row` (= s*stride + tile0): Next and the packed word of
 // a peer that may be touched (`ld`, a superset of the lanes the round
-// touches) and RejectHint/LogTerm of a reject.  The byte accounting is done
+// touches), RejectHint/LogTerm of a reject and the context number of a
+// heartbeat response (`rcl`).  The byte accounting is done
 // by the caller, on the lanes the round actually touches.
 // A wave-level branch skips each group of loads no lane needs (an issued
 // vector memory instruction costs the CU's memory path about the same
 // whether or not its lanes are masked off).
 __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *l_mix,
                                         uint32_t n, uint32_t lane, bool ld, bool rej,
-                                        bool has_ix, PB &b) {
+                                        bool has_ix, bool rcl, PB &b) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
   b.nx = 0;
@@ -541,6 +545,8 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
   }
+  b.rc = 0;
+  if (__builtin_amdgcn_ballot_w64(rcl)) b.rc = bld32(mk_rsrc(a.read_ctx + row, n * 4), rcl ? lane * 4 : kOOB);
 }
 
 #ifndef QE_PSTEP_PROBE  // timing probes only (never the product build): bit 0 drops the
@@ -554,12 +560,18 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 
 // WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
 // (21 KB at S = 5) would allow one 4-wave block per CU
-template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, int WPB = kBlock / 64>
+template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, bool RD,
+          int WPB = kBlock / 64>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
                           amdgpu_waves_per_eu(S <= 6 ? QE_PSTEP_WAVES : 1))) void
 k_progress_step(PArgs a) {
   constexpr int CH = kRingChunk;
   constexpr uint32_t kFull = (1u << S) - 1u;
+  // the ReadIndex queue's acks, one word per group: entry j in bits
+  // [EW*j, EW*j + EW) (QE_READ_QUEUE entries of the mask type)
+  using QT = typename std::conditional<sizeof(MT) == 1, uint32_t, uint64_t>::type;
+  constexpr uint32_t EW = 8 * sizeof(MT);
+  constexpr uint32_t kRQ = QE_READ_QUEUE;
   uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
   Acct<ACCT> ac;
   const uint32_t lane = threadIdx.x & 63;
@@ -595,29 +607,40 @@ k_progress_step(PArgs a) {
                                            n * sizeof(MT)), lane) & kFull)
                   : kFull;
     const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
-    const uint32_t ltr = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), lane) : 0xFFu;
+    const uint32_t ltr0 = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), lane) : 0xFFu;
+    uint32_t ltr = ltr0;  // r.leadTransferee (MsgTransferLeader rewrites it)
     const uint64_t li = bld64(mk_rsrc(a.last_index + g0, n * 8), o8);
     const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), o8);
     const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), o8);
     const rsrc_t r_commit = mk_rsrc(a.committed + g0, n * 8);
     const uint64_t c0 = bld64(r_commit, o8);
     const uint64_t snap_ld = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), o8) : 0;
-    // ReadIndex (ABI 3): the pending request's acks and the slots whose
-    // heartbeat response carries its context
-    const bool rd = a.read_acks != nullptr;  // wave-uniform
-    const uint32_t acks0 =
-        rd ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.read_acks) + g0, n * sizeof(MT)),
-                            lane) & kFull)
-           : 0u;
-    const uint32_t rctx =
-        (rd && a.read_ctx)
-            ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.read_ctx) + g0, n * sizeof(MT)),
-                             lane) & kFull)
-            : kFull;
+    // ReadIndex queue (ABI 5): entry 0's context number, the pending count
+    // (clamped: a count above QE_READ_QUEUE is invalid input) and every
+    // entry's acks in one word
+    const bool rd = RD && a.read_acks != nullptr;  // RD: the variant that tracks ReadIndex
+    uint32_t qh = 0, qn = 0;
+    QT q0 = 0;
+    if (rd) {
+      qn = bld8(mk_rsrc(a.read_count + g0, n), lane);
+      qn = qn < kRQ ? qn : kRQ;
+      qh = bld32(mk_rsrc(a.read_head + g0, n * 4), o8 >> 1);
+      if constexpr (sizeof(QT) == 4)
+        q0 = bld32(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 4), o8 >> 1);
+      else
+        q0 = bld64(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 8), o8);
+    }
+    // the context of a response when read_ctx is NULL: the newest request
+    // pending when the round starts (lastPendingRequestCtx)
+    const uint32_t dctx = qn ? qh + qn - 1u : 0u;
+    const uint32_t qn0 = qn;
+    QT q = q0;
+    bool qtouch = false;
+    uint32_t nrel = 0;
     ac.add(live, (MASKED ? sizeof(MT) : 0) + (JOINT ? sizeof(MT) : 0) +
                      (a.tracked ? sizeof(MT) : 0) + (a.self_slot ? 1 : 0) +
-                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0) +
-                     (rd ? sizeof(MT) : 0) + ((rd && a.read_ctx) ? sizeof(MT) : 0));
+                     (a.transferee ? 1 : 0) + 32 + (a.snap_index ? 8 : 0) + (rd ? 5 : 0) +
+                     ((rd && qn0) ? sizeof(QT) : 0));
     uint64_t m0[S];
     uint32_t ty[S];
 #pragma unroll
@@ -638,13 +661,15 @@ k_progress_step(PArgs a) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint32_t t = ty[s];
-      tys |= static_cast<uint64_t>(t <= QE_MSG_UNREACHABLE ? t : 15u) << (4 * s);
-      msgm |= (t - 1u <= QE_MSG_UNREACHABLE - 1u ? 1u : 0u) << s;
+      tys |= static_cast<uint64_t>(t <= QE_MSG_TRANSFER_LEADER ? t : 15u) << (4 * s);
+      msgm |= (t - 1u <= QE_MSG_TRANSFER_LEADER - 1u ? 1u : 0u) << s;
       rejm |= (t == QE_MSG_APP_RESP_REJECT ? 1u : 0u) << s;
       appm |= (t == QE_MSG_APP_RESP ? 1u : 0u) << s;
       hbm |= (t == QE_MSG_HEARTBEAT_RESP ? 1u : 0u) << s;
     }
     const uint32_t ixm = appm | rejm;  // slots whose message carries m.Index
+    // heartbeat responses whose context number is loaded
+    const uint32_t rcm = (rd && a.read_ctx) ? (hbm & trk) : 0u;
     // ---- round trip 2: m.Index of every MsgAppResp and slot 0's peer loads ----
     uint64_t ix[S];
 #pragma unroll
@@ -661,10 +686,12 @@ k_progress_step(PArgs a) {
     PB cur;
     {  // slot 0, before phase 1: every possible event
       const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
-      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0, cur);
+      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
+              (rcm & 1u) != 0, cur);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
+    uint64_t cfirst = 0;  // the commit after the round's first advance
     uint32_t bset = 0, upd = 0;
     {
       uint64_t vals[S];
@@ -677,6 +704,7 @@ k_progress_step(PArgs a) {
           upd |= 1u << s;
           const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
           if (mci > c && mci >= ts && mci <= li) {
+            cfirst = bset ? cfirst : mci;
             c = mci;
             bset |= 1u << s;
           }
@@ -693,8 +721,6 @@ k_progress_step(PArgs a) {
     x.lb = lane * a.FP * 4;
     x.row = row_ring;
     uint32_t sent = 0, snapm = 0, tnow = 0;
-    uint32_t acks = acks0;
-    bool released = false;
     // touched: a tracked peer with a message, or a bcast target (every
     // tracked slot but the leader's when some accept advanced the commit);
     // ringm: FreeLE may run for this peer
@@ -711,7 +737,8 @@ k_progress_step(PArgs a) {
       PB nxt;
       if (s + 1 < static_cast<uint32_t>(S))
         pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
-                ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0, nxt);
+                ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
+                ((rcm >> (s + 1)) & 1u) != 0, nxt);
       if (!__builtin_amdgcn_ballot_w64(touched)) {
         // no event for this slot in any group of the tile (e.g. the leader's
         // own slot): only the per-peer output
@@ -722,6 +749,7 @@ k_progress_step(PArgs a) {
       }
       ac.add(touched, 12);  // Next + the packed word
       ac.add(touched && tt == QE_MSG_APP_RESP_REJECT, 16);  // RejectHint + LogTerm
+      ac.add(touched && ((rcm >> s) & 1u), 4);               // the heartbeat's context
       PR p;
       p.match = cur.mt;
       p.next = cur.nx;
@@ -874,12 +902,25 @@ k_progress_step(PArgs a) {
             free_le<ACCT>(p, first, c_old, fo, r1, x, ac);
           }
           k2 = p.match < li ? 1u : 0u;
-          // ReadOnlySafe (raft.go:1296-1309): recvAck, then the request is
-          // released (readOnly.advance) once the acks win the vote; a later
-          // response of the round finds it gone (recvAck returns nil)
-          if (rd && !released && ((rctx >> s) & 1u)) {
-            acks |= 1u << s;
-            released = joint_vote(mi, mo, acks, acks) == kVoteWon;
+          // ReadOnlySafe (raft.go:1296-1309): recvAck on the pending request
+          // with the response's context (none pending: recvAck returns nil,
+          // nothing recorded); once its acks win the vote, readOnly.advance
+          // dequeues every request through it (read_only.go:81-112)
+          if (rd) {
+            const uint32_t cx = a.read_ctx ? cur.rc : dctx;
+            const uint32_t j = cx - qh;
+            if (cx != 0 && j < qn) {
+              q |= static_cast<QT>(1u << s) << (EW * j);
+              qtouch = true;
+              const uint32_t e = static_cast<uint32_t>(q >> (EW * j)) & kFull;
+              if (joint_vote(mi, mo, e, e) == kVoteWon) {
+                const uint32_t r = j + 1;
+                q = r >= kRQ ? static_cast<QT>(0) : static_cast<QT>(q >> (EW * r));
+                qh += r;
+                qn -= r;
+                nrel += r;
+              }
+            }
           }
         } else if (tt == QE_MSG_SNAP_STATUS || tt == QE_MSG_SNAP_STATUS_REJECT) {  // :1310-1331
           if (p.state == QE_PR_SNAPSHOT) {
@@ -889,6 +930,20 @@ k_progress_step(PArgs a) {
           }
         } else if (tt == QE_MSG_UNREACHABLE) {  // :1332-1338
           if (p.state == QE_PR_REPLICATE) pr_become_probe(p);
+        } else if (tt == QE_MSG_TRANSFER_LEADER) {  // :1339-1370
+          if ((((mi | mo) >> s) & 1u) != 0) {  // a learner's request is ignored (:1340-1343)
+            bool go = true;
+            if (ltr < static_cast<uint32_t>(S)) {  // a transfer is in progress
+              if (ltr == s) go = false;  // to the same node: ignored (:1347-1350)
+              else ltr = 0xFFu;          // abortLeaderTransfer (:1352)
+            }
+            if (s == self) go = false;  // to the leader itself: ignored (:1355-1358)
+            if (go) {
+              ltr = s;
+              if (p.match == li) tnow |= 1u << s;  // sendTimeoutNow (:1364-1366)
+              else k2 = 1;                         // sendAppend (:1368)
+            }
+          }
         }
       }
       // After an accept: its sendAppend (sendIfEmpty), then the loop; the
@@ -937,13 +992,36 @@ k_progress_step(PArgs a) {
     if (a.tnow) bst_mask<MT>(tnow, opt_rsrc(static_cast<const MT *>(a.tnow), g0, n), lane);
     if (a.bcast) bst8(bc, opt_rsrc(static_cast<const uint8_t *>(a.bcast), g0, n), lane);
     if (rd) {
-      const bool wa = acks != acks0;
-      if (__builtin_amdgcn_ballot_w64(wa))
-        bst_mask<MT>(acks, mk_rsrc(static_cast<MT *>(a.read_acks) + g0, n * sizeof(MT)), lane, wa);
-      ac.add(live && wa, sizeof(MT));
+      // the queue word in canonical form (entries past the count 0), stored
+      // when a response was recorded on it and it changed; head and count
+      // when requests were released
+      const QT canon = qn >= kRQ ? q : static_cast<QT>(q & ((static_cast<QT>(1) << (EW * qn)) - 1u));
+      const bool wq = qtouch && canon != q0, wr = nrel != 0;
+      if (__builtin_amdgcn_ballot_w64(wq)) {
+        if constexpr (sizeof(QT) == 4)
+          bst32(canon, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 4), wq ? o8 >> 1 : kOOB);
+        else
+          bst64(canon, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 8), wq ? o8 : kOOB);
+      }
+      if (__builtin_amdgcn_ballot_w64(wr)) {
+        bst32(qh, mk_rsrc(a.read_head + g0, n * 4), wr ? o8 >> 1 : kOOB);
+        bst8(qn, mk_rsrc(a.read_count + g0, n), wr ? lane : kOOB);
+      }
+      ac.add(wq, sizeof(QT));
+      ac.add(wr, 5);
     }
-    if (a.read_ok) bst8(released ? 1u : 0u, opt_rsrc(a.read_ok, g0, n), lane);
-    ac.add(live && a.read_ok, 1);
+    if (a.read_released) bst8(nrel, opt_rsrc(a.read_released, g0, n), lane);
+    ac.add(live && a.read_released, 1);
+    // committedEntryInCurrentTerm became true: the postponed reads go out
+    const bool tc = c != c0 && !(c0 >= ts && c0 <= li);
+    if (a.term_commit) bst8(tc ? 1u : 0u, opt_rsrc(a.term_commit, g0, n), lane);
+    if (a.term_commit_index && __builtin_amdgcn_ballot_w64(tc))
+      bst64(cfirst, mk_rsrc(a.term_commit_index + g0, n * 8), tc ? o8 : kOOB);
+    ac.add(live && a.term_commit, 1);
+    ac.add(tc && a.term_commit_index, 8);
+    const bool wt = a.transferee && ltr != ltr0;
+    if (__builtin_amdgcn_ballot_w64(wt)) bst8(ltr, mk_rsrc(a.transferee + g0, n), wt ? lane : kOOB);
+    ac.add(wt, 1);
     ac.add(live && c != c0, 8);
     ac.add(live && a.sent, sizeof(MT));
     ac.add(live && a.snap, sizeof(MT));
@@ -954,10 +1032,12 @@ k_progress_step(PArgs a) {
       cnt[P_GROUPS] += 1;
       cnt[P_SUM] += c;
       cnt[P_ADV] += (c != c0);
-      cnt[P_READ] += released ? 1u : 0u;
+      cnt[P_READ] += nrel;
       cnt[P_CSUM] += mix64(gh ^ c ^ (static_cast<uint64_t>(bc) << 62)) +
                      mix64(gh ^ (static_cast<uint64_t>(sent) << 40) ^ kSentSalt) +
-                     (released ? mix64(gh ^ kReadSalt) : 0ull);
+                     (nrel ? mix64(gh ^ kReadSalt ^ (static_cast<uint64_t>(nrel) << 56)) : 0ull) +
+                     (tc ? mix64(gh ^ kTermSalt ^ cfirst) : 0ull) +
+                     (ltr != ltr0 ? mix64(gh ^ kTransferSalt ^ ltr) : 0ull);
     }
   }
   if (a.stats) {
@@ -1218,6 +1298,86 @@ __global__ __launch_bounds__(kBlock) void k_check_quorum(PArgs a) {
   if (a.stats) {
     const int idx[3] = {QE_STAT_GROUPS, QE_STAT_STEPDOWNS, QE_STAT_CHECKSUM};
     block_stats_add<3, kBlock>(cnt, idx, a.stats);
+  }
+}
+
+// qe_read_index: MsgReadIndex on the leader (stepLeader, raft/raft.go:
+// 1078-1096; sendMsgReadIndexResponse :1827-1843).  One lane per group, a
+// wave per 64-group tile; the queue word of a group that queues is rewritten
+// whole (entry `count` = the leader's own ack).
+template <int S, typename MT, bool MASKED, bool JOINT>
+__global__ __launch_bounds__(kBlock) void k_read_index(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  using QT = typename std::conditional<sizeof(MT) == 1, uint32_t, uint64_t>::type;
+  constexpr uint32_t EW = 8 * sizeof(MT);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = t * 64;
+    const uint32_t n = tile_n(a.G, t);
+    const uint32_t o8 = lane * 8, o4 = lane * 4;
+    const bool req = bld8(mk_rsrc(a.ri_request + g0, n), lane) != 0;
+    uint32_t res = QE_RI_NONE, ctx = 0;
+    uint64_t c = 0;
+    if (__builtin_amdgcn_ballot_w64(req)) {
+      const uint32_t mi =
+          MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * sizeof(MT)), lane) &
+                    kFull)
+                 : kFull;
+      const uint32_t mo =
+          JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * sizeof(MT)), lane) &
+                   kFull)
+                : 0u;
+      const uint32_t ro = req ? o8 : kOOB;
+      c = bld64(mk_rsrc(a.committed + g0, n * 8), ro);
+      const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), ro);
+      const uint64_t li = bld64(mk_rsrc(a.last_index + g0, n * 8), ro);
+      const bool single = popc(mi) == 1 && mo == 0;  // ProgressTracker.IsSingleton
+      const bool in_term = c >= ts && c <= li;       // committedEntryInCurrentTerm
+      res = single ? QE_RI_RESPOND
+                   : (!in_term ? QE_RI_POSTPONED : (a.lease_based ? QE_RI_RESPOND : QE_RI_QUEUED));
+      res = req ? res : QE_RI_NONE;
+      const bool qd = res == QE_RI_QUEUED;  // ReadOnlySafe: addRequest + recvAck(r.id)
+      if (__builtin_amdgcn_ballot_w64(qd)) {
+        const uint32_t qo = qd ? o4 : kOOB;
+        uint32_t qn = bld8(mk_rsrc(a.read_count + g0, n), qd ? lane : kOOB);
+        uint32_t qh = bld32(mk_rsrc(a.read_head + g0, n * 4), qo);
+        QT q;
+        if constexpr (sizeof(QT) == 4)
+          q = bld32(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 4), qo);
+        else
+          q = bld64(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 8), qd ? o8 : kOOB);
+        // an empty queue starts over at context 1 when its head is 0 (a
+        // fresh state, or numbers that wrapped exactly)
+        if (qn == 0 && qh == 0) qh = 1;
+        const bool full = qn >= QE_READ_QUEUE || qh + qn == 0u;
+        res = (qd && full) ? QE_RI_FULL : res;
+        const bool add = qd && !full;
+        const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), add ? lane : kOOB) : 0xFFu;
+        const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
+        ctx = qh + qn;
+        // entries past the count are dead: the word is rewritten canonical
+        const QT live = qn >= QE_READ_QUEUE ? q : static_cast<QT>(q & ((static_cast<QT>(1) << (EW * qn)) - 1u));
+        const QT nq = static_cast<QT>(live | (static_cast<QT>(selfb) << (EW * (qn < QE_READ_QUEUE ? qn : 0u))));
+        if (__builtin_amdgcn_ballot_w64(add)) {
+          if constexpr (sizeof(QT) == 4)
+            bst32(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 4), add ? o4 : kOOB);
+          else
+            bst64(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 8), add ? o8 : kOOB);
+          bst32(qh, mk_rsrc(a.read_head + g0, n * 4), add ? o4 : kOOB);
+          bst8(qn + 1, mk_rsrc(a.read_count + g0, n), add ? lane : kOOB);
+        }
+      }
+    }
+    bst8(res, mk_rsrc(a.ri_result + g0, n), lane);
+    if (a.ri_ctx && __builtin_amdgcn_ballot_w64(res == QE_RI_QUEUED))
+      bst32(ctx, mk_rsrc(a.ri_ctx + g0, n * 4), res == QE_RI_QUEUED ? o4 : kOOB);
+    const bool wi = res == QE_RI_RESPOND || res == QE_RI_QUEUED;
+    if (a.ri_index && __builtin_amdgcn_ballot_w64(wi))
+      bst64(c, mk_rsrc(a.ri_index + g0, n * 8), wi ? o8 : kOOB);
   }
 }
 

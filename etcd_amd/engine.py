@@ -302,7 +302,9 @@ class ProgressState:
     upper words come from the peer word's epoch unless QE_PF_RING_WIDE),
     committed, and the leader-log model (term runs).  `extras`
     allocates the optional per-group arrays: "tracked" (slot mask),
-    "self_slot", "lead_transferee" (u8, 0xFF = none), "snap_index" (u64)."""
+    "self_slot", "lead_transferee" (u8, 0xFF = none), "snap_index" (u64),
+    "reads" (ABI 5: the ReadIndex queue -- read_acks [G][QE_READ_QUEUE]
+    mask-typed, read_head u32 (starting at context 1), read_count u8)."""
 
     def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None,
                  extras=(), max_ents=0):
@@ -341,6 +343,13 @@ class ProgressState:
                                 if "lead_transferee" in extras else None)
         self.snap_index = (torch.zeros(self.G, dtype=i64, device=dev)
                            if "snap_index" in extras else None)
+        rq = _lib.QE_READ_QUEUE
+        self.read_acks = (torch.zeros(self.G * rq, dtype=md, device=dev)
+                          if "reads" in extras else None)
+        self.read_head = (torch.ones(self.G, dtype=torch.int32, device=dev)
+                          if "reads" in extras else None)
+        self.read_count = (torch.zeros(self.G, dtype=u8, device=dev)
+                           if "reads" in extras else None)
 
     def struct(self):
         return _lib.QeProgress(
@@ -350,11 +359,13 @@ class ProgressState:
             _ptr(self.first_index), _ptr(self.last_index), self.R, 0, _ptr(self.run_first),
             _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
             _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
-            _ptr(self.snap_index), self.max_ents, 0)
+            _ptr(self.snap_index), self.max_ents, 0, _ptr(self.read_acks), _ptr(self.read_head),
+            _ptr(self.read_count))
 
     ARRAYS = ("match", "next", "pending", "peer", "ilo", "ihi", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
-              "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
+              "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index",
+              "read_acks", "read_head", "read_count")
 
     def load_host(self, **arrays):
         """numpy arrays (uint64 as uint64, masks as uint8/uint16, peer words
@@ -362,9 +373,14 @@ class ProgressState:
         packed into the peer words (absent fields 0).  `ibuf` takes plain
         uint64 Inflights rings, entry-major [S][F][stride] (the oracle's
         layout), converted through qe_ring_pack after the peer words are in
-        place (their ring representation bits are recomputed)."""
+        place (their ring representation bits are recomputed).  Without
+        `ibuf`, rewritten peer words keep describing the resident rings: the
+        rings are decoded with the old words and packed again with the new
+        ones (a new Inflights.start / count selects other live entries)."""
         ibuf = arrays.pop("ibuf", None)
         fields = {k: arrays.pop(k) for k in ("flags", "istart", "icount") if k in arrays}
+        if ibuf is None and (fields or "peer" in arrays):
+            ibuf = self.rings()  # decoded with the words in place now
         if fields:
             n = max(np.asarray(v).size for v in fields.values())
             z = np.zeros(n, np.uint32)
@@ -481,24 +497,27 @@ class PeerMsgs:
         self.msg_count = torch.zeros(n, dtype=torch.uint8, device=dev) if outputs else None
         self.msg_index = torch.zeros(n, dtype=torch.int64, device=dev) if outputs else None
         self.bytes_requested = None
-        # ReadIndex (ABI 3): None unless the caller tracks a pending request
-        self.read_acks = None   # [G] mask-typed, rw
-        self.read_ctx = None    # [G] mask-typed
-        self.read_ok = None     # [G] uint8 out
+        # ReadIndex (ABI 5): contexts carried by heartbeat responses (None =
+        # the newest pending at the start of the round) and the outputs
+        self.read_ctx = None       # [S][stride] uint32 (int32 storage)
+        self.read_released = torch.zeros(ps.G, dtype=torch.uint8, device=dev) if outputs else None
+        self.term_commit = torch.zeros(ps.G, dtype=torch.uint8, device=dev) if outputs else None
+        self.term_commit_index = (torch.zeros(ps.G, dtype=torch.int64, device=dev)
+                                  if outputs else None)
 
-    def track_reads(self, ps, acks, ctx=None):
-        """Attach ReadIndex state: acks / ctx are [G] mask tensors (or numpy
-        arrays); read_ok is allocated."""
-        md = mask_torch_dtype(ps.S)
-
-        def dev(x):
-            if x is None or torch.is_tensor(x):
-                return x
-            a = np.ascontiguousarray(x)
-            return torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).to(ps.device)
-        self.read_acks = dev(acks).to(md)
-        self.read_ctx = dev(ctx).to(md) if ctx is not None else None
-        self.read_ok = torch.zeros(ps.G, dtype=torch.uint8, device=ps.device)
+    def set_read_ctx(self, ps, ctx):
+        """Context numbers of the heartbeat responses: uint32 [S][stride]
+        (numpy or tensor); None = every response carries the newest context
+        pending when the round starts."""
+        if ctx is None:
+            self.read_ctx = None
+            return self
+        if not torch.is_tensor(ctx):
+            a = np.ascontiguousarray(np.asarray(ctx, np.uint32)).view(np.int32)
+            ctx = torch.from_numpy(a.copy())
+        t = torch.zeros(ps.S * ps.stride, dtype=torch.int32, device=ps.device)
+        t[: ctx.numel()].copy_(ctx.reshape(-1).to(torch.int32))
+        self.read_ctx = t
         return self
 
     def struct(self):
@@ -506,7 +525,8 @@ class PeerMsgs:
                                _ptr(self.log_term), _ptr(self.sent), _ptr(self.bcast),
                                _ptr(self.snap), _ptr(self.timeout_now), _ptr(self.msg_count),
                                _ptr(self.msg_index), _ptr(self.bytes_requested),
-                               _ptr(self.read_acks), _ptr(self.read_ctx), _ptr(self.read_ok))
+                               _ptr(self.read_ctx), _ptr(self.read_released),
+                               _ptr(self.term_commit), _ptr(self.term_commit_index))
 
 
 def progress_step(ps, msgs, stats=None):
@@ -537,6 +557,22 @@ def progress_send(ps, want, send_if_empty=False):
         C.byref(p), _ptr(want), int(bool(send_if_empty)), _ptr(sent), _ptr(snap),
         _stream(ps.device)))
     return sent, snap
+
+
+def read_index(ps, request, lease_based=False):
+    """qe_read_index: MsgReadIndex on the leader of every group with
+    request[g] != 0 (raft/raft.go:1078-1096) -> (result uint8[G] QE_RI_*,
+    ctx int32[G] (the context number of a QUEUED request), index int64[G]
+    (the read index of RESPOND / QUEUED))."""
+    G, dev = ps.G, ps.device
+    result = torch.zeros(G, dtype=torch.uint8, device=dev)
+    ctx = torch.zeros(G, dtype=torch.int32, device=dev)
+    index = torch.zeros(G, dtype=torch.int64, device=dev)
+    p = ps.struct()
+    check("qe_read_index", _lib.lib().qe_read_index(
+        C.byref(p), _ptr(request), int(bool(lease_based)), _ptr(result), _ptr(ctx), _ptr(index),
+        _stream(dev)))
+    return result, ctx, index
 
 
 def check_quorum(ps, quorum_active=None, stats=None):

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 4  /* 4: see INTEGRATION.md "ABI 4" (layout changes listed there) */
+#define QE_ABI_VERSION 5  /* 5: see INTEGRATION.md "ABI 5" (layout changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -327,6 +327,16 @@ int qe_election_steps(const qe_election_state *st,
 #define QE_MSG_SNAP_STATUS 4          /* MsgSnapStatus, Reject=false         */
 #define QE_MSG_SNAP_STATUS_REJECT 5   /* MsgSnapStatus, Reject=true          */
 #define QE_MSG_UNREACHABLE 6          /* MsgUnreachable                      */
+#define QE_MSG_TRANSFER_LEADER 7      /* ABI 5: MsgTransferLeader, m.From = the
+                                         slot (raft.go:1339-1370)            */
+
+/* ABI 5: ReadIndex requests a leader keeps pending under ReadOnlySafe
+ * (readOnly.pendingReadIndex + readIndexQueue, raft/read_only.go:39-63), at
+ * most QE_READ_QUEUE per group.  Each request has a context number (the
+ * engine's stand-in for the request's context bytes, unique within the
+ * group): queue entry j has context read_head + j; numbers are 32-bit,
+ * assigned consecutively by qe_read_index, never 0 (0 = no context). */
+#define QE_READ_QUEUE 4
 
 /* Leader-side Progress of every peer of G groups (raft/tracker/progress.go:
  * 30-80) plus the leader's log model: term runs r < run_count[g] covering
@@ -370,12 +380,23 @@ typedef struct qe_progress {
                                    keys); NULL = every slot                  */
   const uint8_t *self_slot;     /* [G] the leader's own slot (bcastAppend
                                    skips it); NULL or >= S = none            */
-  const uint8_t *lead_transferee; /* [G] slot of r.leadTransferee; NULL or
-                                   >= S = no transfer in progress            */
+  uint8_t *lead_transferee;     /* [G] rw (ABI 5): slot of r.leadTransferee;
+                                   >= S = no transfer in progress (None).
+                                   MsgTransferLeader rewrites it; NULL = no
+                                   transfer in progress and the round's
+                                   changes are not stored                    */
   const uint64_t *snap_index;   /* [G] index of the snapshot a MsgSnap
                                    carries; NULL = first_index - 1           */
   uint32_t max_ents;            /* entries per MsgApp (0 = noLimit)          */
   uint32_t reserved2;
+  /* ABI 5: the ReadIndex queue (r.readOnly, ReadOnlySafe); NULL read_acks =
+   * no requests tracked (heartbeat contexts are ignored). */
+  void *read_acks;              /* [G][QE_READ_QUEUE] rw mask-typed: acks of
+                                   queue entry j (0 = oldest) of group g at
+                                   read_acks[g*QE_READ_QUEUE + j] (one 4- or
+                                   8-byte word per group)                    */
+  uint32_t *read_head;          /* [G] rw: context number of queue entry 0   */
+  uint8_t *read_count;          /* [G] rw: pending requests, 0..QE_READ_QUEUE */
 } qe_progress;
 
 /* One round of peer responses: message of slot s for group g at
@@ -399,21 +420,27 @@ typedef struct qe_peer_msgs {
                                    round reads and writes (field granularity,
                                    the rules of DESIGN.md §3) to
                                    *bytes_requested                          */
-  /* ABI 3: ReadIndex under ReadOnlySafe (raft.go:1296-1309,
-   * read_only.go:68-76).  NULL read_acks = no pending request tracked. */
-  void *read_acks;              /* [G] rw mask-typed: acks of the group's
-                                   pending ReadIndex request (recvAck; the
-                                   leader's own ack is set by the caller at
-                                   addRequest, raft.go:1834-1836)           */
-  const void *read_ctx;         /* [G] mask-typed: slots whose
-                                   MsgHeartbeatResp carries the request's
-                                   context (len(m.Context) > 0); NULL =
-                                   every heartbeat response does            */
-  uint8_t *read_ok;             /* [G] out (may be NULL): 1 when a response
-                                   of this round made VoteResult(acks) ==
-                                   VoteWon (readOnly.advance releases the
-                                   request; later responses of the round
-                                   find it gone and record nothing)         */
+  /* ABI 5: ReadIndex under ReadOnlySafe against the queue of p
+   * (raft.go:1296-1309, read_only.go:68-112) */
+  const uint32_t *read_ctx;     /* [S][stride]: context number a
+                                   MsgHeartbeatResp carries (0 = none,
+                                   len(m.Context) == 0); NULL = every one
+                                   carries the newest context pending when
+                                   the round starts (bcastHeartbeat attaches
+                                   lastPendingRequestCtx, raft.go:525-532)   */
+  uint8_t *read_released;       /* [G] out (may be NULL): requests released
+                                   this round, oldest first (readOnly.advance
+                                   dequeues through the acked request)      */
+  uint8_t *term_commit;         /* [G] out (may be NULL): 1 when this round's
+                                   maybeCommit made committedEntryInCurrentTerm
+                                   true, i.e. the leader's postponed
+                                   MsgReadIndex requests are released now
+                                   (raft.go:1259-1262, :1731-1733, :1813-1825) */
+  uint64_t *term_commit_index;  /* [G] out (may be NULL): raftLog.committed
+                                   right after that maybeCommit -- the index
+                                   the released requests are added at
+                                   (sendMsgReadIndexResponse, raft.go:1834);
+                                   written only where term_commit is 1       */
 } qe_peer_msgs;
 
 /* Leader-side handling of one message per peer, slots in ascending order
@@ -429,18 +456,56 @@ typedef struct qe_peer_msgs {
  *     `for maybeSendAppend(from, false) {}`; MsgTimeoutNow to the lead
  *     transferee once its Match == lastIndex (raft.go:1275-1281).
  *   MsgHeartbeatResp: RecentActive, ProbeSent = false, FreeFirstOne when the
- *     inflights are full, sendAppend if Match < lastIndex; with read_acks,
- *     a response carrying the request's context: recvAck, and the request
- *     is released once Voters.VoteResult(acks) == VoteWon.
+ *     inflights are full, sendAppend if Match < lastIndex; with p->read_acks,
+ *     a response carrying a context (ABI 5): recvAck on the queue entry with
+ *     that context number (none pending: nothing is recorded), and once
+ *     Voters.VoteResult(that entry's acks) == VoteWon, readOnly.advance
+ *     releases every entry up to and including it (read_only.go:68-112).
  *   MsgSnapStatus (StateSnapshot only): reject -> PendingSnapshot = 0;
  *     BecomeProbe; ProbeSent = true (raft.go:1310-1331).
  *   MsgUnreachable: Replicate -> BecomeProbe (raft.go:1332-1338).
+ *   MsgTransferLeader (ABI 5, raft.go:1339-1370): a learner's is ignored; a
+ *     transfer to the slot already in progress is ignored; another transfer
+ *     in progress is aborted; a transfer to self_slot is then ignored;
+ *     otherwise lead_transferee = the slot, and MsgTimeoutNow goes out at
+ *     once when its Match == lastIndex, else sendAppend to it.  (The
+ *     reference also resets electionElapsed: tick state stays with the host,
+ *     which sees the new lead_transferee.)
  * A send is raft.maybeSendAppend (raft.go:432-492) on the log model; see
  * qe_progress_send.  Messages from untracked slots are dropped.  An accept
  * with index > lastIndex is processed as the reference does and counted as
  * an invariant violation. */
 int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
                      void *stream);
+
+/* ABI 5: MsgReadIndex on every group's leader whose request[g] is 1
+ * (stepLeader, raft/raft.go:1078-1096, sendMsgReadIndexResponse :1827-1843),
+ * result[g] (QE_RI_*):
+ *   IsSingleton (one voter in Voters[0], Voters[1] empty; tracker.go:158-160)
+ *     -> QE_RI_RESPOND at index = committed;
+ *   no entry of the leader's term committed yet (committedEntryInCurrentTerm,
+ *     :1731-1733: term_start <= committed <= last_index on the log model)
+ *     -> QE_RI_POSTPONED (pendingReadIndexMessages; the host keeps the
+ *     message and adds it again once qe_progress_step reports term_commit --
+ *     its read index is that round's term_commit_index);
+ *   lease_based (ReadOnlyLeaseBased) -> QE_RI_RESPOND at committed;
+ *   ReadOnlySafe -> readOnly.addRequest(committed) + the leader's own ack
+ *     (self_slot; recvAck(r.id)): QE_RI_QUEUED with context number ctx[g]
+ *     and index = committed; the host sends the heartbeats carrying ctx and
+ *     answers when qe_progress_step releases the entry.  With QE_READ_QUEUE
+ *     requests already pending (or the context numbers exhausted:
+ *     read_head + read_count would be 0 mod 2^32) -> QE_RI_FULL, nothing
+ *     changes (an engine limit; the host retries later).
+ * Needs p->read_acks / read_head / read_count unless every result is
+ * RESPOND or POSTPONED (lease_based).  ctx and index may be NULL; they are
+ * written only where they apply.  Groups without a request: result 0. */
+#define QE_RI_NONE 0
+#define QE_RI_RESPOND 1
+#define QE_RI_POSTPONED 2
+#define QE_RI_QUEUED 3
+#define QE_RI_FULL 4
+int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
+                  uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream);
 
 /* MsgCheckQuorum on every group's leader (stepLeader, raft/raft.go:997-1018):
  * the leader's own Progress (self_slot, when tracked) becomes RecentActive;
@@ -449,9 +514,15 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
  * RecentActive, a voter without a Progress missing) -- 0 means the leader
  * steps down (becomeFollower); then RecentActive = false for every tracked
  * slot but the leader's (prs.Visit, raft.go:1013-1017).  Reads inc_mask /
- * out_mask / tracked / self_slot and the peer words of p, rewrites only the
- * words that change.  quorum_active may be NULL.  stats: groups, stepdowns
- * (QE_STAT_STEPDOWNS), checksum. */
+ * out_mask / tracked / self_slot and the peer words of p.  A slot row in
+ * which some group's word changes is rewritten for every tracked slot of
+ * the tile, unchanged words included (whole sectors; the values written are
+ * the round's result either way), so concurrent writers of other words of
+ * p->peer must not overlap the call.  self_slot NULL (or >= S) means the
+ * leader has no Progress of its own (the reference then marks nobody
+ * active, raft.go:1000-1002): a caller whose leader has a slot must pass
+ * it, or the leader is not counted as active.  quorum_active may be NULL.
+ * stats: groups, stepdowns (QE_STAT_STEPDOWNS), checksum. */
 int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stats,
                     void *stream);
 
@@ -609,8 +680,11 @@ int qe_pack_threads(int n);
  * num_slots <= 8, else u16) over tracked slots; is_learner is
  * Progress.IsLearner.  slot_ids is ID-major [S][G] (ABI 3: slot s of group
  * g at slot_ids[s*G + g]) as written by qe_pack_confstate, so a change
- * rewrites only the changed slot's row; the ids of untracked slots are
- * ignored on input and written as 0. */
+ * rewrites only the changed slot's row.  The ids of untracked slots are
+ * ignored on input (qe_confchange) and left as they are, except that a slot
+ * a change untracks gets 0; the packer writes 0 for every unused slot.
+ * qe_pack_match / qe_pack_votes / qe_slot_lookup match ids over all S slots,
+ * so a caller that writes slot_ids itself keeps untracked ones 0. */
 typedef struct qe_conf {
   uint64_t num_groups;
   uint32_t num_slots;

@@ -60,6 +60,7 @@ def _declare(L):
         "orc_max_threads": (i32, []),
         "orc_progress_step_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcMsgs), vp, i32]),
         "orc_check_quorum_batch": (None, [C.POINTER(OrcProg), vp, vp]),
+        "orc_read_index_batch": (None, [C.POINTER(OrcProg), vp, u32, vp, vp, vp]),
         "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
@@ -168,7 +169,8 @@ class OrcProg(C.Structure):
         ("run_term", C.c_void_p), ("run_count", C.c_void_p), ("inc", C.c_void_p),
         ("out", C.c_void_p), ("tracked", C.c_void_p), ("self_slot", C.c_void_p),
         ("lead_transferee", C.c_void_p), ("snap_index", C.c_void_p), ("max_ents", C.c_uint32),
-        ("reserved2", C.c_uint32),
+        ("reserved2", C.c_uint32), ("read_acks", C.c_void_p), ("read_head", C.c_void_p),
+        ("read_count", C.c_void_p),
     ]
 
 
@@ -176,8 +178,9 @@ class OrcMsgs(C.Structure):
     _fields_ = [("type", C.c_void_p), ("index", C.c_void_p), ("hint", C.c_void_p),
                 ("logterm", C.c_void_p), ("sent", C.c_void_p), ("bcast", C.c_void_p),
                 ("snap", C.c_void_p), ("timeout_now", C.c_void_p), ("msg_count", C.c_void_p),
-                ("msg_index", C.c_void_p), ("read_acks", C.c_void_p), ("read_ctx", C.c_void_p),
-                ("read_ok", C.c_void_p), ("bytes", C.c_void_p)]
+                ("msg_index", C.c_void_p), ("read_ctx", C.c_void_p),
+                ("read_released", C.c_void_p), ("term_commit", C.c_void_p),
+                ("term_commit_index", C.c_void_p), ("bytes", C.c_void_p)]
 
 
 PF_STATE, PF_PROBE_SENT, PF_RECENT_ACTIVE = 3, 4, 8
@@ -197,7 +200,9 @@ class ProgressBatch:
     `istart`, `icount` are read-only views of their fields (set_peer
     rewrites them)."""
 
-    OPTIONAL = ("inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index")
+    OPTIONAL = ("inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index",
+                "read_acks", "read_head", "read_count")
+    READ_QUEUE = 4
 
     def __init__(self, G, S, F, R, stride=None, max_ents=0):
         self.G, self.S, self.F, self.R = G, S, F, R
@@ -238,6 +243,15 @@ class ProgressBatch:
         ct = self.icount if icount is None else np.broadcast_to(icount, self.pw.shape)
         self.pw[:] = pack_word(f, st, ct)
 
+    def track_reads(self):
+        """Allocate the ReadIndex queue (ABI 5): acks word per group (uint32
+        for S <= 8, uint64 above: entry j in bits [8*mb*j, ...)), the
+        context number of entry 0 (starting at 1) and the count."""
+        self.read_acks = np.zeros(self.G, np.uint32 if self.S <= 8 else np.uint64)
+        self.read_head = np.ones(self.G, np.uint32)
+        self.read_count = np.zeros(self.G, np.uint8)
+        return self
+
     def copy(self):
         c = ProgressBatch.__new__(ProgressBatch)
         for k, v in self.__dict__.items():
@@ -251,7 +265,8 @@ class ProgressBatch:
                        P(self.last_index), self.R, 0, P(self.run_first), P(self.run_term),
                        P(self.run_count), P(self.inc), P(self.out), P(self.tracked),
                        P(self.self_slot), P(self.lead_transferee), P(self.snap_index),
-                       self.max_ents, 0)
+                       self.max_ents, 0, P(self.read_acks), P(self.read_head),
+                       P(self.read_count))
 
 
 class StepOut:
@@ -265,24 +280,29 @@ class StepOut:
         self.timeout_now = np.zeros(pb.G, md)
         self.msg_count = np.zeros(pb.S * pb.stride, np.uint8)
         self.msg_index = np.zeros(pb.S * pb.stride, np.uint64)
-        self.read_ok = np.zeros(pb.G, np.uint8)
+        self.read_released = np.zeros(pb.G, np.uint8)
+        self.term_commit = np.zeros(pb.G, np.uint8)
+        self.term_commit_index = np.zeros(pb.G, np.uint64)
         self.stats = np.zeros(NSTAT, np.uint64)
         self.bytes = np.zeros(1, np.uint64)
 
 
-def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0, read_acks=None,
-                  read_ctx=None, outputs=True, count_bytes=False):
+def progress_step(pb, mtype, mindex, mhint, mlogterm, goff=0, threads=0, read_ctx=None,
+                  outputs=True, count_bytes=False):
     """One round of stepLeader message handling (oracle).  Returns StepOut.
-    read_acks (mask array, updated in place) / read_ctx: the ReadIndex
-    request of each group (ABI 3).  outputs=False leaves the optional outputs
-    NULL (as a kernel call without them); count_bytes: o.bytes[0] = the
-    round's algorithmic bytes by the accounting rules."""
+    The ReadIndex queue is pb's (pb.track_reads()); read_ctx (uint32
+    [S][stride]) the contexts heartbeat responses carry (None: the newest
+    pending).  outputs=False leaves the optional outputs NULL (as a kernel
+    call without them); count_bytes: o.bytes[0] = the round's algorithmic
+    bytes by the accounting rules."""
     o = StepOut(pb)
     opt = (lambda a: P(a)) if outputs else (lambda a: None)
+    if read_ctx is not None:
+        read_ctx = np.ascontiguousarray(read_ctx, np.uint32)
     m = OrcMsgs(P(mtype), P(mindex), P(mhint), P(mlogterm), opt(o.sent), opt(o.bcast),
                 opt(o.snap), opt(o.timeout_now), opt(o.msg_count), opt(o.msg_index),
-                P(read_acks), P(read_ctx) if read_acks is not None else None,
-                P(o.read_ok) if (read_acks is not None and outputs) else None,
+                P(read_ctx) if pb.read_acks is not None else None, opt(o.read_released),
+                opt(o.term_commit), opt(o.term_commit_index),
                 P(o.bytes) if count_bytes else None)
     s = pb.struct(goff)
     lib().orc_progress_step_batch(C.byref(s), C.byref(m), P(o.stats), threads)
@@ -297,6 +317,18 @@ def progress_send(pb, want, send_if_empty, max_ents=None):
     me = pb.max_ents if max_ents is None else max_ents
     lib().orc_progress_send_batch(C.byref(s), P(want), send_if_empty, me, P(sent), P(snap))
     return sent, snap
+
+
+def read_index(pb, request, lease_based=False):
+    """MsgReadIndex on the leader of every group with request[g] != 0
+    (oracle) -> (result uint8[G], ctx uint32[G], index uint64[G])."""
+    result = np.zeros(pb.G, np.uint8)
+    ctx = np.zeros(pb.G, np.uint32)
+    index = np.zeros(pb.G, np.uint64)
+    s = pb.struct()
+    lib().orc_read_index_batch(C.byref(s), P(np.ascontiguousarray(request, np.uint8)),
+                               int(bool(lease_based)), P(result), P(ctx), P(index))
+    return result, ctx, index
 
 
 def check_quorum(pb, goff=0):

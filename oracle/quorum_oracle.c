@@ -999,9 +999,14 @@ typedef struct orc_prog {
   const void *inc, *out;
   const void *tracked;            /* NULL: every slot holds a Progress      */
   const uint8_t *self_slot;       /* NULL / >= S: the leader has no slot    */
-  const uint8_t *lead_transferee; /* NULL / >= S: no transfer in progress   */
+  uint8_t *lead_transferee;       /* rw; NULL / >= S: no transfer           */
   const uint64_t *snap_index;     /* NULL: first_index - 1                  */
   uint32_t max_ents, reserved2;   /* entries per MsgApp, 0 = noLimit        */
+  /* the ReadIndex queue (qe_progress ABI 5): acks word per group (entry j
+   * of mask width at bits [8*mb*j, ...)), context number of entry 0, count */
+  void *read_acks;
+  uint32_t *read_head;
+  uint8_t *read_count;
 } orc_prog;
 
 typedef struct orc_msgs {
@@ -1013,15 +1018,77 @@ typedef struct orc_msgs {
   void *timeout_now;   /* [G] slots sent MsgTimeoutNow                    */
   uint8_t *msg_count;  /* [S][stride] messages sent to the peer           */
   uint64_t *msg_index; /* [S][stride] m.Index of the first of them        */
-  void *read_acks;     /* [G] rw ReadIndex acks (NULL: none tracked)      */
-  const void *read_ctx;/* [G] heartbeat responses carrying the context    */
-  uint8_t *read_ok;    /* [G] out: request released this round            */
+  const uint32_t *read_ctx;   /* [S][stride] context a heartbeat response
+                                 carries (0 none); NULL: the newest pending */
+  uint8_t *read_released;     /* [G] out: requests released this round    */
+  uint8_t *term_commit;       /* [G] out: first commit in the leader's term */
+  uint64_t *term_commit_index;/* [G] out: committed right after it          */
   uint64_t *bytes;     /* byte accounting (DESIGN.md §3 rules), or NULL   */
 } orc_msgs;
 
 /* message kinds (qe_peer_msgs.type) */
 enum { M_NONE = 0, M_APP_RESP, M_APP_RESP_REJECT, M_HEARTBEAT_RESP, M_SNAP_STATUS,
-       M_SNAP_STATUS_REJECT, M_UNREACHABLE };
+       M_SNAP_STATUS_REJECT, M_UNREACHABLE, M_TRANSFER_LEADER };
+#define READ_QUEUE 4 /* QE_READ_QUEUE */
+
+/* readOnly (raft/read_only.go:39-63) of one group as the reference keeps
+ * it: the queue of pending requests in arrival order, each with its
+ * context (here its context number) and its acks (a set of slots). */
+typedef struct orc_ro {
+  uint32_t n;                      /* len(readIndexQueue)                  */
+  uint32_t ctx[READ_QUEUE];        /* readIndexQueue                       */
+  uint32_t acks[READ_QUEUE];       /* pendingReadIndex[ctx].acks           */
+} orc_ro;
+
+static uint64_t ro_word_get(const void *w, uint32_t mb, uint64_t g) {
+  return mb == 1 ? ((const uint32_t *)w)[g] : ((const uint64_t *)w)[g];
+}
+static void ro_word_set(void *w, uint32_t mb, uint64_t g, uint64_t v) {
+  if (mb == 1) ((uint32_t *)w)[g] = (uint32_t)v;
+  else ((uint64_t *)w)[g] = v;
+}
+/* the device form -> the queue: entry j has context head + j */
+static void ro_load(orc_ro *r, uint64_t word, uint32_t head, uint32_t count, uint32_t mb) {
+  r->n = count < READ_QUEUE ? count : READ_QUEUE;
+  for (uint32_t j = 0; j < r->n; j++) {
+    r->ctx[j] = head + j;
+    r->acks[j] = (uint32_t)(word >> (8 * mb * j)) & ((1u << (8 * mb)) - 1u);
+  }
+}
+/* the queue -> the device form (entries past the count 0) */
+static uint64_t ro_word(const orc_ro *r, uint32_t mb) {
+  uint64_t w = 0;
+  for (uint32_t j = 0; j < r->n; j++) w |= (uint64_t)r->acks[j] << (8 * mb * j);
+  return w;
+}
+/* recvAck (read_only.go:68-76): index of the pending request with context
+ * ctx, or -1 (recvAck returns nil: nothing recorded) */
+static int ro_find(const orc_ro *r, uint32_t ctx) {
+  if (ctx == 0) return -1; /* len(m.Context) == 0 (raft.go:1296) */
+  for (uint32_t j = 0; j < r->n; j++)
+    if (r->ctx[j] == ctx) return (int)j;
+  return -1;
+}
+/* advance (read_only.go:81-112): dequeue the requests up to and including
+ * the one with context ctx; returns how many were released */
+static uint32_t ro_advance(orc_ro *r, uint32_t ctx) {
+  uint32_t i = 0;
+  int found = 0;
+  for (uint32_t j = 0; j < r->n; j++) {
+    i++;
+    if (r->ctx[j] == ctx) {
+      found = 1;
+      break;
+    }
+  }
+  if (!found) return 0;
+  for (uint32_t j = i; j < r->n; j++) {
+    r->ctx[j - i] = r->ctx[j];
+    r->acks[j - i] = r->acks[j];
+  }
+  r->n -= i;
+  return i;
+}
 
 static uint32_t pr_word(const orc_pr *p) {
   return p->state | (p->probe_sent ? PF_PROBE_SENT : 0) | (p->recent_active ? PF_RECENT_ACTIVE : 0) |
@@ -1106,13 +1173,18 @@ static int send_append(orc_gctx *c, orc_pr *p, uint32_t s, int send_if_empty) {
   return 1;
 }
 
-/* Per-group parts: (commit, bcast count), the sent mask and a released
- * ReadIndex request. */
+/* Per-group parts: (commit, bcast count), the sent mask, the ReadIndex
+ * requests released, the first commit in the leader's term and a changed
+ * lead transferee. */
 uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint32_t bcast,
-                           uint32_t released) {
-  return orc_mix64((gid * PHI) ^ committed ^ ((uint64_t)bcast << 62)) +
-         orc_mix64((gid * PHI) ^ ((uint64_t)send << 40) ^ 0xD1B54A32D192ED03ull) +
-         (released ? orc_mix64((gid * PHI) ^ 0x8CB92BA72F3D8DD7ull) : 0);
+                           uint32_t released, int term_commit, uint64_t term_commit_index,
+                           int lt_changed, uint32_t lt) {
+  uint64_t h = gid * PHI;
+  return orc_mix64(h ^ committed ^ ((uint64_t)bcast << 62)) +
+         orc_mix64(h ^ ((uint64_t)send << 40) ^ 0xD1B54A32D192ED03ull) +
+         (released ? orc_mix64(h ^ 0x8CB92BA72F3D8DD7ull ^ ((uint64_t)released << 56)) : 0) +
+         (term_commit ? orc_mix64(h ^ 0x589965CC75374CC3ull ^ term_commit_index) : 0) +
+         (lt_changed ? orc_mix64(h ^ 0x1D8E4E27C47D124Full ^ lt) : 0);
 }
 
 /* One round of leader-side message handling per group, messages taken in
@@ -1135,6 +1207,16 @@ uint64_t orc_checksum_step(uint64_t gid, uint64_t committed, uint32_t send, uint
  *   MsgSnapStatus      in StateSnapshot only: (reject -> PendingSnapshot =
  *                      0), BecomeProbe, ProbeSent = true        :1310-1331
  *   MsgUnreachable     Replicate -> BecomeProbe                 :1332-1338
+ *   MsgTransferLeader  learner: ignored; same transferee: ignored; another
+ *                      in progress: aborted; to self: ignored; else
+ *                      leadTransferee = from, MsgTimeoutNow if its Match ==
+ *                      lastIndex, else sendAppend             :1339-1370
+ * MsgHeartbeatResp under ReadOnlySafe with a context: recvAck, and
+ * VoteResult(acks) == VoteWon -> readOnly.advance (:1296-1309).  Every
+ * maybeCommit that returns true calls releasePendingReadIndexMessages
+ * (:1259-1262), which answers the postponed MsgReadIndex requests once
+ * committedEntryInCurrentTerm holds (:1813-1825): reported as term_commit
+ * with the committed index at that moment.
  * A message from a slot without a Progress is dropped (:1100-1104).  The
  * commit gate is raftLog.maybeCommit on the log model (term(i) == Term <=>
  * term_start <= i <= last_index, log.go:325-331).  An accept beyond
@@ -1170,7 +1252,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
       uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
       uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
       uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
-      uint32_t lt = a->lead_transferee ? a->lead_transferee[g] : 0xFFu;
+      uint32_t lt = a->lead_transferee ? a->lead_transferee[g] : 0xFFu, lt0 = lt;
       uint64_t ts = a->term_start[g], li = c.li, cm = a->committed[g], c0 = cm;
       uint32_t nr = a->run_count[g] < a->R ? a->run_count[g] : a->R;
       uint64_t rf[16], rt[16];
@@ -1178,10 +1260,23 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         rf[r] = a->run_first[r * a->stride + g];
         rt[r] = a->run_term[r * a->stride + g];
       }
-      /* ReadOnlySafe: the pending request's acks (read_only.go:68-76) */
-      uint32_t acks = m->read_acks ? ld_mask(m->read_acks, mb, g) & full : 0, acks0 = acks;
-      uint32_t rctx = (m->read_acks && m->read_ctx) ? ld_mask(m->read_ctx, mb, g) & full : full;
-      int released = 0;
+      /* ReadOnlySafe: the leader's readOnly queue (read_only.go:39-63) */
+      int rd = a->read_acks != NULL;
+      orc_ro ro;
+      uint64_t rword0 = 0;
+      uint32_t rhead0 = 0, rn0 = 0, released = 0, dctx = 0;
+      int rtouch = 0;
+      ro.n = 0;
+      if (rd) {
+        rword0 = ro_word_get(a->read_acks, mb, g);
+        rhead0 = a->read_head[g];
+        ro_load(&ro, rword0, rhead0, a->read_count[g], mb);
+        rn0 = ro.n;
+        /* lastPendingRequestCtx (raft.go:525-532) */
+        dctx = ro.n ? ro.ctx[ro.n - 1] : 0;
+      }
+      int first_commit = 1;
+      uint64_t tci = 0;
       /* byte accounting (only when m->bytes): everything the round needs,
        * field granularity, each once */
       uint64_t B = 0;
@@ -1232,6 +1327,11 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
             for (uint32_t q = 0; q < S; q++) vals[q] = prs[q].match;
             uint64_t mci = orc_joint_committed(S, mi, mo, vals);
             if (orc_maybe_commit(mci, &cm, ts, li)) {
+              /* releasePendingReadIndexMessages: the reads postponed while no
+               * entry of this term was committed are answered at the commit
+               * of this moment (the first such call of the round) */
+              if (first_commit) tci = cm;
+              first_commit = 0;
               if (bc < 255) bc++;
               /* bcastAppend: every Progress but the leader's own (:515-522) */
               for (uint32_t q = 0; q < S; q++)
@@ -1249,11 +1349,17 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
           if (p->state == PR_REPLICATE && infl_full(p)) infl_free_le(p, *ib(p, p->start));
           if (p->match < li) send_append(&c, p, s, 1);
           /* :1296-1309: ReadOnlySafe with a context -> recvAck; a won vote
-           * releases the request (readOnly.advance removes it, so a later
-           * response's recvAck returns nil and records nothing) */
-          if (m->read_acks && !released && ((rctx >> s) & 1u)) {
-            acks |= 1u << s;
-            if (orc_joint_vote(mi, mo, acks, acks) == VOTE_WON) released = 1;
+           * -> advance releases the queue through that request (a later
+           * response carrying a released context records nothing) */
+          if (rd) {
+            uint32_t cx = m->read_ctx ? m->read_ctx[off] : dctx;
+            int j = ro_find(&ro, cx);
+            if (j >= 0) {
+              ro.acks[j] |= 1u << s;
+              rtouch = 1;
+              if (orc_joint_vote(mi, mo, ro.acks[j], ro.acks[j]) == VOTE_WON)
+                released += ro_advance(&ro, cx);
+            }
           }
         } else if (ty == M_SNAP_STATUS || ty == M_SNAP_STATUS_REJECT) {
           if (p->state == PR_SNAPSHOT) {
@@ -1263,18 +1369,37 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
           }
         } else if (ty == M_UNREACHABLE) {
           if (p->state == PR_REPLICATE) pr_become_probe(p);
+        } else if (ty == M_TRANSFER_LEADER) {
+          int is_learner = !(((mi | mo) >> s) & 1u); /* tracked, not a voter */
+          if (!is_learner) {
+            int go = 1;
+            if (lt < S) {              /* lastLeadTransferee != None */
+              if (lt == s) go = 0;     /* same node: ignored */
+              else lt = 0xFFu;         /* abortLeaderTransfer */
+            }
+            if (go && s == self) go = 0; /* already leader */
+            if (go) {
+              lt = s;
+              if (p->match == li) tnow |= 1u << s; /* sendTimeoutNow */
+              else send_append(&c, p, s, 1);
+            }
+          }
         }
       }
+      int tc = cm != c0 && !(c0 >= ts && c0 <= li); /* committedEntryInCurrentTerm became true */
+      uint64_t rword = rd ? ro_word(&ro, mb) : 0;
+      int wq = rd && rtouch && rword != rword0;
       if (m->bytes) {
         /* per group: masks, log model, commit, ReadIndex masks */
         B += (a->inc ? mb : 0) + (a->out ? mb : 0) + (a->tracked ? mb : 0) + (a->self_slot ? 1 : 0) +
-             (a->lead_transferee ? 1 : 0) + 32 + (a->snap_index ? 8 : 0) +
-             (m->read_acks ? mb : 0) + ((m->read_acks && m->read_ctx) ? mb : 0);
+             (a->lead_transferee ? 1 : 0) + 32 + (a->snap_index ? 8 : 0);
+        /* the queue: head and count, the acks word when requests pend */
+        B += rd ? 5 + (rn0 ? READ_QUEUE * mb : 0) : 0;
         for (uint32_t s = 0; s < S; s++) {
           uint64_t off = s * a->stride + g;
           int tr = (trk >> s) & 1u;
           uint32_t ty = tr ? m->type[off] : 0;
-          int msg = ty >= M_APP_RESP && ty <= M_UNREACHABLE;
+          int msg = ty >= M_APP_RESP && ty <= M_TRANSFER_LEADER;
           int touched = tr && (msg || (bc > 0 && s != self));
           const orc_pr *p = &prs[s];
           B += 8;                                             /* Match (the commit pass) */
@@ -1283,6 +1408,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
           if (touched) {
             B += 12;                                          /* Next + the packed word  */
             B += ty == M_APP_RESP_REJECT ? 16 : 0;            /* RejectHint, LogTerm     */
+            B += (rd && m->read_ctx && ty == M_HEARTBEAT_RESP) ? 4 : 0; /* its context   */
             B += state0[s] == PR_SNAPSHOT ? 8 : 0;            /* PendingSnapshot         */
             B += p->match != match0[s] ? 8 : 0;
             B += p->next != next0[s] ? 8 : 0;
@@ -1295,8 +1421,11 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         B += runs_read ? 1 + 16 * (uint64_t)nr : 0;           /* the term-run table      */
         B += cm != c0 ? 8 : 0;
         B += (m->sent ? mb : 0) + (m->snap ? mb : 0) + (m->timeout_now ? mb : 0) +
-             (m->bcast ? 1 : 0) + (m->read_ok ? 1 : 0);
-        B += (m->read_acks && acks != acks0) ? mb : 0;
+             (m->bcast ? 1 : 0) + (m->read_released ? 1 : 0) + (m->term_commit ? 1 : 0);
+        B += wq ? READ_QUEUE * mb : 0;
+        B += released ? 5 : 0;
+        B += (tc && m->term_commit_index) ? 8 : 0;
+        B += (a->lead_transferee && lt != lt0) ? 1 : 0;
         lbytes += B;
       }
       for (uint32_t s = 0; s < S; s++) pr_store2(&prs[s], a, s, g);
@@ -1305,13 +1434,21 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
       if (m->snap) st_mask(m->snap, mb, g, c.snapm);
       if (m->timeout_now) st_mask(m->timeout_now, mb, g, tnow);
       if (m->bcast) m->bcast[g] = (uint8_t)bc;
-      if (m->read_acks) st_mask(m->read_acks, mb, g, acks);
-      if (m->read_ok) m->read_ok[g] = (uint8_t)released;
+      if (wq) ro_word_set(a->read_acks, mb, g, rword);
+      if (rd && released) {
+        a->read_head[g] = rhead0 + released;
+        a->read_count[g] = (uint8_t)ro.n;
+      }
+      if (m->read_released) m->read_released[g] = (uint8_t)released;
+      if (m->term_commit) m->term_commit[g] = (uint8_t)tc;
+      if (m->term_commit_index && tc) m->term_commit_index[g] = tci;
+      if (a->lead_transferee && lt != lt0) a->lead_transferee[g] = (uint8_t)lt;
       ls[ST_GROUPS] += 1;
       ls[ST_COMMIT_SUM] += cm;
       ls[ST_COMMIT_ADVANCED] += (cm != c0);
       ls[ST_READ_RELEASED] += released;
-      ls[ST_CHECKSUM] += orc_checksum_step(a->goff + g, cm, c.sent, bc, released);
+      ls[ST_CHECKSUM] += orc_checksum_step(a->goff + g, cm, c.sent, bc, released, tc, tci,
+                                           lt != lt0, lt);
     }
 #pragma omp critical
     {
@@ -1361,6 +1498,61 @@ void orc_check_quorum_batch(const orc_prog *a, uint8_t *qa, uint64_t *stats) {
   }
   if (stats)
     for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+}
+
+/* MsgReadIndex on each group's leader with request[g] != 0 (stepLeader,
+ * raft/raft.go:1078-1096; sendMsgReadIndexResponse :1827-1843):
+ *   r.prs.IsSingleton() (tracker.go:158-160) -> respond at committed;
+ *   !committedEntryInCurrentTerm() (:1731-1733) -> postponed;
+ *   ReadOnlyLeaseBased -> respond at committed;
+ *   ReadOnlySafe -> addRequest(committed, m) + recvAck(r.id) (read_only.go:
+ *   56-76), the request's context number being the next in the queue; a
+ *   queue of READ_QUEUE requests (or exhausted numbers) -> full (the
+ *   engine's limit, nothing changes).
+ * result: 1 respond, 2 postponed, 3 queued, 4 full (QE_RI_*). */
+void orc_read_index_batch(const orc_prog *a, const uint8_t *request, uint32_t lease_based,
+                          uint8_t *result, uint32_t *ctx, uint64_t *index) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  for (uint64_t g = 0; g < a->G; g++) {
+    result[g] = 0;
+    if (!request[g]) continue;
+    uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+    uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+    uint64_t c = a->committed[g], ts = a->term_start[g], li = a->last_index[g];
+    if (popc(mi) == 1 && mo == 0) { /* only one voting member: the leader */
+      result[g] = 1;
+      if (index) index[g] = c;
+      continue;
+    }
+    if (!(c >= ts && c <= li)) { /* no entry of this term committed yet */
+      result[g] = 2;
+      continue;
+    }
+    if (lease_based) {
+      result[g] = 1;
+      if (index) index[g] = c;
+      continue;
+    }
+    orc_ro ro;
+    uint32_t head = a->read_head[g];
+    ro_load(&ro, ro_word_get(a->read_acks, mb, g), head, a->read_count[g], mb);
+    if (ro.n == 0 && head == 0) head = 1; /* context numbers start at 1 */
+    if (ro.n >= READ_QUEUE || head + ro.n == 0u) {
+      result[g] = 4;
+      continue;
+    }
+    uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+    ro.ctx[ro.n] = head + ro.n;                              /* addRequest */
+    ro.acks[ro.n] = self < S ? 1u << self : 0u;              /* recvAck(r.id) */
+    ro.n++;
+    ro_word_set(a->read_acks, mb, g, ro_word(&ro, mb));
+    a->read_head[g] = head;
+    a->read_count[g] = (uint8_t)ro.n;
+    result[g] = 3;
+    if (ctx) ctx[g] = head + ro.n - 1;
+    if (index) index[g] = c;
+  }
 }
 
 /* raft.sendAppend / maybeSendAppend(to, send_if_empty) once for every slot

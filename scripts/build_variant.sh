@@ -13,4 +13,4 @@ if [ "$WHAT" = prog ]; then
   cp -p "$R"/etcd_amd/build/qe_inst_[0-9]*.o "$R"/etcd_amd/build/qe_api.o "$R"/etcd_amd/build/qe_pack.o \
         "$R"/etcd_amd/build/qe_host.o "$R"/etcd_amd/build/qe_comm.o "$OBJ"/
 fi
-make -s -j8 -C "$R/etcd_amd/csrc" OBJDIR="$OBJ" LIBOUT="$R/etcd_amd/lib/variants/libetcd_quorum_$NAME.so" EXTRA="$FLAGS"
+make -s -j8 -C "$R/etcd_amd/csrc" OBJDIR="$OBJ" LIBOUT="$R/etcd_amd/lib/variants/libetcd_quorum_$NAME.so" EXTRA="-DQE_VARIANT_BUILD $FLAGS"

@@ -10,4 +10,4 @@ OBJ=$R/etcd_amd/build_$NAME
 rm -rf "$OBJ"; mkdir -p "$OBJ" "$R/etcd_amd/lib/variants"
 cp -p "$R"/etcd_amd/build/*.o "$R"/etcd_amd/build/*.d "$OBJ"/
 for o in ${OBJS:-qe_inst_prog_5}; do rm -f "$OBJ/$o.o"; done
-make -s -j8 -C "$R/etcd_amd/csrc" OBJDIR="$OBJ" LIBOUT="$R/etcd_amd/lib/variants/libetcd_quorum_$NAME.so" EXTRA="$FLAGS"
+make -s -j8 -C "$R/etcd_amd/csrc" OBJDIR="$OBJ" LIBOUT="$R/etcd_amd/lib/variants/libetcd_quorum_$NAME.so" EXTRA="-DQE_VARIANT_BUILD $FLAGS"

@@ -1,21 +1,26 @@
-"""Leader-side transcriptions of the reference tests that pin the two
-stepLeader decisions ABI 3 fuses onto the resident Progress state: the
-ReadIndex ack on MsgHeartbeatResp (raft/raft.go:1296-1309,
-raft/read_only.go:68-76) and MsgCheckQuorum (raft/raft.go:997-1018).
+"""Leader-side transcriptions of the reference tests that pin the stepLeader
+decisions fused onto the resident Progress state: ReadIndex as readOnly
+keeps it (MsgReadIndex raft/raft.go:1078-1096, the queue of
+raft/read_only.go:39-112, the heartbeat acks :1296-1309, the postponed
+reads of a new leader :1259-1262 / :1813-1825), MsgCheckQuorum
+(raft/raft.go:997-1018) and MsgTransferLeader (raft/raft.go:1339-1370).
 
 Each reference test drives a small in-process cluster; the leader's view of
 it is restated here as rounds of the batch engine on one group (slot s is
 node id s+1, slot 0 is the leader), through the backend interface of
 tests/progress_scenarios.py plus
-  step(t, idx, hint, lt, read=(acks, ctx) or None) -> out with "read_ok",
-      "acks" when read is given
+  step(t, idx, hint, lt, ctx=None) -> out with "read_released",
+      "term_commit", "term_commit_index", "timeout_now"
+  read_index(lease_based=False) -> (QE_RI_* result, context number, index)
+  queue() -> (pending count, head context number, acks of each entry)
+  transferee() -> lead_transferee slot (0xFF none)
   check_quorum() -> (quorum_active, RecentActive bits of the slots).
 The same functions drive the oracle (CPU tests) and the HIP engine (GPU
 tests).  Expectations are what each reference test asserts; the rest of
 its message flow (proposals, appends, acks) is executed, not assumed."""
 import numpy as np
 
-from tests.progress_scenarios import F_CAP, PF_RECENT_ACTIVE, initial_arrays
+from tests.progress_scenarios import F_CAP, PF_RECENT_ACTIVE, bits, initial_arrays
 
 REPLICATE = 1
 
@@ -56,12 +61,23 @@ def _propose(be, S, voters_acking):
     be.step(t, idx, z, z)
 
 
-def _heartbeat_round(be, S, slots, acks, ctx=None):
+def _heartbeat_round(be, S, slots, ctx=None):
+    """MsgHeartbeatResp from `slots`; ctx: None (each carries the newest
+    pending context, as the heartbeats of bcastHeartbeat do), an int (every
+    one carries that context number, 0 = none) or a per-slot dict."""
     t = np.zeros(S, np.uint8)
     for s in slots:
         t[s] = 3  # MsgHeartbeatResp
     z = np.zeros(S, np.uint64)
-    return be.step(t, z, z, z, read=(acks, ctx))
+    c = None
+    if ctx is not None:
+        c = np.zeros(S, np.uint32)
+        for s in slots:
+            c[s] = ctx[s] if isinstance(ctx, dict) else ctx
+    return be.step(t, z, z, z, ctx=c)
+
+
+QUEUED, RESPOND, POSTPONED, FULL = 3, 1, 2, 4
 
 
 def read_only_option_safe(be):
@@ -79,22 +95,21 @@ def read_only_option_safe(be):
     for want in wri:
         for _ in range(10):
             _propose(be, S, (1, 2))
-        req_index = be.committed()  # readOnly.addRequest(r.raftLog.committed, m)
-        out = _heartbeat_round(be, S, (1, 2), acks=0b001)
-        assert out["read_ok"] == 1, want
-        assert req_index == want
-        assert out["acks"] == 0b011, out["acks"]  # c's ack came after the release
+        res, ctx, index = be.read_index()
+        assert (res, index) == (QUEUED, want), (res, index, want)
+        assert be.queue()[0] == 1
+        out = _heartbeat_round(be, S, (1, 2))
+        assert out["read_released"] == 1, want
+        assert be.queue()[0] == 0
 
 
 def read_only_with_learner(be):
     """TestReadOnlyWithLearner (raft/raft_test.go:2231-2278): voters {1},
     learner {2}.  Ten proposals per round commit on the leader alone (the
-    learner's MsgAppResp advances its Match, not the quorum); the read is
-    released at committed = 11, 21, 31, 41.  The reference answers a
-    single-voter leader's ReadIndex at once (r.prs.IsSingleton,
-    raft.go:1079-1085, a host-side shortcut); on the device the same
-    release follows from the leader's own ack: VoteResult over Voters {1}
-    is already won when the learner's heartbeat response arrives."""
+    learner's MsgAppResp advances its Match, not the quorum); the leader is
+    the only voting member, so r.prs.IsSingleton() answers the read at once
+    at committed = 11, 21, 31, 41 (raft.go:1079-1085), without a heartbeat
+    round."""
     S = 2
     sc = _leader_after_hup(S)
     be.load(sc, initial_arrays(sc), inc=0b01)
@@ -103,25 +118,271 @@ def read_only_with_learner(be):
         for _ in range(10):
             _propose(be, S, (1,))
         assert be.committed() == want  # committed by the leader's own Match
-        out = _heartbeat_round(be, S, (1,), acks=0b01)
-        assert out["read_ok"] == 1 and be.committed() == want
+        res, _, index = be.read_index()
+        assert (res, index) == (RESPOND, want)
+        assert be.queue()[0] == 0
+
+
+def read_only_option_lease(be):
+    """TestReadOnlyOptionLease (raft/raft_test.go:2282-2337), leader a's
+    side: ReadOnlyLeaseBased answers at once at committed (11, ..., 61)."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    for want in [11, 21, 31, 41, 51, 61]:
+        for _ in range(10):
+            _propose(be, S, (1, 2))
+        res, _, index = be.read_index(lease_based=True)
+        assert (res, index) == (RESPOND, want)
+        assert be.queue()[0] == 0
+
+
+def raft_frees_read_only_mem(be):
+    """TestRaftFreesReadOnlyMem (raft/raft_test.go:1359-1403): peers {1,2},
+    the leader committed to its lastIndex; MsgReadIndex from 2 queues one
+    request (readIndexQueue and pendingReadIndex of length 1); the
+    heartbeat response from 2 carrying its context releases it and both
+    are empty again."""
+    S = 2
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    res, ctx, index = be.read_index()
+    assert (res, index) == (QUEUED, 1)
+    n, head, acks = be.queue()
+    assert (n, head) == (1, ctx) and acks == [0b01]  # the leader's own ack
+    out = _heartbeat_round(be, S, (1,), ctx=ctx)
+    assert out["read_released"] == 1
+    assert be.queue()[0] == 0
+
+
+def read_only_for_new_leader(be):
+    """TestReadOnlyForNewLeader (raft/raft_test.go:2341-2410), the leader's
+    side.  Node 1 (log [1@1, 2@1], committed 1) wins term 2 and appends its
+    empty entry 3@2; MsgApp is dropped, so nothing of term 2 commits and
+    the ReadIndex is postponed (raft.go:1087-1092).  After recover: the
+    heartbeat responses make the leader probe (sendAppend), a MsgProp
+    appends 4@2 (the peers are paused: nothing sent), the followers' accept
+    of [3, 4] commits 4 -- the first commit in the term -- and
+    releasePendingReadIndexMessages answers the postponed read at index 4
+    (windex): it is added to the queue at 4, and the heartbeat responses
+    carrying its context release it.  A second ReadIndex is queued at once."""
+    S = 3
+    sc = {"name": "", "S": S, "self": 0, "max_ents": 0,
+          "log": {"runs": [[0, 0], [1, 1], [3, 2]], "committed": 1, "term_start": 3,
+                  "first_index": 1, "last_index": 3},
+          # becomeLeader: reset() gives every Progress Match 0, Next =
+          # lastIndex + 1 = 3 before the empty entry; the leader's own
+          # Progress follows its appends (Replicate); bcastAppend's probes
+          # went out (ProbeSent) and were dropped
+          "peers": [_peer(3, 4, REPLICATE)] + [_peer(0, 3, 0, probe_sent=True)
+                                              for _ in range(S - 1)]}
+    be.load(sc, initial_arrays(sc))
+    res, _, _ = be.read_index()
+    assert res == POSTPONED
+    # recover; heartbeat responses (no read pending: no context) -> probes
+    out = _heartbeat_round(be, S, (1, 2))
+    assert bits(out["sent"]) == [1, 2] and out["term_commit"] == 0
+    be.append()  # MsgProp: 4@2; the followers are paused again
+    out = be.send(0b110, 1)
+    assert out["sent"] == 0
+    # the followers append [3, 4] and accept; slot 1's accept commits 4
+    t = np.array([0, 1, 1], np.uint8)
+    idx = np.array([0, 4, 4], np.uint64)
+    z = np.zeros(S, np.uint64)
+    out = be.step(t, idx, z, z)
+    assert be.committed() == 4
+    assert out["term_commit"] == 1 and out["term_commit_index"] == 4
+    # the postponed read: sendMsgReadIndexResponse -> addRequest(4)
+    res, ctx, index = be.read_index()
+    assert res == QUEUED and index == 4
+    out = _heartbeat_round(be, S, (1, 2), ctx=ctx)
+    assert out["read_released"] == 1 and out["term_commit"] == 0
+    # a new ReadIndex is accepted at once
+    res, ctx2, index = be.read_index()
+    assert res == QUEUED and index == 4 and ctx2 == ctx + 1
+    out = _heartbeat_round(be, S, (1, 2), ctx=ctx2)
+    assert out["read_released"] == 1
+
+
+def two_reads_in_flight(be):
+    """Two pending requests (derived from readOnly.advance, read_only.go:
+    81-112): a response carrying the older context releases only the older
+    one; a later response carrying a released context records nothing
+    (recvAck returns nil); a response carrying the newer context releases
+    the newer one.  Then two more: a quorum on the newer one releases both
+    at once (advance dequeues everything up to it)."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    _, a, _ = be.read_index()
+    _, b, _ = be.read_index()
+    assert b == a + 1 and be.queue()[0] == 2
+    out = _heartbeat_round(be, S, (1,), ctx=a)  # acks(a) = {1, 2}: a quorum
+    assert out["read_released"] == 1
+    n, head, acks = be.queue()
+    assert (n, head, acks) == (1, b, [0b001])
+    out = _heartbeat_round(be, S, (2,), ctx=a)  # a is gone: nothing recorded
+    assert out["read_released"] == 0 and be.queue() == (1, b, [0b001])
+    out = _heartbeat_round(be, S, (2,), ctx=b)
+    assert out["read_released"] == 1 and be.queue()[0] == 0
+    _, c, _ = be.read_index()
+    _, d, _ = be.read_index()
+    out = _heartbeat_round(be, S, (1,), ctx=c)  # one round: 1 acks c ...
+    assert out["read_released"] == 1
+    _, e, _ = be.read_index()
+    assert be.queue()[0] == 2  # d, e
+    # slot 1 carries e, slot 2 carries d; slots go in order, so slot 1's ack
+    # makes e's acks {1, 2} a quorum and advance releases d and e together;
+    # slot 2's response then finds d gone
+    out = _heartbeat_round(be, S, (1, 2), ctx={1: e, 2: d})
+    assert out["read_released"] == 2 and be.queue()[0] == 0
+
+
+def read_queue_full(be):
+    """The engine keeps QE_READ_QUEUE = 4 pending requests per group; a fifth
+    is refused (QE_RI_FULL, nothing changes) until a release makes room.
+    The reference's queue is unbounded (read_only.go:56-63): this is the
+    engine's limit, reported, never silent."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    ctxs = [be.read_index()[1] for _ in range(4)]
+    assert ctxs == list(range(ctxs[0], ctxs[0] + 4))
+    res, _, _ = be.read_index()
+    assert res == FULL and be.queue()[0] == 4
+    out = _heartbeat_round(be, S, (2,))  # the newest context: releases all 4
+    assert out["read_released"] == 4
+    assert be.read_index()[0] == QUEUED
 
 
 def learner_ack_does_not_count(be):
     """Derived from TestReadOnlyWithLearner's rule that learners never count
     (VoteResult ranges over Voters only, raft.go:1300): voters {1,2},
-    learner {3}; the learner's ack alone leaves the request pending, the
-    voter's ack releases it; a response without the context
-    (len(m.Context) == 0) is not an ack."""
+    learner {3}; the learner's ack alone leaves the request pending, a
+    response without a context (len(m.Context) == 0) is not an ack, the
+    voter's ack releases it."""
     S = 3
     sc = _leader_after_hup(S)
     be.load(sc, initial_arrays(sc), inc=0b011)
-    out = _heartbeat_round(be, S, (2,), acks=0b001)
-    assert out["read_ok"] == 0 and out["acks"] == 0b101
-    out = _heartbeat_round(be, S, (1,), acks=0b101, ctx=0b000)  # no context
-    assert out["read_ok"] == 0 and out["acks"] == 0b101
-    out = _heartbeat_round(be, S, (1,), acks=0b101)
-    assert out["read_ok"] == 1 and out["acks"] == 0b111
+    res, ctx, _ = be.read_index()
+    assert res == QUEUED
+    out = _heartbeat_round(be, S, (2,), ctx=ctx)
+    assert out["read_released"] == 0 and be.queue()[2] == [0b101]
+    out = _heartbeat_round(be, S, (1,), ctx=0)  # no context
+    assert out["read_released"] == 0 and be.queue()[2] == [0b101]
+    out = _heartbeat_round(be, S, (1,), ctx=ctx)
+    assert out["read_released"] == 1
+
+
+def _transfer(be, S, slot):
+    t = np.zeros(S, np.uint8)
+    t[slot] = 7  # MsgTransferLeader from node slot+1
+    z = np.zeros(S, np.uint64)
+    return be.step(t, z, z, z)
+
+
+def leader_transfer_to_up_to_date_node(be):
+    """TestLeaderTransferToUpToDateNode (raft/raft_test.go:3435-3456), the
+    leader's side: node 2 is caught up (Match == lastIndex), so the leader
+    records it as leadTransferee and sends MsgTimeoutNow at once
+    (raft.go:1363-1366), no MsgApp."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    out = _transfer(be, S, 1)
+    assert bits(out["timeout_now"]) == [1] and out["sent"] == 0
+    assert be.transferee() == 1
+
+
+def leader_transfer_to_slow_follower(be):
+    """TestLeaderTransferToSlowFollower (raft/raft_test.go:3523-3541), the
+    leader's side: node 3 was isolated during a proposal (Match 1, its
+    MsgApp for entry 2 lost: Replicate, Next 3, one inflight); the transfer
+    to 3 sends an append instead (raft.go:1367-1369); node 3 rejects it,
+    the leader probes from its Match, node 3's accept of 2 brings its Match
+    to lastIndex and the leader sends MsgTimeoutNow (raft.go:1278-1281)."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    _propose(be, S, (1,))  # node 3 isolated: its MsgApp is lost
+    z = np.zeros(S, np.uint64)
+    out = _transfer(be, S, 2)
+    assert be.transferee() == 2
+    assert out["timeout_now"] == 0 and bits(out["sent"]) == [2]
+    t = np.array([0, 0, 2], np.uint8)  # reject of Index 2, hint 1
+    out = be.step(t, np.array([0, 0, 2], np.uint64), np.array([0, 0, 1], np.uint64), z)
+    assert bits(out["sent"]) == [2] and out["timeout_now"] == 0
+    out = be.step(np.array([0, 0, 1], np.uint8), np.array([0, 0, 2], np.uint64), z, z)
+    assert bits(out["timeout_now"]) == [2]
+
+
+def leader_transfer_to_self(be):
+    """TestLeaderTransferToSelf (raft/raft_test.go:3589-3598): a transfer to
+    the leader itself is a no-op (raft.go:1355-1358)."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    out = _transfer(be, S, 0)
+    assert out["timeout_now"] == 0 and out["sent"] == 0 and be.transferee() == 0xFF
+
+
+def leader_transfer_to_non_existing_node(be):
+    """TestLeaderTransferToNonExistingNode (raft/raft_test.go:3600-3608): a
+    request from a node without a Progress is dropped (raft.go:1100-1104);
+    slot 3 holds no Progress here."""
+    S = 4
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc), tracked=0b0111, inc=0b0111)
+    out = _transfer(be, S, 3)
+    assert out["timeout_now"] == 0 and out["sent"] == 0 and be.transferee() == 0xFF
+
+
+def leader_transfer_second_to_another_node(be):
+    """TestLeaderTransferSecondTransferToAnotherNode (raft/raft_test.go:
+    3754-3771): node 3 isolated (but caught up: MsgTimeoutNow is sent and
+    lost), then a transfer to 2 aborts it (raft.go:1346-1353) and goes to 2."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    out = _transfer(be, S, 2)
+    assert bits(out["timeout_now"]) == [2] and be.transferee() == 2
+    out = _transfer(be, S, 1)
+    assert bits(out["timeout_now"]) == [1] and be.transferee() == 1
+
+
+def leader_transfer_second_to_same_node(be):
+    """TestLeaderTransferSecondTransferToSameNode (raft/raft_test.go:
+    3775-3799): a second request for the transfer in progress is ignored
+    (raft.go:1347-1350): no MsgTimeoutNow, no MsgApp, leadTransferee kept."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    _transfer(be, S, 2)
+    out = _transfer(be, S, 2)
+    assert out["timeout_now"] == 0 and out["sent"] == 0 and be.transferee() == 2
+
+
+def leader_transfer_back(be):
+    """TestLeaderTransferBack (raft/raft_test.go:3733-3750): with a transfer
+    to 3 pending, a transfer to the leader itself aborts it
+    (abortLeaderTransfer, raft.go:1352) and is then ignored: no transfer is
+    left in progress."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc))
+    _transfer(be, S, 2)
+    out = _transfer(be, S, 0)
+    assert be.transferee() == 0xFF and out["timeout_now"] == 0 and out["sent"] == 0
+
+
+def leader_transfer_learner_ignored(be):
+    """Derived from raft.go:1340-1343: a learner's MsgTransferLeader is
+    ignored (voters {1,2}, learner {3})."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc), inc=0b011)
+    out = _transfer(be, S, 2)
+    assert out["timeout_now"] == 0 and out["sent"] == 0 and be.transferee() == 0xFF
 
 
 def _stepdown_run(be, heartbeats):
@@ -187,40 +448,58 @@ def add_node_check_quorum(be):
     assert qa == 0, (qa, ra)  # steps down
 
 
-SCENARIOS = [read_only_option_safe, read_only_with_learner, learner_ack_does_not_count,
+SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lease,
+             raft_frees_read_only_mem, read_only_for_new_leader, two_reads_in_flight,
+             read_queue_full, learner_ack_does_not_count,
              leader_stepdown_when_quorum_active, leader_stepdown_when_quorum_lost,
-             add_node_check_quorum]
+             add_node_check_quorum, leader_transfer_to_up_to_date_node,
+             leader_transfer_to_slow_follower, leader_transfer_to_self,
+             leader_transfer_to_non_existing_node, leader_transfer_second_to_another_node,
+             leader_transfer_second_to_same_node, leader_transfer_back,
+             leader_transfer_learner_ignored]
 
 
 class OracleRoundBackend:
     """The oracle (oracle/quorum_oracle.c) over one group, with the ReadIndex
-    and CheckQuorum entry points."""
+    queue, qe_read_index and CheckQuorum entry points."""
 
     def __init__(self, orc):
         self.orc = orc
 
-    def load(self, sc, a, inc=None):
+    def load(self, sc, a, inc=None, tracked=None):
         S = sc["S"]
         pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
         a = dict(a)
         pb.pw = self.orc.pack_word(a.pop("flags"), 0, a.pop("icount"))
         for k, v in a.items():
             setattr(pb, k, v.copy())
+        md = self.orc.mask_dtype(S)
         if inc is not None:
-            pb.inc = np.array([inc], self.orc.mask_dtype(S))
+            pb.inc = np.array([inc], md)
+        if tracked is not None:
+            pb.tracked = np.array([tracked], md)
+        pb.track_reads()
         self.pb, self.sc = pb, sc
 
-    def step(self, t, idx, hint, lt, read=None):
-        md = self.orc.mask_dtype(self.sc["S"])
-        acks = ctx = None
-        if read is not None:
-            acks = np.array([read[0]], md)
-            ctx = None if read[1] is None else np.array([read[1]], md)
-        o = self.orc.progress_step(self.pb, t, idx, hint, lt, read_acks=acks, read_ctx=ctx)
-        out = {"sent": o.sent[0], "bcast": o.bcast[0]}
-        if read is not None:
-            out["read_ok"], out["acks"] = int(o.read_ok[0]), int(acks[0])
-        return out
+    def step(self, t, idx, hint, lt, ctx=None):
+        o = self.orc.progress_step(self.pb, t, idx, hint, lt, read_ctx=ctx)
+        return {"sent": o.sent[0], "bcast": o.bcast[0], "timeout_now": o.timeout_now[0],
+                "read_released": int(o.read_released[0]), "term_commit": int(o.term_commit[0]),
+                "term_commit_index": int(o.term_commit_index[0])}
+
+    def read_index(self, lease_based=False):
+        r, c, i = self.orc.read_index(self.pb, np.ones(1, np.uint8), lease_based)
+        return int(r[0]), int(c[0]), int(i[0])
+
+    def queue(self):
+        pb = self.pb
+        n, head = int(pb.read_count[0]), int(pb.read_head[0])
+        mb = 1 if self.sc["S"] <= 8 else 2
+        w = int(pb.read_acks[0])
+        return n, head, [(w >> (8 * mb * j)) & ((1 << (8 * mb)) - 1) for j in range(n)]
+
+    def transferee(self):
+        return int(self.pb.lead_transferee[0])
 
     def send(self, want, sei):
         w = np.array([want], self.orc.mask_dtype(self.sc["S"]))

@@ -28,7 +28,8 @@ def test_header_declares_expected_surface():
               "qe_stats_reduce", "qe_gen_groups", "qe_abi_version", "qe_strerror",
               "qe_mask_bytes", "qe_tune", "qe_allreduce_stats", "qe_comm_init",
               "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes", "qe_check_quorum",
-              "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange"]:
+              "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange",
+              "qe_read_index"]:
         assert f in fns
 
 
@@ -60,10 +61,11 @@ int main(void) {
   F(qe_confstate_csr, auto_leave) F(qe_confstate_csr, perm)
   Z(qe_progress) F(qe_progress, peer) F(qe_progress, infl_lo) F(qe_progress, infl_hi) F(qe_progress, log_runs)
   F(qe_progress, out_mask) F(qe_progress, tracked) F(qe_progress, snap_index)
-  F(qe_progress, max_ents)
+  F(qe_progress, max_ents) F(qe_progress, read_acks) F(qe_progress, read_head)
+  F(qe_progress, read_count) F(qe_progress, lead_transferee)
   Z(qe_peer_msgs) F(qe_peer_msgs, bcast) F(qe_peer_msgs, timeout_now) F(qe_peer_msgs, msg_index)
-  F(qe_peer_msgs, bytes_requested) F(qe_peer_msgs, read_acks) F(qe_peer_msgs, read_ctx)
-  F(qe_peer_msgs, read_ok)
+  F(qe_peer_msgs, bytes_requested) F(qe_peer_msgs, read_ctx) F(qe_peer_msgs, read_released)
+  F(qe_peer_msgs, term_commit) F(qe_peer_msgs, term_commit_index)
   Z(qe_conf) F(qe_conf, slot_ids) F(qe_conf, tracked) F(qe_conf, auto_leave)
   Z(qe_conf_changes) F(qe_conf_changes, stride) F(qe_conf_changes, node_id)
   F(qe_conf_changes, new_progress)
@@ -96,7 +98,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 4
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 5
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0
@@ -106,7 +108,9 @@ def test_constants_and_introspection():
     for name, val in [("QE_VOTE_PENDING", 1), ("QE_VOTE_LOST", 2), ("QE_VOTE_WON", 3),
                       ("QE_STATS_COUNTERS", 16), ("QE_STATS_SHARDS", 64), ("QE_EINVAL", -22),
                       ("QE_PF_RECENT_ACTIVE", 8), ("QE_PW_START_SHIFT", 8),
-                      ("QE_PW_COUNT_SHIFT", 16), ("QE_PF_RING_WIDE", 16)]:
+                      ("QE_PW_COUNT_SHIFT", 16), ("QE_PF_RING_WIDE", 16),
+                      ("QE_MSG_TRANSFER_LEADER", 7), ("QE_READ_QUEUE", 4), ("QE_RI_RESPOND", 1),
+                      ("QE_RI_POSTPONED", 2), ("QE_RI_QUEUED", 3), ("QE_RI_FULL", 4)]:
         m = re.search(rf"#define {name} \(?(-?\d+)u?\)?", src)
         assert m and int(m.group(1)) == val, name
 
@@ -141,6 +145,21 @@ def test_argument_errors_without_gpu():
     assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_EINVAL
     pr = _lib.QeProgress(num_groups=0, num_slots=3)  # empty batch is a no-op
     assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_OK
+    assert L.qe_read_index(C.byref(pr), None, 0, None, None, None, None) == _lib.QE_OK
+    assert L.qe_read_index(None, None, 0, None, None, None, None) == _lib.QE_EINVAL
+    v = C.c_void_p(64)
+    pr = _lib.QeProgress(num_groups=4, num_slots=3, inflight_cap=4, stride=4, committed=v,
+                         term_start=v, last_index=v)
+    # ReadOnlySafe needs the queue; LeaseBased does not
+    assert L.qe_read_index(C.byref(pr), v, 0, v, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_read_index(C.byref(pr), None, 1, v, None, None, None) == _lib.QE_EINVAL
+    # a queue comes whole or not at all (qe_progress_step)
+    pr = _lib.QeProgress(num_groups=4, num_slots=3, inflight_cap=4, stride=4, log_runs=1,
+                         match=v, next=v, pending_snapshot=v, peer=v, infl_lo=v, infl_hi=v,
+                         committed=v, term_start=v, first_index=v, last_index=v, run_first=v,
+                         run_term=v, run_count=v, read_acks=v)
+    m = _lib.QePeerMsgs(type=v, index=v, reject_hint=v, log_term=v)
+    assert L.qe_progress_step(C.byref(pr), C.byref(m), None, None) == _lib.QE_EINVAL
     assert L.qe_confchange(None, None, None, None) == _lib.QE_EINVAL
     cf = _lib.QeConf(num_groups=4, num_slots=17)
     assert L.qe_confchange(C.byref(cf), C.byref(_lib.QeConfChanges()), None, None) == _lib.QE_EINVAL

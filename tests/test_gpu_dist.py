@@ -27,7 +27,8 @@ def _bench(args, env_extra):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("workload", ["config2_n5", "config5_prevote_cq", "progress_step"])
+@pytest.mark.parametrize("workload", ["config2_n5", "config4_repl", "config5_prevote_cq",
+                                      "progress_step"])
 def test_two_ranks_equal_one_process_over_the_union(workload):
     G = 1 << 18
     common = ["--workload", workload, "--no-aux", "--no-cpu-baseline", "--steps", "3",

@@ -19,6 +19,7 @@ from tests.test_progress_oracle import log_runs
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 EXTRAS = ("tracked", "self_slot", "lead_transferee", "snap_index")
+READS = EXTRAS + ("reads",)
 
 
 @pytest.fixture(scope="module")
@@ -94,7 +95,7 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0, base=0):
 
 def random_msgs(rng, pb):
     n = pb.S * pb.G
-    mtype = rng.integers(0, 8, n).astype(np.uint8)  # 7 = unknown kind -> ignored
+    mtype = rng.integers(0, 9, n).astype(np.uint8)  # 8 = unknown kind -> ignored
     li = np.tile(pb.last_index, pb.S)
     lo = np.uint64(getattr(pb, "base", 0))
     mindex = np.where(rng.random(n) < 0.5, pb.next - 1,
@@ -107,12 +108,15 @@ def random_msgs(rng, pb):
 def to_device(eng, pb, masks, extras=()):
     ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride,
                            extras=extras, max_ents=pb.max_ents)
+    md = orc.mask_dtype(pb.S)
     ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, peer=pb.pw,
                  ibuf=pb.ibuf, committed=pb.committed,
                  term_start=pb.term_start, first_index=pb.first_index, last_index=pb.last_index,
                  run_first=pb.run_first, run_term=pb.run_term, run_count=pb.run_count,
                  inc=pb.inc, out=pb.out, tracked=pb.tracked, self_slot=pb.self_slot,
-                 lead_transferee=pb.lead_transferee, snap_index=pb.snap_index)
+                 lead_transferee=pb.lead_transferee, snap_index=pb.snap_index,
+                 read_acks=None if pb.read_acks is None else pb.read_acks.view(md),
+                 read_head=pb.read_head, read_count=pb.read_count)
     return ps
 
 
@@ -135,6 +139,14 @@ def assert_same(ps, pb):
     h = ps.host()
     for k in ("match", "next", "pending", "committed"):
         np.testing.assert_array_equal(h[k], getattr(pb, k), err_msg=k)
+    if pb.lead_transferee is not None:
+        np.testing.assert_array_equal(h["lead_transferee"], pb.lead_transferee,
+                                      err_msg="lead_transferee")
+    if pb.read_acks is not None:  # the ReadIndex queue (ABI 5), raw words
+        np.testing.assert_array_equal(h["read_acks"], pb.read_acks.view(orc.mask_dtype(pb.S)),
+                                      err_msg="read_acks")
+        np.testing.assert_array_equal(h["read_head"], pb.read_head, err_msg="read_head")
+        np.testing.assert_array_equal(h["read_count"], pb.read_count, err_msg="read_count")
     np.testing.assert_array_equal(h["peer"] & ~RING_MASK, pb.pw, err_msg="packed peer words")
     live = live_entries(pb.pw, pb.S, pb.F, pb.stride)
     np.testing.assert_array_equal(h["ibuf"][live], pb.ibuf[live], err_msg="live ring entries")
@@ -163,57 +175,92 @@ def assert_outputs(msgs, o, S):
     np.testing.assert_array_equal(cnt, o.msg_count, err_msg="msg_count")
     got_ix = msgs.msg_index.cpu().numpy().view(np.uint64)
     np.testing.assert_array_equal(got_ix[cnt > 0], o.msg_index[cnt > 0], err_msg="msg_index")
+    np.testing.assert_array_equal(msgs.read_released.cpu().numpy(), o.read_released,
+                                  err_msg="read_released")
+    tc = msgs.term_commit.cpu().numpy()
+    np.testing.assert_array_equal(tc, o.term_commit, err_msg="term_commit")
+    tci = msgs.term_commit_index.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(tci[tc > 0], o.term_commit_index[tc > 0],
+                                  err_msg="term_commit_index")
 
 
-def random_reads(rng, pb):
-    """A pending ReadIndex request per group (70 %): the leader's own ack or
-    a random subset, and the heartbeat responses carrying its context."""
-    md = orc.mask_dtype(pb.S)
-    acks = rng.integers(0, 1 << pb.S, pb.G).astype(md)
-    acks[rng.random(pb.G) < 0.5] = 1
-    ctx = rng.integers(0, 1 << pb.S, pb.G).astype(md)
-    ctx[rng.random(pb.G) < 0.3] = (1 << pb.S) - 1
-    return acks, ctx
+def random_queue(rng, pb):
+    """A random ReadIndex queue per group (ABI 5): 0..4 pending requests with
+    random acks (dead entries hold garbage), context numbers from near 1 to
+    near 2^32."""
+    pb.track_reads()
+    G = pb.G
+    pb.read_count[:] = rng.integers(0, 5, G)
+    pb.read_head[:] = np.where(rng.random(G) < 0.8, rng.integers(1, 50, G),
+                               rng.integers(1, 1 << 32, G, dtype=np.uint64)).astype(np.uint32)
+    wbits = 32 if pb.S <= 8 else 64
+    pb.read_acks[:] = rng.integers(0, 1 << 62, G, dtype=np.uint64).astype(
+        np.uint32 if wbits == 32 else np.uint64)
+
+
+def random_read_ctx(rng, pb):
+    """The context numbers heartbeat responses carry: none, a pending
+    request's (any), a released or not-yet-assigned one, or garbage."""
+    n = pb.S * pb.G
+    head = np.tile(pb.read_head, pb.S).astype(np.int64)
+    cnt = np.tile(pb.read_count, pb.S).astype(np.int64)
+    pick = rng.integers(0, 4, n)
+    off = rng.integers(-2, 6, n)
+    ctx = np.where(pick == 0, 0, np.where(pick == 3, rng.integers(0, 1 << 32, n),
+                                           head + np.where(pick == 1, rng.integers(0, 4, n) % np.maximum(cnt, 1), off)))
+    return (ctx & 0xFFFFFFFF).astype(np.uint32)
 
 
 CASES = [(1, (), ()), (3, (), EXTRAS), (5, (), ()), (5, (), EXTRAS), (5, ("inc",), EXTRAS),
          (7, ("inc", "out"), EXTRAS), (10, ("inc", "out"), ()), (16, ("inc",), EXTRAS)]
 
 
-@pytest.mark.parametrize("F", [8, 32])
+@pytest.mark.parametrize("F", [3, 5, 8, 32])
 @pytest.mark.parametrize("R", [3, 6])
 @pytest.mark.parametrize("S,masks,extras", CASES)
 def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
     """Random states and the full message mix (rejects with LogTerm > 0,
-    snapshots, heartbeats with ReadIndex acks, ...) through the 4-run (R = 3,
-    the production kernel) and 8-run (R = 6) kernels, row-resident (F = 8)
-    and memory (F = 32) rings.  Odd rounds run the instrumented variant,
-    whose byte count must equal the oracle's exactly."""
+    snapshots, heartbeats carrying ReadIndex contexts against a random
+    queue, MsgTransferLeader, ...) through the 4-run (R = 3, the production
+    kernel) and 8-run (R = 6) kernels; row-resident rings of one 16-byte
+    access (F = 3), padded pitch (F = 5) and two accesses (F = 8), and
+    memory rings (F = 32).  Odd rounds run the instrumented variant, whose
+    byte count must equal the oracle's exactly."""
     rng = np.random.default_rng(100 + S + 7 * len(extras) + 31 * R + F)
     G = 3001
     pb = random_state(rng, G, S, F, R, masks, extras, max_ents=int(rng.integers(0, 4)))
-    ps = to_device(eng, pb, masks, extras)
+    reads = "lead_transferee" in extras  # the ReadIndex queue with the full extras
+    if reads:
+        random_queue(rng, pb)
+    ps = to_device(eng, pb, masks, extras + (("reads",) if reads else ()))
     md = orc.mask_dtype(S)
     for rnd in range(6):
         mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
         msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
-        acks = ctx = None
-        if rnd % 3 != 2:
-            acks, ctx = random_reads(rng, pb)
-            msgs.track_reads(ps, acks.copy(), ctx if rnd % 3 == 0 else None)
+        ctx = None
+        if reads and rnd % 3 != 2:  # every third round: the newest-context default
+            ctx = random_read_ctx(rng, pb)
+            msgs.set_read_ctx(ps, ctx)
+        if reads and rnd == 3:  # new requests (qe_read_index) between rounds
+            req = (rng.random(G) < 0.6).astype(np.uint8)
+            lease = bool(rng.integers(0, 2))
+            r_g, c_g, i_g = eng.read_index(ps, torch.from_numpy(req).to(DEV), lease)
+            r_o, c_o, i_o = orc.read_index(pb, req, lease)
+            np.testing.assert_array_equal(r_g.cpu().numpy(), r_o)
+            q = r_o == 3
+            np.testing.assert_array_equal(c_g.cpu().numpy().view(np.uint32)[q], c_o[q])
+            w = (r_o == 1) | q
+            np.testing.assert_array_equal(i_g.cpu().numpy().view(np.uint64)[w], i_o[w])
+            assert_same(ps, pb)
         stats = eng.stats_buffer(DEV)
         if rnd % 2:
             msgs.bytes_requested = torch.zeros(1, dtype=torch.int64, device=DEV)
         eng.progress_step(ps, msgs, stats)
         got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
-        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, read_acks=acks,
-                              read_ctx=ctx if rnd % 3 == 0 else None, count_bytes=True)
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, read_ctx=ctx, count_bytes=True)
         assert_same(ps, pb)
         assert_outputs(msgs, o, S)
         np.testing.assert_array_equal(got, o.stats)
-        if acks is not None:
-            np.testing.assert_array_equal(msgs.read_acks.cpu().numpy().view(md), acks)
-            np.testing.assert_array_equal(msgs.read_ok.cpu().numpy(), o.read_ok)
         if rnd % 2:
             assert int(msgs.bytes_requested.item()) == int(o.bytes[0]), (rnd, S)
         # a sendAppend / bcastAppend round to random peers
@@ -236,7 +283,7 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
             assert_same(ps, pb)
 
 
-@pytest.mark.parametrize("F", [8, 32])
+@pytest.mark.parametrize("F", [3, 5, 8, 32])
 @pytest.mark.parametrize("base", [(1 << 32) - 37, (1 << 43) - 29, 3 * (1 << 44) + 11])
 def test_progress_rings_across_epochs(eng, base, F):
     """ABI 4's 32-bit ring words with every log index shifted by `base`:
@@ -320,17 +367,21 @@ def test_progress_long_rings_and_bcasts(eng):
 
 
 class GpuBackend:
-    """tests/progress_scenarios.py backend over the HIP engine (one group)."""
+    """tests/progress_scenarios.py / leader_round_scenarios.py backend over
+    the HIP engine (one group)."""
 
     def __init__(self, eng):
         self.eng = eng
 
-    def load(self, sc, a, inc=None):
+    def load(self, sc, a, inc=None, tracked=None):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
         ps = self.eng.ProgressState(1, sc["S"], cap(sc), len(sc["log"]["runs"]), DEV, stride=1,
-                                    extras=EXTRAS, max_ents=sc["max_ents"],
+                                    extras=READS, max_ents=sc["max_ents"],
                                     masks=("inc",) if inc is not None else ())
-        ps.tracked = None  # every slot holds a Progress (as the oracle backend)
+        if tracked is None:
+            ps.tracked = None  # every slot holds a Progress (as the oracle backend)
+        else:
+            ps.tracked.fill_(tracked)
         if "snap_index" not in a:
             ps.snap_index = None
         ps.load_host(**a)
@@ -338,23 +389,33 @@ class GpuBackend:
             ps.inc.fill_(inc)
         self.ps, self.sc = ps, sc
 
-    def step(self, t, idx, hint, lt, read=None):
+    def step(self, t, idx, hint, lt, ctx=None):
         msgs = load_msgs(self.eng, self.ps, t, idx, hint, lt)
-        md = orc.mask_dtype(self.sc["S"])
-        if read is not None:
-            msgs.track_reads(self.ps, np.array([read[0]], md),
-                             None if read[1] is None else np.array([read[1]], md))
+        msgs.set_read_ctx(self.ps, ctx)
         self.eng.progress_step(self.ps, msgs)
-        out = {"sent": int(msgs.sent[0]), "snap": int(msgs.snap[0]),
-               "timeout_now": int(msgs.timeout_now[0]),
-               "msg_count": msgs.msg_count.cpu().numpy()[: self.sc["S"] * self.ps.stride: self.ps.stride],
-               "msg_index": msgs.msg_index.cpu().numpy().view(np.uint64)[
-                   : self.sc["S"] * self.ps.stride: self.ps.stride],
-               "bcast": int(msgs.bcast[0])}
-        if read is not None:
-            out["read_ok"] = int(msgs.read_ok[0])
-            out["acks"] = int(msgs.read_acks[0]) & ((1 << self.sc["S"]) - 1)
-        return out
+        st = self.ps.stride
+        return {"sent": int(msgs.sent[0]), "snap": int(msgs.snap[0]),
+                "timeout_now": int(msgs.timeout_now[0]),
+                "msg_count": msgs.msg_count.cpu().numpy()[: self.sc["S"] * st: st],
+                "msg_index": msgs.msg_index.cpu().numpy().view(np.uint64)[: self.sc["S"] * st: st],
+                "bcast": int(msgs.bcast[0]), "read_released": int(msgs.read_released[0]),
+                "term_commit": int(msgs.term_commit[0]),
+                "term_commit_index": int(msgs.term_commit_index[0])}
+
+    def read_index(self, lease_based=False):
+        req = torch.ones(1, dtype=torch.uint8, device=DEV)
+        r, c, i = self.eng.read_index(self.ps, req, lease_based)
+        return int(r[0]), int(c[0]) & 0xFFFFFFFF, int(i[0])
+
+    def queue(self):
+        ps = self.ps
+        n, head = int(ps.read_count[0]), int(ps.read_head[0]) & 0xFFFFFFFF
+        mask = (1 << self.sc["S"]) - 1
+        acks = [int(ps.read_acks[j]) & 0xFFFF for j in range(n)]
+        return n, head, [a & 0xFFFF if self.sc["S"] > 8 else a & 0xFF for a in acks]
+
+    def transferee(self):
+        return int(self.ps.lead_transferee[0])
 
     def send(self, want, sei):
         dt = torch.uint8 if self.sc["S"] <= 8 else torch.int16
@@ -398,11 +459,12 @@ def test_progress_scenarios_on_gpu(eng):
 
 
 def test_readindex_and_checkquorum_scenarios_on_gpu(eng):
-    """TestReadOnlyOptionSafe (raft_test.go:2177), TestReadOnlyWithLearner
-    (:2231) and the learner-ack rule through qe_progress_step's heartbeat
-    ReadIndex acks; TestLeaderStepdownWhenQuorumActive / ...Lost
-    (:1748-1781) through qe_progress_step heartbeats chained into
-    qe_check_quorum (tests/leader_round_scenarios.py)."""
+    """ReadIndex through qe_read_index and qe_progress_step's queue
+    (TestReadOnlyOptionSafe / WithLearner / OptionLease, TestRaftFreesReadOnlyMem,
+    TestReadOnlyForNewLeader, two requests in flight, the queue limit, the
+    learner-ack rule), CheckQuorum (TestLeaderStepdownWhenQuorumActive /
+    Lost, TestAddNodeCheckQuorum) and MsgTransferLeader (TestLeaderTransfer*)
+    -- tests/leader_round_scenarios.py."""
     from tests.leader_round_scenarios import SCENARIOS
     for sc in SCENARIOS:
         sc(GpuBackend(eng))
@@ -454,9 +516,11 @@ def test_bytes_requested_equal_oracle_on_bench_state(eng):
     mindex, mhint, mlogterm = (t.cpu().numpy().view(np.uint64) for t in mix)
     b = eng.progress_bytes_requested(ps, msgs)
     o = orc.StepOut(pb)
-    m = orc.OrcMsgs(orc.P(mtype), orc.P(mindex), orc.P(mhint), orc.P(mlogterm), orc.P(o.sent),
-                    orc.P(o.bcast), None, None, orc.P(o.msg_count), orc.P(o.msg_index), None,
-                    None, None, orc.P(o.bytes))
+    m = orc.OrcMsgs(type=orc.P(mtype), index=orc.P(mindex), hint=orc.P(mhint),
+                    logterm=orc.P(mlogterm), sent=orc.P(o.sent), bcast=orc.P(o.bcast),
+                    msg_count=orc.P(o.msg_count), msg_index=orc.P(o.msg_index),
+                    read_released=orc.P(o.read_released), term_commit=orc.P(o.term_commit),
+                    term_commit_index=orc.P(o.term_commit_index), bytes=orc.P(o.bytes))
     import ctypes as C
     orc.lib().orc_progress_step_batch(C.byref(pb.struct()), C.byref(m), orc.P(o.stats), 0)
     assert_same(ps, pb)
@@ -556,7 +620,8 @@ def test_bytes_requested_accounting(eng):
     ps = to_device(eng, pb, ())
     mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
     msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
-    for k in ("sent", "bcast", "snap", "timeout_now", "msg_count", "msg_index"):
+    for k in ("sent", "bcast", "snap", "timeout_now", "msg_count", "msg_index", "read_released",
+              "term_commit", "term_commit_index"):
         setattr(msgs, k, None)
     b = eng.progress_bytes_requested(ps, msgs)
     o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, outputs=False, count_bytes=True)
