@@ -71,6 +71,11 @@ WORKLOADS = {
     "progress_step": ("16M groups x 5 peers: one round of MsgAppResp accept/reject + "
                       "MsgHeartbeatResp through the full Progress state machine "
                       "(inflights F=8, leader-log model R=4)", 1 << 24, 5, "progress"),
+    "progress_step_n7": ("16M groups x 7 peers: the progress_step round with 6 followers "
+                         "(BASELINE config 2's 7-voter shape)", 1 << 24, 7, "progress"),
+    "progress_step_joint": ("16M groups x joint 5+5 over 6 slots (one voter replaced: C_old "
+                            "{0,1,2,3,4}, C_new {0,1,2,3,5}): the progress_step round, commits "
+                            "need both halves", 1 << 24, 6, "progress_joint"),
     "progress_send": ("16M groups x bcastAppend after a proposal (qe_progress_send to the 4 "
                       "followers, StateReplicate, Inflights F=8 with room): one MsgApp and one "
                       "ring entry per peer", 1 << 24, 5, "psend"),
@@ -489,10 +494,14 @@ def setup(name, G, S, kind, d, stats):
         # HBM bytes per group-step: state in+out / steps (register-resident)
         bpg = (8 + 1 + 1 + 1 + 1 + 1 + 8 + 1 + 1 + 1) / steps_per_launch
         return step, bpg, G * steps_per_launch, "group-steps", {"b": b, "est": est}
-    if kind == "progress":
+    if kind in ("progress", "progress_joint"):
         F, R, ME = 8, int(os.environ.get("QE_BENCH_RUNS", "4")), 16  # R: A/B knob only
+        joint = kind == "progress_joint"
         ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff, extras=("self_slot",),
-                                  max_ents=ME)
+                                  max_ents=ME, masks=("inc", "out") if joint else ())
+        if joint:  # EnterJoint of a one-voter replacement, as config4_repl_joint
+            ps.inc.fill_(0b101111)
+            ps.out.fill_(0b011111)
         msgs = engine.PeerMsgs(ps)
         msgs.snap = msgs.timeout_now = None  # no snapshots / transfers in this workload
         # no ReadIndex in this workload (heartbeat rounds carry it); the
@@ -851,7 +860,7 @@ def run_workload(name, args, d, steps, warmup):
     del keep
     torch.cuda.empty_cache()
     extra = {}
-    if kind in ("elec", "elec_pvcq", "progress"):
+    if kind in ("elec", "elec_pvcq", "progress", "progress_joint"):
         rv = valu_roofline(name, kern_avg, units)
         if rv:
             extra["roofline_valu"] = rv

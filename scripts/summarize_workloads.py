@@ -10,14 +10,21 @@ into the committed evidence:
                                          VALU instructions per launch
 
 HBM bytes (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are KiB.
-FETCH_SIZE counts each memory-side read request as 64 B; gfx950's wide
-coalesced streams issue 128-B requests, so for the streaming kernels
-(k_cv_stream, k_repl_stream) the read bytes are 2 x FETCH_SIZE, calibrated
-in round 1 (2 x FETCH_SIZE = algorithmic reads within 0.01 %).  Kernels
-whose reads are mostly narrow or scattered (Progress step: 8-B Inflights
-rows, byte loads; election) issue 64-B requests and read
-FETCH_SIZE x 1 (checked for the Progress step against its access
-inventory).  usage: summarize_workloads.py <tag> [dir]
+Calibrated on this box's own access widths (scripts/pmc_calib.hip,
+profiles/r04/pmc_calib.json): FETCH_SIZE reports exactly half of the bytes
+a read moves from memory for every row width the engine uses (1, 2, 4, 8
+and 16 B per lane: x2.000).  A row read at half density (every other u64,
+or 16 B of each lane's 32-B ring) still moves every sector it touches:
+FETCH_SIZE then equals the bytes the lanes asked for, which is half of the
+sectors moved -- x2 again for the memory-side bytes.  So every kernel's
+read traffic is 2 x FETCH_SIZE.  WRITE_SIZE counts whole 32-B sectors: exact for full rows
+(x1.000 for 4-, 8-, 16-B lanes), 32 B for a 4-B append into a lane's
+32-B ring (x0.125) and for 16 B of it (x0.5) -- it is the memory-side
+write traffic as is.  (Rounds 1-3 used x1 for the narrow-access kernels,
+which undercounted their reads by half; check_quorum's figure fell below
+its algorithmic bytes.)  usage: summarize_workloads.py <tag> [dir] [bench.log]:
+with a bench JSON line, every workload's traffic is checked against its
+algorithmic bytes (units x bytes_per_unit) and a figure below it is refused.
 """
 import csv
 import glob
@@ -28,7 +35,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# workload -> (kernel-name prefix of the dominant kernel, FETCH_SIZE factor)
+# workload -> (kernel-name prefix of the dominant kernel, FETCH_SIZE factor:
+# 2 for every kernel, profiles/r04/pmc_calib.json)
 DOMINANT = {
     "config2_n5": ("void qe::k_cv_stream<5, 0,", 2),
     "config2_n7": ("void qe::k_cv_stream<7, 0,", 2),
@@ -37,18 +45,22 @@ DOMINANT = {
     "config3_joint_packed": ("void qe::k_cv_stream<10, 2,", 2),
     # check_quorum: dword rows of the peer words (256 B per row instruction)
     # and byte rows: 64-B requests, FETCH_SIZE x 1
-    "check_quorum": ("void qe::k_check_quorum<5,", 1),
+    "check_quorum": ("void qe::k_check_quorum<5,", 2),
     "config4_repl": ("void qe::k_repl_stream<5,", 2),
-    "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 1),
-    "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 1),
-    "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false,", 1),
+    "config5_elec": ("void qe::k_election<5, unsigned char, 0>", 2),
+    "config5_prevote_cq": ("void qe::k_election<5, unsigned char, 3>", 2),
+    "progress_step": ("void qe::k_progress_step<5, unsigned char, false, false, 4, false,", 2),
     # confchange: its ID block and u64 rows are read 512 B per instruction
     # (128-B requests): 2 x FETCH_SIZE = 75.0 B/group = its algorithmic reads
     # (r02h); round-2 summaries before r02h used 1
     "confchange": ("void qe::k_confchange<5>", 2),
     "config4_repl_joint": ("void qe::k_repl_stream<6, true, true,", 2),
-    "ready_collect": ("qe::k_collect_scatter", 1),
-    "progress_send": ("void qe::k_progress_send<5,", 1),
+    # ready_collect: all three kernels of one qe_collect (count, scan, scatter)
+    "ready_collect": (("void qe::k_collect_count", "void qe::k_collect_scan",
+                       "void qe::k_collect_scatter"), 2),
+    "progress_send": ("void qe::k_progress_send<5,", 2),
+    "progress_step_n7": ("void qe::k_progress_step<7, unsigned char, false, false, 4, false,", 2),
+    "progress_step_joint": ("void qe::k_progress_step<6, unsigned char, true, true, 4, false,", 2),
 }
 
 
@@ -60,9 +72,25 @@ def counters(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def algorithmic_bytes(bench_log):
+    """workload -> algorithmic bytes per launch from a bench.py JSON line
+    (the headline and every aux workload: bytes_per_unit x units)."""
+    line = [l for l in open(bench_log) if l.startswith("{")][-1]
+    d = json.loads(line)
+    out = {}
+    wl = d["config"]["workload"].split(":")[0]
+    r = d["roofline"]
+    out[wl] = r["achieved"] * 1e9 * r["kernel_ms"] / 1e3
+    for k, v in d.get("aux", {}).items():
+        if "achieved_GBs" in v and "kernel_ms" in v:
+            out[k] = v["achieved_GBs"] * 1e9 * v["kernel_ms"] / 1e3
+    return out
+
+
 def main():
     tag = sys.argv[1]
     base = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "profw")
+    algo = algorithmic_bytes(sys.argv[3]) if len(sys.argv) > 3 else {}
     outd = os.path.join(ROOT, "profiles", tag)
     os.makedirs(outd, exist_ok=True)
     summary, traffic = {}, {}
@@ -76,14 +104,17 @@ def main():
         c = {}
         for p in ("fetch", "write", "sq", "vmem"):
             c.update(counters(os.path.join(d, p, "**", "*counter_collection.csv")))
-        names = [k for k in stats if k.startswith(prefix)]
-        if not names:
+        prefixes = prefix if isinstance(prefix, tuple) else (prefix,)
+        bare = lambda x: x[5:] if x.startswith("void ") else x  # noqa: E731
+        names = [next((k for k in stats if bare(k).startswith(bare(p_))), None) for p_ in prefixes]
+        if not all(names):
             continue
-        k = names[0]
-        row = {"kernel": k, "avg_ns": float(stats[k]["AverageNs"]), "calls": int(stats[k]["Calls"])}
-        for (kn, cn), v in c.items():
-            if kn == k:
-                row[cn] = v
+        k = " + ".join(names)
+        row = {"kernel": k, "avg_ns": sum(float(stats[n]["AverageNs"]) for n in names),
+               "calls": int(stats[names[-1]]["Calls"])}
+        for (kn, cn), v in c.items():  # a multi-kernel workload: the sum per launch
+            if kn in names:
+                row[cn] = row.get(cn, 0.0) + v
         summary[wl] = row
         if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
             t = {"kernel": k, "profile": f"profiles/{tag}_pmc.json",
@@ -97,6 +128,13 @@ def main():
             if "SQ_INSTS_VMEM_RD" in row:
                 t["vmem_rd_per_launch"] = row["SQ_INSTS_VMEM_RD"]
                 t["vmem_wr_per_launch"] = row.get("SQ_INSTS_VMEM_WR")
+            if wl in algo:
+                t["algorithmic_bytes_per_launch"] = algo[wl]
+                t["traffic_over_algorithmic"] = t["hbm_bytes_per_launch"] / algo[wl]
+                if t["hbm_bytes_per_launch"] < 0.995 * algo[wl]:
+                    raise SystemExit(f"{wl}: PMC traffic {t['hbm_bytes_per_launch'] / 1e9:.3f} GB "
+                                     f"is below its algorithmic {algo[wl] / 1e9:.3f} GB -- "
+                                     f"a wrong counter correction, refused")
             traffic[wl] = t
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
