@@ -558,12 +558,34 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 #define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
 #endif
 
+// Diagnostic build only (QE_PSTEP_STAMPS, never the product): s_memtime
+// stamps at section boundaries of the production kernel, summed per wave and
+// added to a.acct[0..kStampN) -- shares of a wave's cycles per section
+// (cdna_hip_programming.md §7, In-kernel stamps; the build's run time is not
+// quoted, only the shares).
+#ifdef QE_PSTEP_STAMPS
+#define QE_STAMP(acc, k, prev)                                                            \
+  do {                                                                                    \
+    uint64_t t_;                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    acc[k] += t_ - prev;                                                                  \
+    prev = t_;                                                                            \
+  } while (0)
+#else
+#define QE_STAMP(acc, k, prev) \
+  do {                         \
+  } while (0)
+#endif
+constexpr int kStampN = 9;
+
 // WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
 // (21 KB at S = 5) would allow one 4-wave block per CU
 template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, bool RD,
           int WPB = kBlock / 64>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
-                          amdgpu_waves_per_eu(S <= 6 ? QE_PSTEP_WAVES : 1))) void
+                          amdgpu_waves_per_eu(S <= 9 ? QE_PSTEP_WAVES : 2))) void
 k_progress_step(PArgs a) {
   constexpr int CH = kRingChunk;
   constexpr uint32_t kFull = (1u << S) - 1u;
@@ -572,8 +594,16 @@ k_progress_step(PArgs a) {
   using QT = typename std::conditional<sizeof(MT) == 1, uint32_t, uint64_t>::type;
   constexpr uint32_t EW = 8 * sizeof(MT);
   constexpr uint32_t kRQ = QE_READ_QUEUE;
-  uint64_t cnt[P_N] = {0, 0, 0, 0, 0};
+  // statistics: per-lane counts in 32 bits (a lane sees at most one group
+  // per tile), the sums in 64
+  uint32_t n_groups = 0, n_adv = 0, n_viol = 0, n_read = 0;
+  uint64_t sum_c = 0, csum = 0;
   Acct<ACCT> ac;
+#ifdef QE_PSTEP_STAMPS
+  uint64_t stamp[kStampN] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
+#endif
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave =
       static_cast<uint64_t>(blockIdx.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -591,6 +621,10 @@ k_progress_step(PArgs a) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
     const bool live = lane < n;
+    QE_STAMP(stamp, 7, tprev);  // the previous tile's tail
+#ifdef QE_PSTEP_STAMPS
+    stamp[8] += 1;
+#endif
     bool runs_staged = false;  // wave-uniform
     uint32_t nr = 0;
     // ---- round trip 1: per group; message type and Match per slot ----
@@ -681,6 +715,22 @@ k_progress_step(PArgs a) {
       l_mix[wv][s][0][lane] = m0[s];
       l_mix[wv][s][1][lane] = ix[s];
     }
+    // the term-run table of every group with a tracked peer's rejection (the
+    // only user: findConflictByTerm in phase 2), loaded with round trip 2
+    // and staged into LDS at once -- not a round trip of its own
+    const bool need_runs = (rejm & trk) != 0;
+    if (__builtin_amdgcn_ballot_w64(need_runs)) {
+      runs_staged = true;
+      const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), need_runs ? lane : kOOB);
+      nr = rc < a.R ? rc : a.R;
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
+        const uint32_t off = (need_runs && static_cast<uint32_t>(r) < a.R) ? o8 : kOOB;
+        l_run[wv][r][0][lane] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
+        l_run[wv][r][1][lane] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
+      }
+    }
     bool runs_counted = false;  // ACCT: the run table counts once, when first used
     auto ty_of = [&](uint32_t s) -> uint32_t { return static_cast<uint32_t>(tys >> (4 * s)) & 15u; };
     PB cur;
@@ -711,6 +761,7 @@ k_progress_step(PArgs a) {
         }
       }
     }
+    QE_STAMP(stamp, 0, tprev);  // round trips 1-2 and phase 1
     // ---- phase 2: every peer's event sequence ----
     PSend x;
     x.F = F;
@@ -745,6 +796,7 @@ k_progress_step(PArgs a) {
         if (a.msg_count) bst8(0u, mk_rsrc(a.msg_count + row, n), lane);
         ac.add(live && a.msg_count, 1);
         if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
+        QE_STAMP(stamp, 6, tprev);
         continue;
       }
       ac.add(touched, 12);  // Next + the packed word
@@ -811,27 +863,9 @@ k_progress_step(PArgs a) {
       const uint32_t k3 = bcast_target ? popc(bset & ~below & ~(1u << s)) : 0u;
       uint32_t k2 = 0;
       bool lp = false;
-      if (!runs_staged &&
-          __builtin_amdgcn_ballot_w64(touched && tt == QE_MSG_APP_RESP_REJECT && cur.lt > 0)) {
-        // the first slot of the tile that needs findConflictByTerm loads the
-        // run table for every group of the tile
-        runs_staged = true;
-        const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), lane);
-        nr = rc < a.R ? rc : a.R;
-#pragma unroll
-        for (int r = 0; r < RM; r++) {
-          const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
-          if (static_cast<uint32_t>(r) < a.R) {
-            const uint32_t off = static_cast<uint32_t>(r) < nr ? o8 : kOOB;
-            l_run[wv][r][0][lane] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
-            l_run[wv][r][1][lane] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
-          } else {
-            l_run[wv][r][0][lane] = 0;
-            l_run[wv][r][1][lane] = 0;
-          }
-        }
-      }
+      QE_STAMP(stamp, 1, tprev);  // the slot's loads (Progress, ring, run table)
       if (!(QE_PSTEP_PROBE & 36) && __builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
+      QE_STAMP(stamp, 2, tprev);  // the bcasts before the peer's message
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
@@ -864,7 +898,7 @@ k_progress_step(PArgs a) {
         } else if (tt == QE_MSG_APP_RESP) {  // raft.go:1237-1282
           p.recent_active = 1;
           const uint64_t idx = cur.ix;
-          cnt[P_VIOL] += (idx > li);
+          n_viol += (idx > li);
           const bool old_paused = pr_paused(p, F);
           if (up) {  // MaybeUpdate (progress.go:144-153)
             p.match = idx;
@@ -946,6 +980,7 @@ k_progress_step(PArgs a) {
           }
         }
       }
+      QE_STAMP(stamp, 3, tprev);  // the message handler
       // After an accept: its sendAppend (sendIfEmpty), then the loop; the
       // later bcasts follow the loop.  Otherwise the message's sendAppend
       // and the later bcasts are consecutive sendIfEmpty sends: one burst.
@@ -954,7 +989,9 @@ k_progress_step(PArgs a) {
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (!(QE_PSTEP_PROBE & 64) && __builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
       }
+      QE_STAMP(stamp, 4, tprev);  // the message's sends, the send loop, later bcasts
       if (row_ring && !(QE_PSTEP_PROBE & 9)) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
+      QE_STAMP(stamp, 5, tprev);  // the ring write-back
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
       const bool tw = touched && !(QE_PSTEP_PROBE & 17);
@@ -983,6 +1020,7 @@ k_progress_step(PArgs a) {
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
       if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
+      QE_STAMP(stamp, 6, tprev);  // the peer's Progress stores and outputs
     }
     const uint32_t bc = popc(bset);
     bst64(c, r_commit, c != c0 ? o8 : kOOB);
@@ -1029,11 +1067,11 @@ k_progress_step(PArgs a) {
     ac.add(live && a.bcast, 1);
     if (live) {
       const uint64_t gh = (a.goff + g0 + lane) * kPhi;
-      cnt[P_GROUPS] += 1;
-      cnt[P_SUM] += c;
-      cnt[P_ADV] += (c != c0);
-      cnt[P_READ] += nrel;
-      cnt[P_CSUM] += mix64(gh ^ c ^ (static_cast<uint64_t>(bc) << 62)) +
+      n_groups += 1;
+      sum_c += c;
+      n_adv += (c != c0);
+      n_read += nrel;
+      csum += mix64(gh ^ c ^ (static_cast<uint64_t>(bc) << 62)) +
                      mix64(gh ^ (static_cast<uint64_t>(sent) << 40) ^ kSentSalt) +
                      (nrel ? mix64(gh ^ kReadSalt ^ (static_cast<uint64_t>(nrel) << 56)) : 0ull) +
                      (tc ? mix64(gh ^ kTermSalt ^ cfirst) : 0ull) +
@@ -1044,9 +1082,23 @@ k_progress_step(PArgs a) {
     const int idx[P_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
                           QE_STAT_INVARIANT_VIOLATIONS, QE_STAT_READ_RELEASED,
                           QE_STAT_CHECKSUM};
+    uint64_t cnt[P_N];
+    cnt[P_GROUPS] = n_groups;
+    cnt[P_SUM] = sum_c;
+    cnt[P_ADV] = n_adv;
+    cnt[P_VIOL] = n_viol;
+    cnt[P_READ] = n_read;
+    cnt[P_CSUM] = csum;
     block_stats_add<P_N, 64 * WPB>(cnt, idx, a.stats);
   }
   acct_flush<ACCT>(ac, a.acct);
+#ifdef QE_PSTEP_STAMPS
+  QE_STAMP(stamp, 7, tprev);
+  if (lane == 0 && a.acct)
+    for (int k = 0; k < kStampN; k++)
+      atomicAdd(reinterpret_cast<unsigned long long *>(a.acct + k),
+                static_cast<unsigned long long>(stamp[k]));
+#endif
 }
 
 // qe_progress_send: raft.sendAppend / maybeSendAppend(to, send_if_empty)

@@ -496,6 +496,10 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
  *     requests already pending (or the context numbers exhausted:
  *     read_head + read_count would be 0 mod 2^32) -> QE_RI_FULL, nothing
  *     changes (an engine limit; the host retries later).
+ * addRequest ignores a context already pending (read_only.go:57-60): a
+ * host that resends a request (etcd's server retries the same request id,
+ * server/etcdserver/v3_server.go:808-824) keeps its context number and does
+ * not submit it again.
  * Needs p->read_acks / read_head / read_count unless every result is
  * RESPOND or POSTPONED (lease_based).  ctx and index may be NULL; they are
  * written only where they apply.  Groups without a request: result 0. */
