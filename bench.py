@@ -19,7 +19,6 @@ import os
 import sys
 import time
 
-import socket
 import subprocess
 
 import numpy as np
@@ -121,12 +120,11 @@ def maybe_spawn(args):
     Rank 0 of the children prints the JSON line."""
     if "WORLD_SIZE" in os.environ or args.gpus <= 1:
         return False
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
-           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    # --standalone: the rendezvous store binds a free port itself (a port
+    # picked here and released could be taken before the launcher binds it)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone",
+           "--local-addr", "127.0.0.1", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     sys.exit(subprocess.call(cmd, env=env))
