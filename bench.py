@@ -818,6 +818,29 @@ def vmem_issue(workload, kern_ms, units):
             "probe_cycles": VMEM_PROBE_CYC, "source": t.get("profile")}
 
 
+def occupancy(workload):
+    """Registers, LDS and resident waves per SIMD of the workload's dominant
+    kernel(s) (the PMC record's kernel name looked up in
+    profiles/kernel_resources.json, scripts/kernel_resources.py)."""
+    names = load_pmc(workload).get("kernel")
+    try:
+        with open(os.path.join(ROOT, "profiles", "kernel_resources.json")) as f:
+            res = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if not names:
+        return None
+    bare = lambda x: x[5:] if x.startswith("void ") else x  # noqa: E731
+    res = {bare(k): v for k, v in res.items()}
+    out = {}
+    for n in names.split(" + "):
+        n = bare(n)
+        if n in res:
+            out[n[:n.index("(")]] = {k: res[n][k] for k in ("vgpr", "scratch_bytes", "lds_bytes",
+                                                            "waves_per_simd")}
+    return out or None
+
+
 def valu_roofline(workload, kern_ms, units):
     """VALU-issue roofline of a VALU-bound kernel: its VALU instructions per
     launch (SQ_INSTS_VALU, committed PMC) over the live kernel time, against
@@ -865,6 +888,9 @@ def run_workload(name, args, d, steps, warmup):
     vi = vmem_issue(name, kern_avg, units) if kind not in ("elec", "elec_pvcq") else None
     if vi:  # (the elections are VALU-bound: roofline_valu)
         extra["vmem_issue"] = vi
+    oc = occupancy(name)
+    if oc:
+        extra["occupancy"] = oc
     return {**extra,
         "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
         "unit": f"{unit_name}/s", "value": value, "ms_per_step": ms_step,
@@ -1009,7 +1035,7 @@ def main():
             r = run_workload(name, args, d, max(5, args.steps // 2), max(2, args.warmup // 2))
             aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
                                            "achieved_GBs", "hbm_frac", "invariant_violations")}
-            for k in ("roofline_valu", "vmem_issue"):
+            for k in ("roofline_valu", "vmem_issue", "occupancy"):
                 if k in r:
                     aux[name][k] = r[k]
 
