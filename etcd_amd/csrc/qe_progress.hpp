@@ -42,31 +42,39 @@ namespace qe {
 
 constexpr int kRingChunk = 8;  // F <= kRingChunk: the ring lives in registers (row form)
 
+// Cache policy of the Progress kernels' accesses (A/B knobs: 0 = default,
+// 2 = non-temporal)
+#ifndef QE_LD_AUX
+#define QE_LD_AUX 0
+#endif
+#ifndef QE_ST_AUX
+#define QE_ST_AUX 0
+#endif
 __device__ __forceinline__ uint64_t bld64(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, QE_LD_AUX));
 }
 __device__ __forceinline__ uint32_t bld8(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, QE_LD_AUX);
 }
 __device__ __forceinline__ void bst64(uint64_t v, rsrc_t r, uint32_t off) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, QE_ST_AUX);
 }
 __device__ __forceinline__ void bst8(uint32_t v, rsrc_t r, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, QE_ST_AUX);
 }
 __device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, QE_LD_AUX);
 }
 __device__ __forceinline__ void bst32(uint32_t v, rsrc_t r, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, QE_ST_AUX);
 }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 bld128(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, QE_LD_AUX));
 }
 __device__ __forceinline__ void bst128(u32x4 v, rsrc_t r, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, QE_ST_AUX);
 }
 // LDS-DMA (buffer_load_dwordx4 ... lds): 16 bytes per lane from base + off
 // (num_records `bytes`: an offset past it loads nothing) into the wave's LDS
