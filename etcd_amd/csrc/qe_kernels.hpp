@@ -585,7 +585,8 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
     const uint32_t mi = incp ? (incp[g] & kFull) : kFull;
     const uint32_t mo = (joint && outp) ? (outp[g] & kFull) : 0u;
     const uint32_t ml = lrnp ? (lrnp[g] & kFull) : 0u;
-    const uint32_t self = 1u << (a.self_slot[g] % S);
+    const uint32_t sidx = a.self_slot[g] % S;
+    const uint32_t self = 1u << sidx;
     const uint32_t voters = mi | mo;
     const bool promotable = (self & voters) != 0 && (self & ml) == 0;
     uint64_t t = a.term[g];
@@ -614,15 +615,31 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
           val = sgp[so] & resp;
           hup = a.shup && a.shup[so] != 0;
         }
-        if (cq && sta == QE_STATE_LEADER) {
-          // CheckQuorum round (raft.go:997-1018)
-          if constexpr (!scripted) {
+        // One set of slot draws per step, d = fmix32(gkey + step*C1 + s*C2
+        // (+ C3 for a leader's CheckQuorum round)) (oracle elec_draw), for
+        // the S - 1 slots other than self (its draw is never used): a wave
+        // mixing leaders and candidates hashes once, not once per branch.
+        const bool ldr = cq && sta == QE_STATE_LEADER;
+        const bool camp = !ldr && (sta == QE_STATE_FOLLOWER || sta == QE_STATE_LEADER || hup);
+        if constexpr (!scripted) {
+          if (!camp) {
+            const uint32_t off = ldr ? 0x27D4EB2Fu : 0u;
 #pragma unroll
-            for (int s = 0; s < S; s++) {
-              const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u + 0x27D4EB2Fu);
-              resp |= (((peers >> s) & 1u) && (d & 0xFFFFu) < a.p_active) ? (1u << s) : 0u;
+            for (int j = 0; j + 1 < S; j++) {
+              const uint32_t s = static_cast<uint32_t>(j) + (static_cast<uint32_t>(j) >= sidx ? 1u : 0u);
+              const uint32_t d = fmix32(hb + s * 0x85EBCA77u + off);
+              const bool peer = ((peers >> s) & 1u) != 0;
+              const uint32_t lo = d & 0xFFFFu;
+              // a leader: heard from within the election timeout (p_active);
+              // a candidate: the response delivered (p_drop) and granted
+              const bool deliver = peer && (ldr ? lo < a.p_active : lo >= a.p_drop);
+              resp |= deliver ? (1u << s) : 0u;
+              val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
             }
           }
+        }
+        if (ldr) {
+          // CheckQuorum round (raft.go:997-1018)
           const uint32_t recent = resp | self;
           const uint32_t present = voters & ~ml;
           const bool qa = (joint ? joint_vote(mi, mo, present, recent & present)
@@ -633,19 +650,9 @@ __global__ __launch_bounds__(kBlock) void k_election(EArgs a) {
             sta = QE_STATE_FOLLOWER;
             c32[E_DOWN] += 1;
           }
-        } else if (sta == QE_STATE_FOLLOWER || sta == QE_STATE_LEADER || hup) {
+        } else if (camp) {
           elec_campaign<joint>(pre, mi, mo, ml, self, t, sta, vd, gr, c32);
         } else {
-          // d = fmix32(gkey + step*C1 + s*C2) per slot (oracle elec_draw)
-          if constexpr (!scripted) {
-#pragma unroll
-            for (int s = 0; s < S; s++) {
-              const uint32_t d = fmix32(hb + static_cast<uint32_t>(s) * 0x85EBCA77u);
-              const bool deliver = ((peers >> s) & 1u) && (d & 0xFFFFu) >= a.p_drop;
-              resp |= deliver ? (1u << s) : 0u;
-              val |= (deliver && (d >> 16) < a.p_grant) ? (1u << s) : 0u;
-            }
-          }
           const uint32_t gbefore = popc(gr & vd & ~ml & voters);
           const uint32_t fresh = resp & ~vd;  // RecordVote: first vote sticks
           vd |= fresh;
