@@ -148,6 +148,7 @@ class Dist:
         torch.cuda.set_device(dev_idx)
         self.dev = torch.device("cuda", dev_idx)
         self.comm = None
+        self.stats_path = None  # set when qe_allreduce_stats could not be used
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.backend == "nccl":
@@ -195,9 +196,19 @@ class Dist:
         through qe_allreduce_stats (128 B, once per run, latency-bound and
         off the data path); gloo rehearsal: torch on the host."""
         if self.world > 1:
+            if self.backend == "nccl" and self.stats_path is None:
+                try:
+                    engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
+                        engine._ptr(folded), folded.numel(), self._rccl(),
+                        engine._stream(self.dev)))
+                    return folded
+                except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+                    # the engine's communicator failed on this node: the stats
+                    # (not the timed path) go through torch's RCCL instead, and
+                    # the JSON line says so
+                    self.stats_path = f"torch.distributed all_reduce (qe_allreduce_stats: {e})"
             if self.backend == "nccl":
-                engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
-                    engine._ptr(folded), folded.numel(), self._rccl(), engine._stream(self.dev)))
+                dist.all_reduce(folded, op=dist.ReduceOp.SUM)
             else:
                 t = self._coll(folded)
                 dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -1086,7 +1097,10 @@ def main():
             },
             "cpu_baseline": cpu,
             "checks": {"invariant_violations": main_res["invariant_violations"],
-                       "stats_checksum": main_res["checksum"]},
+                       "stats_checksum": main_res["checksum"],
+                       "stats_allreduce": (None if d.world == 1 else d.stats_path or (
+                           "qe_allreduce_stats (RCCL)" if d.backend == "nccl"
+                           else f"torch.distributed {d.backend} (rehearsal)"))},
             "aux": aux,
         }
         print(json.dumps(line))
