@@ -42,32 +42,46 @@ namespace qe {
 
 constexpr int kRingChunk = 8;  // F <= kRingChunk: the ring lives in registers (row form)
 
-// Cache policy of the Progress kernels' accesses (A/B knobs: 0 = default,
-// 2 = non-temporal)
+// Cache policy of the Progress kernels' accesses (the helpers' AUX: 0 =
+// default, 2 = non-temporal).  The Progress step re-touches the lines it
+// loads (non-temporal loads: +15 %) and so does CheckQuorum (+17 %); the send
+// kernel's appends and Progress rows go non-temporal, kNT: -9 %
+// (profiles/r04/pstep_ab.txt, send_cq_nt_ab.txt).
+// QE_LD_AUX / QE_ST_AUX: A/B knobs for the default.
 #ifndef QE_LD_AUX
 #define QE_LD_AUX 0
 #endif
 #ifndef QE_ST_AUX
 #define QE_ST_AUX 0
 #endif
+#ifndef QE_SEND_AUX  // A/B knob: the send kernel's policy
+#define QE_SEND_AUX 2
+#endif
+constexpr int kNT = QE_SEND_AUX;
+template <int AUX = QE_LD_AUX>
 __device__ __forceinline__ uint64_t bld64(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, QE_LD_AUX));
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
 }
+template <int AUX = QE_LD_AUX>
 __device__ __forceinline__ uint32_t bld8(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, QE_LD_AUX);
+  return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, AUX);
 }
+template <int AUX = QE_ST_AUX>
 __device__ __forceinline__ void bst64(uint64_t v, rsrc_t r, uint32_t off) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, QE_ST_AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, AUX);
 }
+template <int AUX = QE_ST_AUX>
 __device__ __forceinline__ void bst8(uint32_t v, rsrc_t r, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, QE_ST_AUX);
+  __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, AUX);
 }
+template <int AUX = QE_LD_AUX>
 __device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, QE_LD_AUX);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
 }
+template <int AUX = QE_ST_AUX>
 __device__ __forceinline__ void bst32(uint32_t v, rsrc_t r, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, QE_ST_AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, AUX);
 }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 bld128(rsrc_t r, uint32_t off) {
@@ -218,10 +232,11 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t start, uint32_t count, uin
 // a non-empty ring turns it wide -- every live entry's upper word (the
 // epoch) is written first, a rare path; a wide ring also gets the entry's
 // upper word.
+template <int AUX = QE_ST_AUX>
 __device__ __forceinline__ void ring_add_mem(PR &p, const PSend &x, bool on, uint32_t pos,
                                              uint64_t v) {
   const uint32_t h = static_cast<uint32_t>(v >> 32);
-  bst32(static_cast<uint32_t>(v), x.rlo, on ? x.lb + pos * 4 : kOOB);
+  bst32<AUX>(static_cast<uint32_t>(v), x.rlo, on ? x.lb + pos * 4 : kOOB);
   const bool first = p.count == 0;
   const bool conv = on && !first && !rep_wide(p.rep) && h != rep_epoch(p.rep);
   if (__builtin_amdgcn_ballot_w64(conv)) {
@@ -229,7 +244,7 @@ __device__ __forceinline__ void ring_add_mem(PR &p, const PSend &x, bool on, uin
     uint32_t q = p.start;
     while (q >= x.F) q -= x.F;
     for (uint32_t j = 0; __builtin_amdgcn_ballot_w64(conv && j < p.count); j++) {
-      bst32(ep, x.rhi, (conv && j < p.count) ? x.lb + q * 4 : kOOB);
+      bst32<AUX>(ep, x.rhi, (conv && j < p.count) ? x.lb + q * 4 : kOOB);
       if (++q >= x.F) q = 0;
     }
   }
@@ -240,7 +255,7 @@ __device__ __forceinline__ void ring_add_mem(PR &p, const PSend &x, bool on, uin
       p.rep = QE_PF_RING_WIDE;
   }
   const bool whi = on && rep_wide(p.rep);
-  if (__builtin_amdgcn_ballot_w64(whi)) bst32(h, x.rhi, whi ? x.lb + pos * 4 : kOOB);
+  if (__builtin_amdgcn_ballot_w64(whi)) bst32<AUX>(h, x.rhi, whi ? x.lb + pos * 4 : kOOB);
 }
 
 // Entry at ring position pos, memory form, decoded with the representation
@@ -264,7 +279,7 @@ constexpr uint32_t kLoop = 0xFFFFFFFFu;
 // (OptimisticUpdate + Inflights.Add) until the ring is full or Next passes
 // lastIndex, then empty MsgApps for the remaining calls with sendIfEmpty.
 // The appended entries extend `run`.
-template <bool ACCT>
+template <bool ACCT, int AUX = QE_ST_AUX>
 __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x, PRun &run,
                                            Acct<ACCT> &ac) {
   const bool loop = k == kLoop;
@@ -319,7 +334,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
       const PRun here{0, 0, p.next};
       const uint64_t last = run_val(here, 0, x.me, x.li);
       const uint32_t pos = ring_pos(p.start, p.count, x.F);
-      ring_add_mem(p, x, on, pos, last);
+      ring_add_mem<AUX>(p, x, on, pos, last);
       if (on) {
         if (run.n == 0) {
           run.p = pos;
@@ -1229,14 +1244,14 @@ __device__ __forceinline__ void ps_issue(const PArgs &a, uint64_t t, uint32_t la
   const uint64_t g0 = t * 64;
   const uint32_t n = tile_n(a.G, t);
   const uint32_t o8 = lane * 8, o4 = lane * 4;
-  x.fi = bld64(mk_rsrc(a.first_index + g0, n * 8), w ? o8 : kOOB);
-  x.li = bld64(mk_rsrc(a.last_index + g0, n * 8), w ? o8 : kOOB);
-  x.sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), w ? o8 : kOOB) : 0;
+  x.fi = bld64<kNT>(mk_rsrc(a.first_index + g0, n * 8), w ? o8 : kOOB);
+  x.li = bld64<kNT>(mk_rsrc(a.last_index + g0, n * 8), w ? o8 : kOOB);
+  x.sn = a.snap_index ? bld64<kNT>(mk_rsrc(a.snap_index + g0, n * 8), w ? o8 : kOOB) : 0;
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
-    x.nx[s] = bld64(mk_rsrc(a.next + row, n * 8), bit_off(w, s, o8));
-    x.pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), bit_off(w, s, o4));
+    x.nx[s] = bld64<kNT>(mk_rsrc(a.next + row, n * 8), bit_off(w, s, o8));
+    x.pw[s] = bld32<kNT>(mk_rsrc(a.pw + row, n * 4), bit_off(w, s, o4));
   }
 }
 
@@ -1276,13 +1291,13 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
     xs.first_index = 0;
     xs.snapped = false;
     PRun run{0, 0, 0};
-    send_burst<false>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
+    send_burst<false, kNT>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
     const uint32_t nw = pr_pack(p);
     const bool wn = on && p.next != x.nx[s], wp = on && xs.snapped, ww = on && nw != x.pw[s];
-    if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
+    if (__builtin_amdgcn_ballot_w64(wn)) bst64<kNT>(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
     if (__builtin_amdgcn_ballot_w64(wp))
-      bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? lane * 8 : kOOB);
-    if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), ww ? lane * 4 : kOOB);
+      bst64<kNT>(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? lane * 8 : kOOB);
+    if (__builtin_amdgcn_ballot_w64(ww)) bst32<kNT>(nw, mk_rsrc(a.pw + row, n * 4), ww ? lane * 4 : kOOB);
     sent |= xs.count_msgs ? (1u << s) : 0u;
     snapm |= xs.snapped ? (1u << s) : 0u;
   }
