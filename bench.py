@@ -100,6 +100,9 @@ def parse():
                     help="CPU baseline threads (0 = this process's CPU share: the affinity "
                          "set, capped by OMP_NUM_THREADS when the box sets it)")
     ap.add_argument("--cpu-groups", type=int, default=1 << 21)
+    ap.add_argument("--allow-stats-fallback", action="store_true",
+                    help="N > 1: accept the stats all-reduce through torch when the engine's "
+                         "qe_allreduce_stats path cannot be set up (reported; otherwise exit 3)")
     ap.add_argument("--aux-groups-div", type=int, default=1,
                     help="rehearsal only: divide every secondary workload's group count")
     return ap.parse_args()
@@ -130,29 +133,45 @@ def maybe_spawn(args):
     sys.exit(subprocess.call(cmd, env=env))
 
 
+COMM_INIT_TIMEOUT_MS = 120_000  # qe_comm_init_timeout: peers that never join
+
+
 class Dist:
     """One process per GPU (torch.distributed.run env).  Collectives go over
     RCCL (backend "nccl") by default: barrier/max through torch, the stats
     all-reduce through the engine's own C ABI (qe_allreduce_stats on an RCCL
-    communicator set up with qe_comm_init -- the path a Go host uses).
+    communicator set up with qe_comm_init_timeout -- the path a Go host uses).
     QE_DIST_BACKEND=gloo with QE_DEVICE_MOD=1 rehearses the multi-rank logic
-    on a 1-GPU box (all ranks on cuda:0, counters reduced on the host)."""
+    on a 1-GPU box (all ranks on cuda:0, counters reduced on the host).
 
-    def __init__(self):
+    Which path the statistics take is decided ONCE, at start-up, by every
+    rank together (_select_stats_path): each rank reports whether its part
+    of the engine communicator's set-up succeeded and the ranks take the MIN
+    over the torch group, so all of them use qe_allreduce_stats or all of
+    them use torch's all_reduce -- never a mix, which would leave the ranks
+    in different collectives (a hang).  A fallback is reported in the JSON
+    line and fails the run unless --allow-stats-fallback is given."""
+
+    def __init__(self, backend=None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.backend = os.environ.get("QE_DIST_BACKEND", "nccl")
+        self.backend = backend or os.environ.get("QE_DIST_BACKEND", "nccl")
         mod = int(os.environ.get("QE_DEVICE_MOD", "0"))
         dev_idx = self.local % mod if mod > 0 else self.local
-        torch.cuda.set_device(dev_idx)
-        self.dev = torch.device("cuda", dev_idx)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(dev_idx)
+            self.dev = torch.device("cuda", dev_idx)
+        else:  # CPU tests of the rank logic (gloo)
+            self.dev = torch.device("cpu")
         self.comm = None
-        self.stats_path = None  # set when qe_allreduce_stats could not be used
+        self.stats_path = None      # what the stats all-reduce went through
+        self.stats_fallback = None  # why the engine's collective is not used (all ranks)
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)
+                self._select_stats_path()
             else:
                 dist.init_process_group(self.backend)
 
@@ -173,47 +192,94 @@ class Dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def _rccl(self):
-        """The engine's RCCL communicator (qe_comm_init); the 128-byte id
-        travels from rank 0 over torch.distributed."""
-        if self.comm is None:
-            import ctypes as C
-            lib = engine._lib.lib()
-            idb = (C.c_uint8 * lib.qe_comm_id_bytes())()
-            if self.rank == 0:
+    def all_ok(self, ok):
+        """True iff `ok` holds on every rank (MIN over the torch group), so
+        every rank takes the same branch after it."""
+        if self.world == 1:
+            return bool(ok)
+        t = self._coll(torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.dev))
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item()) == 1
+
+    def _errors(self, err):
+        """Every rank's error text (all_gather_object), for the JSON line."""
+        errs = [None] * self.world
+        dist.all_gather_object(errs, err)
+        return "; ".join(f"rank {r}: {e}" for r, e in enumerate(errs) if e)
+
+    def _try_engine_comm(self):
+        """(communicator or None, error text) -- never raises, and bounded:
+        rank 0's unique id (or its failure) travels over torch.distributed,
+        then every rank calls qe_comm_init_timeout."""
+        import ctypes as C
+        lib = engine._lib.lib()
+        idb = (C.c_uint8 * lib.qe_comm_id_bytes())()
+        payload = [None, ""]
+        if self.rank == 0:
+            try:
                 engine.check("qe_comm_unique_id", lib.qe_comm_unique_id(idb))
-            obj = [bytes(idb)]
-            dist.broadcast_object_list(obj, src=0)
-            idb = (C.c_uint8 * len(obj[0])).from_buffer_copy(obj[0])
-            comm = C.c_void_p()
-            engine.check("qe_comm_init", lib.qe_comm_init(C.byref(comm), self.world, self.rank,
-                                                           idb, self.dev.index))
+                payload = [bytes(idb), ""]
+            except Exception as e:  # noqa: BLE001 -- every rank learns it below
+                payload = [None, f"qe_comm_unique_id: {e}"]
+        dist.broadcast_object_list(payload, src=0)
+        if payload[0] is None:
+            return None, payload[1] if self.rank == 0 else ""
+        idb = (C.c_uint8 * len(payload[0])).from_buffer_copy(payload[0])
+        comm = C.c_void_p()
+        try:
+            engine.check("qe_comm_init_timeout", lib.qe_comm_init_timeout(
+                C.byref(comm), self.world, self.rank, idb, self.dev.index, COMM_INIT_TIMEOUT_MS))
+        except Exception as e:  # noqa: BLE001
+            return None, str(e)
+        return comm, ""
+
+    def _select_stats_path(self):
+        comm, err = self._try_engine_comm()
+        if self.all_ok(comm is not None):
             self.comm = comm
-        return self.comm
+            self.stats_path = "qe_allreduce_stats (RCCL)"
+            return
+        if comm is not None:  # this rank joined, another did not: nobody uses it
+            engine._lib.lib().qe_comm_abort(comm)
+        self.stats_fallback = self._errors(err) or "engine communicator unavailable"
+        self.stats_path = f"torch.distributed all_reduce (FALLBACK: {self.stats_fallback})"
+
+    def _torch_sum(self, folded):
+        if self.backend == "nccl":
+            dist.all_reduce(folded, op=dist.ReduceOp.SUM)
+            return folded
+        t = self._coll(folded)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.to(self.dev)
 
     def sum_stats(self, folded):
         """All-reduce (sum) of the uint64 statistics vector: RCCL over xGMI
-        through qe_allreduce_stats (128 B, once per run, latency-bound and
-        off the data path); gloo rehearsal: torch on the host."""
-        if self.world > 1:
-            if self.backend == "nccl" and self.stats_path is None:
-                try:
-                    engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
-                        engine._ptr(folded), folded.numel(), self._rccl(),
-                        engine._stream(self.dev)))
-                    return folded
-                except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-                    # the engine's communicator failed on this node: the stats
-                    # (not the timed path) go through torch's RCCL instead, and
-                    # the JSON line says so
-                    self.stats_path = f"torch.distributed all_reduce (qe_allreduce_stats: {e})"
-            if self.backend == "nccl":
-                dist.all_reduce(folded, op=dist.ReduceOp.SUM)
-            else:
-                t = self._coll(folded)
-                dist.all_reduce(t, op=dist.ReduceOp.SUM)
-                folded = t.to(self.dev)
-        return folded
+        through qe_allreduce_stats (128 B, once per workload, latency-bound
+        and off the data path); gloo rehearsal: torch on the host.  The
+        ranks agree on the outcome of every engine all-reduce before using
+        it; a failure anywhere aborts the engine communicator on every rank
+        (a collective a peer never entered cannot complete) and all of them
+        continue on torch's all_reduce, as a reported fallback."""
+        if self.world == 1:
+            return folded
+        if self.comm is None:
+            if self.stats_path is None:  # the gloo rehearsal (no engine communicator)
+                self.stats_path = f"torch.distributed {self.backend} (rehearsal)"
+            return self._torch_sum(folded)
+        keep = folded.clone()
+        err = ""
+        try:
+            engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
+                engine._ptr(folded), folded.numel(), self.comm, engine._stream(self.dev)))
+        except Exception as e:  # noqa: BLE001
+            err = f"qe_allreduce_stats: {e}"
+        if self.all_ok(not err):
+            return folded
+        engine._lib.lib().qe_comm_abort(self.comm)
+        self.comm = None
+        self.stats_fallback = self._errors(err) or "qe_allreduce_stats failed on a rank"
+        self.stats_path = f"torch.distributed all_reduce (FALLBACK: {self.stats_fallback})"
+        return self._torch_sum(keep)
 
     def close(self):
         if self.comm is not None:
@@ -1098,13 +1164,25 @@ def main():
             "cpu_baseline": cpu,
             "checks": {"invariant_violations": main_res["invariant_violations"],
                        "stats_checksum": main_res["checksum"],
-                       "stats_allreduce": (None if d.world == 1 else d.stats_path or (
-                           "qe_allreduce_stats (RCCL)" if d.backend == "nccl"
-                           else f"torch.distributed {d.backend} (rehearsal)"))},
+                       "stats_allreduce": None if d.world == 1 else d.stats_path,
+                       "stats_fallback": d.stats_fallback},
             "aux": aux,
         }
         print(json.dumps(line))
+    fallback = d.stats_fallback
     d.close()
+    sys.exit(exit_status(fallback, args.allow_stats_fallback))
+
+
+def exit_status(fallback, allow):
+    """3 when the stats all-reduce fell back to torch (on every rank) and
+    --allow-stats-fallback was not given, so a multi-GPU run cannot pass
+    without exercising qe_allreduce_stats; else 0."""
+    if fallback and not allow:
+        print(f"bench.py: the statistics all-reduce fell back to torch on every rank "
+              f"({fallback}); rerun with --allow-stats-fallback to accept", file=sys.stderr)
+        return 3
+    return 0
 
 
 if __name__ == "__main__":

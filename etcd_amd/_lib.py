@@ -200,7 +200,9 @@ PROTOTYPES = {
     "qe_comm_id_bytes": (C.c_size_t, []),
     "qe_comm_unique_id": (C.c_int, [vp]),
     "qe_comm_init": (C.c_int, [C.POINTER(vp), u32, u32, vp, C.c_int]),
+    "qe_comm_init_timeout": (C.c_int, [C.POINTER(vp), u32, u32, vp, C.c_int, u32]),
     "qe_comm_destroy": (C.c_int, [vp]),
+    "qe_comm_abort": (C.c_int, [vp]),
     "qe_allreduce_stats": (C.c_int, [vp, u32, vp, vp]),
 }
 

@@ -441,11 +441,7 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
   a.term_commit = m->term_commit;
   a.term_commit_index = m->term_commit_index;
   a.stats = stats;
-#ifdef QE_PSTEP_STAMPS  // diagnostic build: bytes_requested receives the stamp sums
-  const int kind = 0;
-#else
   const int kind = m->bytes_requested ? 2 : 0;
-#endif
   return dispatch_progress(p->num_slots, a, kind, p->inc_mask != nullptr, p->out_mask != nullptr,
                            static_cast<hipStream_t>(stream));
 }

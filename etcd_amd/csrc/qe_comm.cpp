@@ -14,6 +14,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <thread>
+
 #include "../../include/etcd_quorum.h"
 
 namespace qe {
@@ -40,7 +43,8 @@ int qe_comm_unique_id(void *id) {
   return QE_OK;
 }
 
-int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id, int device) {
+int qe_comm_init_timeout(void **comm, uint32_t nranks, uint32_t rank, const void *id,
+                         int device, uint32_t timeout_ms) {
   if (!comm || !id || nranks == 0 || rank >= nranks || device < 0) return QE_EINVAL;
   *comm = nullptr;
   int rc = qe::hip_status(hipSetDevice(device));
@@ -48,10 +52,46 @@ int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id, in
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   ncclComm_t c = nullptr;
-  rc = comm_status(ncclCommInitRank(&c, static_cast<int>(nranks), u, static_cast<int>(rank)));
-  if (rc) return rc;
+  if (timeout_ms == 0) {  // blocking: ncclCommInitRank returns once every rank joined
+    rc = comm_status(ncclCommInitRank(&c, static_cast<int>(nranks), u, static_cast<int>(rank)));
+    if (rc) return rc;
+    *comm = c;
+    return QE_OK;
+  }
+  // non-blocking communicator: the init returns at once and is polled, so a
+  // rank whose peers never join (one of them failed before calling init)
+  // gives up after timeout_ms instead of waiting forever; the caller then
+  // agrees with its peers over its own transport which path to take
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c, static_cast<int>(nranks), u, static_cast<int>(rank), &cfg);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress && c != nullptr) {
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
+    if (ms >= static_cast<long long>(timeout_ms)) {
+      ncclCommAbort(c);
+      qe::set_error("qe_comm_init_timeout: the other ranks did not join in time");
+      return QE_ECOMM;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) break;
+  }
+  if (r != ncclSuccess) {
+    if (c) ncclCommAbort(c);
+    return comm_status(r == ncclInProgress ? ncclInternalError : r);
+  }
   *comm = c;
   return QE_OK;
+}
+
+int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id, int device) {
+  return qe_comm_init_timeout(comm, nranks, rank, id, device, 0);
+}
+
+int qe_comm_abort(void *comm) {
+  if (!comm) return QE_EINVAL;
+  return comm_status(ncclCommAbort(static_cast<ncclComm_t>(comm)));
 }
 
 int qe_comm_destroy(void *comm) {
@@ -61,9 +101,14 @@ int qe_comm_destroy(void *comm) {
 
 int qe_allreduce_stats(uint64_t *stats, uint32_t n, void *comm, void *stream) {
   if (!stats || !comm || n == 0 || n > QE_STATS_WORDS) return QE_EINVAL;
-  return comm_status(ncclAllReduce(stats, stats, n, ncclUint64, ncclSum,
-                                   static_cast<ncclComm_t>(comm),
-                                   static_cast<hipStream_t>(stream)));
+  const ncclComm_t c = static_cast<ncclComm_t>(comm);
+  ncclResult_t r = ncclAllReduce(stats, stats, n, ncclUint64, ncclSum, c,
+                                 static_cast<hipStream_t>(stream));
+  // a non-blocking communicator (qe_comm_init_timeout) may return before the
+  // collective is enqueued: wait for the enqueue (not for the sum itself)
+  while (r == ncclInProgress)
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) break;
+  return comm_status(r);
 }
 
 }  // extern "C"

@@ -1,23 +1,25 @@
 // qe_kernels.hpp — MI355X (gfx950) kernels of the batched quorum engine.
 //
-// One lane owns one pair of adjacent groups: every slot row of the SoA match
-// array is read with 16-byte loads, so one wave instruction moves 1 KiB of a
-// slot row and all 64 lanes' loads fall in eight contiguous 128-byte lines.
-// A wave iterates over tiles of 64*PAIRS pairs; the grid is persistent
-// (a few workgroups per CU) and strides over tiles.  See DESIGN.md §2-§3.
+// One lane owns one group: a slot row of the SoA arrays ([S][stride]) is one
+// coalesced access per wave (512 B of u64 for a 64-group tile), addressed
+// through a per-tile buffer descriptor whose num_records clips the ragged
+// last tile.  The stream kernels (qe_stream.hpp) give each wave a chunk of
+// tiles and keep tile k+1's loads in flight while tile k is decided; the
+// Progress kernels (qe_progress.hpp) walk one tile per wave.  See DESIGN.md
+// §2-§3.
 #pragma once
 // A/B knobs are for variant libraries built by
-// scripts/build_variant*.sh, which define QE_VARIANT_BUILD.  QE_PSTEP_PROBE
-// drops work (results change); the others only change code paths or launch
-// shapes.  A product build with any of them set is refused, so a stray -D can
-// never ship a library that computes something else.
+// scripts/build_variant*.sh, which define QE_VARIANT_BUILD; they only change
+// code paths or launch shapes (the experiments that dropped work, the
+// stamps and the LDS-DMA ring of round 4 left the product kernel in round 5:
+// git show bdcd377:etcd_amd/csrc/qe_progress.hpp).  A product build with any
+// of them set is refused, so a stray -D can never ship a library that
+// computes something else.
 #if !defined(QE_VARIANT_BUILD) &&                                                  \
-    (defined(QE_PSTEP_PROBE) || defined(QE_CQ_CHANGED_ONLY) ||                     \
-     defined(QE_STREAM_ALL_ROWS) || defined(QE_NO_RM8) || defined(QE_RM16_WPB) ||  \
-     defined(QE_PSTEP_WAVES) || defined(QE_STREAM_TPW) || defined(QE_STREAM_WAVES) || \
-     defined(QE_JOINT_MIN_WAVES) || defined(QE_PSTEP_STAMPS) || defined(QE_PSTEP_RING_DMA) || \
-     defined(QE_PSTEP_FENCE) || defined(QE_LD_AUX) || defined(QE_ST_AUX) || \
-     defined(QE_SEND_AUX))
+    (defined(QE_CQ_CHANGED_ONLY) || defined(QE_STREAM_ALL_ROWS) || defined(QE_NO_RM8) || \
+     defined(QE_RM16_WPB) || defined(QE_PSTEP_WAVES) || defined(QE_STREAM_TPW) ||        \
+     defined(QE_STREAM_WAVES) || defined(QE_JOINT_MIN_WAVES) || defined(QE_LD_AUX) ||     \
+     defined(QE_ST_AUX) || defined(QE_SEND_AUX))
 #error "A/B knob set in a product build: use scripts/build_variant*.sh (QE_VARIANT_BUILD)"
 #endif
 #include <hip/hip_runtime.h>

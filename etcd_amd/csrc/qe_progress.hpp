@@ -90,42 +90,6 @@ __device__ __forceinline__ u32x4 bld128(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst128(u32x4 v, rsrc_t r, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, QE_ST_AUX);
 }
-// LDS-DMA (buffer_load_dwordx4 ... lds): 16 bytes per lane from base + off
-// (num_records `bytes`: an offset past it loads nothing) into the wave's LDS
-// row dst[0..64) (lane i at dst[i]), no VGPR destination.  Inline asm, so
-// hipcc leaves it out of its s_waitcnt bookkeeping: with the builtin it
-// waits vmcnt(0) at every later use of a load while a DMA is in flight,
-// which drains the next slot's prefetch and this slot's stores.  Every DMA
-// here is followed by a load whose result the reader waits for (in-order
-// return): lds_after.  M0 (the DMA's LDS base) is saved and restored in
-// the same statement.
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-typedef uint32_t sgpr4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void lds_dma16(const void *base, uint32_t bytes, u32x4 *dst,
-                                          uint32_t off) {
-  const uint64_t b = reinterpret_cast<uintptr_t>(base);
-  const sgpr4 d = {static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32) & 0xFFFFu, bytes,
-                   0x00020000u};
-  const uint32_t la = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_u32x4 *)dst)));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(off), "s"(d), "s"(la)
-      : "memory");
-}
-// dst[lane] once `dep` has arrived: dep is the result of a vector load
-// issued after the DMA that filled dst, and loads return in issue order, so
-// the wait hipcc emits for dep (an operand of the empty asm) retires the DMA
-// too; the LDS address passes through the asm, so the read cannot move above
-// that wait.
-__device__ __forceinline__ u32x4 lds_after(const u32x4 *dst, uint32_t lane, uint32_t dep) {
-  uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const lds_u32x4 *)(dst + lane)));
-  asm volatile("" : "+v"(la) : "v"(dep));
-  return *(const lds_u32x4 *)static_cast<uintptr_t>(la);
-}
 template <typename MT>
 __device__ __forceinline__ void bst_mask(uint32_t v, rsrc_t r, uint32_t lane, bool on = true) {
   const uint32_t off = on ? lane * static_cast<uint32_t>(sizeof(MT)) : kOOB;
@@ -363,15 +327,12 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
 // read or rewritten (`ld`: touched, with live entries) in registers, one or
 // two 16-byte loads per lane; hi[] holds every position's upper word (the
 // epoch unless the peer is wide).
-// (DMA: the low words arrived by LDS-DMA with the slot's prefetch, in dlo)
-template <bool DMA>
 __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
-                                              const uint32_t (&dlo)[kRingChunk],
                                               uint32_t (&lo)[kRingChunk],
                                               uint32_t (&hi)[kRingChunk]) {
 #pragma unroll
-  for (int k = 0; k < kRingChunk; k++) lo[k] = DMA && ld ? dlo[k] : 0u;
-  if (!DMA && __builtin_amdgcn_ballot_w64(ld)) {
+  for (int k = 0; k < kRingChunk; k++) lo[k] = 0u;
+  if (__builtin_amdgcn_ballot_w64(ld)) {
     const u32x4 a = bld128(x.rlo, ld ? x.lb : kOOB);
     lo[0] = a.x, lo[1] = a.y, lo[2] = a.z, lo[3] = a.w;
     if (FP > 4) {
@@ -613,54 +574,20 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
   else b.rc = 0;
 }
 
-#ifndef QE_PSTEP_FENCE  // 1: pb_ready before a slot's stores
-#define QE_PSTEP_FENCE 1
-#endif
 // The next slot's loads have arrived (an empty asm using them: hipcc waits
-// for them here).  Called before a slot's first store, on every path (the
-// last slot's nxt holds constants): with the loads retired there, `cur =
-// nxt` at the loop latch and the first use of cur at the loop head need no
-// wait, where hipcc's path-merged bookkeeping would otherwise wait vmcnt(0)
-// -- draining the slot's own stores before the next slot starts (vmcnt
-// counts stores, in issue order).
+// for them here).  Called before a slot's first store, on every path: with
+// the loads retired there, `cur = nxt` at the loop latch and the first use of
+// cur at the loop head need no wait, where hipcc's path-merged bookkeeping
+// would otherwise wait vmcnt(0) -- draining the slot's own stores before the
+// next slot starts (vmcnt counts stores, in issue order).  S = 7 4.89 ->
+// 4.68 ms, joint 4.26 -> 4.07 ms (profiles/r04/pstep_ab.txt).
 __device__ __forceinline__ void pb_ready(const PB &b) {
-  if (QE_PSTEP_FENCE) asm volatile("" ::"v"(b.nx), "v"(b.w), "v"(b.hn), "v"(b.lt), "v"(b.rc));
+  asm volatile("" ::"v"(b.nx), "v"(b.w), "v"(b.hn), "v"(b.lt), "v"(b.rc));
 }
-
-#ifndef QE_PSTEP_PROBE  // timing probes only (never the product build): bit 0 drops the
-#define QE_PSTEP_PROBE 0  // per-peer stores, bit 1 the ring loads, bit 2 the sends, bit 3
-#endif                    // the ring store, bit 4 the Progress stores, bit 5 the k1 burst,
-                          // bit 6 the burst of the bcasts after an accept's send loop
-
-#ifndef QE_PSTEP_RING_DMA  // 1: a touched peer's ring by LDS-DMA one slot ahead (DR); off:
-#define QE_PSTEP_RING_DMA 0   // S = 5 +1.9 %, S = 7 / joint within 1 % of the fenced
-#endif                        // register path (profiles/r04/pstep_ab.txt)
 
 #ifndef QE_PSTEP_WAVES
 #define QE_PSTEP_WAVES 3  // min waves per SIMD requested (VGPR budget)
 #endif
-
-// Diagnostic build only (QE_PSTEP_STAMPS, never the product): s_memtime
-// stamps at section boundaries of the production kernel, summed per wave and
-// added to a.acct[0..kStampN) -- shares of a wave's cycles per section
-// (cdna_hip_programming.md §7, In-kernel stamps; the build's run time is not
-// quoted, only the shares).
-#ifdef QE_PSTEP_STAMPS
-#define QE_STAMP(acc, k, prev)                                                            \
-  do {                                                                                    \
-    uint64_t t_;                                                                          \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    acc[k] += t_ - prev;                                                                  \
-    prev = t_;                                                                            \
-  } while (0)
-#else
-#define QE_STAMP(acc, k, prev) \
-  do {                         \
-  } while (0)
-#endif
-constexpr int kStampN = 9;
 
 // WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
 // (21 KB at S = 5) would allow one 4-wave block per CU
@@ -681,11 +608,6 @@ k_progress_step(PArgs a) {
   uint32_t n_groups = 0, n_adv = 0, n_viol = 0, n_read = 0;
   uint64_t sum_c = 0, csum = 0;
   Acct<ACCT> ac;
-#ifdef QE_PSTEP_STAMPS
-  uint64_t stamp[kStampN] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t tprev;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
-#endif
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave =
       static_cast<uint64_t>(blockIdx.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -698,31 +620,11 @@ k_progress_step(PArgs a) {
   // phase 2) and the group's term runs once a slot needs them
   __shared__ uint64_t l_mix[WPB][S][2][64];
   __shared__ uint64_t l_run[WPB][RM][2][64];
-  // DR: a touched peer's ring (row form, low words) arrives by LDS-DMA with
-  // its slot's prefetch, one slot ahead, so it is no round trip of its own;
-  // one buffer per wave (read into registers before the next slot's DMA).
-  // Not with the 8/16-run tables: their LDS would cost resident blocks.
-  constexpr bool DR = RM <= 4 && QE_PSTEP_RING_DMA;
-  __shared__ u32x4 l_ring[DR ? WPB : 1][2][64];
   const uint32_t wv = threadIdx.x >> 6;
-  const bool dr = DR && row_ring;  // wave-uniform
-  // the DMA of slot s's ring for the lanes in `want` (before the slot's
-  // Progress loads: their arrival then implies the ring's)
-  auto ring_dma = [&](uint64_t g0, uint32_t n, uint32_t s, bool want) {
-    if (!dr || !__builtin_amdgcn_ballot_w64(want)) return;
-    const uint64_t rb = (static_cast<uint64_t>(s) * a.stride + g0) * a.FP;
-    const uint32_t off = want ? lane * a.FP * 4 : kOOB;
-    lds_dma16(a.ilo + rb, n * a.FP * 4, &l_ring[DR ? wv : 0][0][0], off);
-    if (a.FP > 4) lds_dma16(a.ilo + rb, n * a.FP * 4, &l_ring[DR ? wv : 0][1][0], off + 16);
-  };
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
     const bool live = lane < n;
-    QE_STAMP(stamp, 7, tprev);  // the previous tile's tail
-#ifdef QE_PSTEP_STAMPS
-    stamp[8] += 1;
-#endif
     uint32_t nr = 0;
     // ---- round trip 1: per group; message type and Match per slot ----
     const uint32_t mi =
@@ -832,7 +734,6 @@ k_progress_step(PArgs a) {
     PB cur;
     {  // slot 0, before phase 1: every possible event
       const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
-      ring_dma(g0, n, 0, ld);
       pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
               (rcm & 1u) != 0, cur);
     }
@@ -859,7 +760,6 @@ k_progress_step(PArgs a) {
       }
     }
     pb_ready(cur);  // (so no wait at the slot loop's head merges in the stores)
-    QE_STAMP(stamp, 0, tprev);  // round trips 1-2 and phase 1
     // ---- phase 2: every peer's event sequence ----
     PSend x;
     x.F = F;
@@ -883,23 +783,8 @@ k_progress_step(PArgs a) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const uint32_t tt = ty_of(s);
       const bool touched = ((tchm >> s) & 1u) != 0;
-      // this slot's ring from LDS (its DMA preceded cur's loads), into
-      // registers before the next slot's DMA reuses the buffer
-      uint32_t dlo[kRingChunk];
-#pragma unroll
-      for (int k = 0; k < kRingChunk; k++) dlo[k] = 0;
-      if (dr && __builtin_amdgcn_ballot_w64(touched)) {
-        const u32x4 a0 = lds_after(&l_ring[DR ? wv : 0][0][0], lane, cur.w);
-        dlo[0] = a0.x, dlo[1] = a0.y, dlo[2] = a0.z, dlo[3] = a0.w;
-        if (a.FP > 4) {
-          const u32x4 a1 = lds_after(&l_ring[DR ? wv : 0][1][0], lane, cur.w);
-          dlo[4] = a1.x, dlo[5] = a1.y, dlo[6] = a1.z, dlo[7] = a1.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      PB nxt;
+      PB nxt{};  // (the last slot has no next: zeros)
       if (s + 1 < static_cast<uint32_t>(S)) {
-        ring_dma(g0, n, s + 1, ((tchm >> (s + 1)) & 1u) != 0);
         pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
                 ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
                 ((rcm >> (s + 1)) & 1u) != 0, nxt);
@@ -911,7 +796,6 @@ k_progress_step(PArgs a) {
         if (a.msg_count) bst8(0u, mk_rsrc(a.msg_count + row, n), lane);
         ac.add(live && a.msg_count, 1);
         if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
-        QE_STAMP(stamp, 6, tprev);
         continue;
       }
       ac.add(touched, 12);  // Next + the packed word
@@ -946,9 +830,7 @@ k_progress_step(PArgs a) {
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
       if (row_ring) {
-        const bool rl = touched && c_old > 0 && !(QE_PSTEP_PROBE & 2);
-        if constexpr (DR) ring_load_row<true>(x, rl, rep0, a.FP, dlo, rlo, rhi);
-        else ring_load_row<false>(x, rl, rep0, a.FP, dlo, rlo, rhi);
+        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi);
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
@@ -981,9 +863,7 @@ k_progress_step(PArgs a) {
       uint32_t k2 = 0;
       bool lp = false;
       pb_ready(nxt);  // (before the sends: in memory form they append in memory)
-      QE_STAMP(stamp, 1, tprev);  // the slot's loads (Progress, ring, run table)
-      if (!(QE_PSTEP_PROBE & 36) && __builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
-      QE_STAMP(stamp, 2, tprev);  // the bcasts before the peer's message
+      if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
@@ -1098,21 +978,16 @@ k_progress_step(PArgs a) {
           }
         }
       }
-      QE_STAMP(stamp, 3, tprev);  // the message handler
       // After an accept: its sendAppend (sendIfEmpty), then the loop; the
       // later bcasts follow the loop.  Otherwise the message's sendAppend
       // and the later bcasts are consecutive sendIfEmpty sends: one burst.
       const uint32_t km = lp ? kLoop : k2 + k3;
-      if (!(QE_PSTEP_PROBE & 4)) {
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
-      if (!(QE_PSTEP_PROBE & 64) && __builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      }
-      QE_STAMP(stamp, 4, tprev);  // the message's sends, the send loop, later bcasts
-      if (row_ring && !(QE_PSTEP_PROBE & 9)) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
-      QE_STAMP(stamp, 5, tprev);  // the ring write-back
+      if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
+      if (row_ring) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
-      const bool tw = touched && !(QE_PSTEP_PROBE & 17);
+      const bool tw = touched;
       const bool wm = tw && up, wn = tw && p.next != cur.nx;
       const bool wp = tw && (p.pending != pd0 || p.reset);
       const bool ww = tw && nw != cur.w;
@@ -1138,7 +1013,6 @@ k_progress_step(PArgs a) {
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
       if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
-      QE_STAMP(stamp, 6, tprev);  // the peer's Progress stores and outputs
     }
     const uint32_t bc = popc(bset);
     bst64(c, r_commit, c != c0 ? o8 : kOOB);
@@ -1210,13 +1084,6 @@ k_progress_step(PArgs a) {
     block_stats_add<P_N, 64 * WPB>(cnt, idx, a.stats);
   }
   acct_flush<ACCT>(ac, a.acct);
-#ifdef QE_PSTEP_STAMPS
-  QE_STAMP(stamp, 7, tprev);
-  if (lane == 0 && a.acct)
-    for (int k = 0; k < kStampN; k++)
-      atomicAdd(reinterpret_cast<unsigned long long *>(a.acct + k),
-                static_cast<unsigned long long>(stamp[k]));
-#endif
 }
 
 // qe_progress_send: raft.sendAppend / maybeSendAppend(to, send_if_empty)

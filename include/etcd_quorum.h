@@ -778,7 +778,18 @@ size_t qe_comm_id_bytes(void);                 /* size of the id (128) */
 int qe_comm_unique_id(void *id);               /* rank 0: new id (host) */
 int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id,
                  int device);
+/* qe_comm_init with a bound (ABI 6): the communicator is created
+ * non-blocking and polled; when the other ranks have not joined after
+ * timeout_ms (e.g. one of them failed before calling init) it is aborted and
+ * QE_ECOMM returned, so no rank waits forever.  timeout_ms == 0: blocking,
+ * as qe_comm_init.  Hosts then agree over their own transport on the path
+ * every rank takes (bench.py Dist._select_stats_path). */
+int qe_comm_init_timeout(void **comm, uint32_t nranks, uint32_t rank, const void *id,
+                         int device, uint32_t timeout_ms);
 int qe_comm_destroy(void *comm);
+/* ncclCommAbort (ABI 6): frees the communicator without waiting for its
+ * outstanding collectives -- the way out when a peer failed mid-run. */
+int qe_comm_abort(void *comm);
 
 /* stats[0..n) (DEVICE, n <= QE_STATS_WORDS; normally the QE_STATS_COUNTERS
  * words qe_stats_reduce produced) = elementwise sum over all ranks of comm,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Timing variant of libetcd_quorum.so where only the S = 5 Progress objects
 # are rebuilt with extra flags (the bench's Progress workloads run S = 5):
-#   scripts/build_variant5.sh NAME "-DQE_PSTEP_PROBE=1"
+#   scripts/build_variant5.sh NAME "-DQE_PSTEP_WAVES=4"
 # OBJS="qe_inst_5 qe_inst_6" rebuilds those objects instead.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)

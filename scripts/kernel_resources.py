@@ -4,6 +4,7 @@ the code objects inside the in-tree objects (etcd_amd/build/*.o: the
 .hip_fatbin section, unbundled for gfx950, its AMDGPU metadata note).
 
   python scripts/kernel_resources.py [pattern ...]  -> profiles/kernel_resources.json
+  QE_KR_OUT=profiles/x.json python scripts/kernel_resources.py PATTERN  -> another file
 
 Waves per SIMD (gfx950, wave64): min(8, 512 // vgpr_alloc) with VGPRs+AGPRs
 allocated in granules of 8, and the LDS bound: floor(160 KiB / LDS per
@@ -88,7 +89,7 @@ def main():
             for mangled, dem in zip(ks, demangle(list(ks))):
                 if any(p in dem for p in pats):
                     res[dem] = dict(ks[mangled], object=os.path.basename(obj))
-    path = os.path.join(ROOT, "profiles", "kernel_resources.json")
+    path = os.path.join(ROOT, os.environ.get("QE_KR_OUT", "profiles/kernel_resources.json"))
     with open(path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(f"{len(res)} kernels -> {path}")

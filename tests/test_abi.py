@@ -184,6 +184,10 @@ def test_comm_argument_errors_without_gpu():
     assert L.qe_comm_init(C.byref(comm), 2, 2, idb, 0) == _lib.QE_EINVAL  # rank >= nranks
     assert L.qe_comm_init(C.byref(comm), 1, 0, None, 0) == _lib.QE_EINVAL
     assert L.qe_comm_destroy(None) == _lib.QE_EINVAL
+    assert L.qe_comm_abort(None) == _lib.QE_EINVAL
+    assert L.qe_comm_init_timeout(None, 1, 0, idb, 0, 1000) == _lib.QE_EINVAL
+    assert L.qe_comm_init_timeout(C.byref(comm), 2, 2, idb, 0, 1000) == _lib.QE_EINVAL
+    assert L.qe_comm_init_timeout(C.byref(comm), 1, 0, None, 0, 1000) == _lib.QE_EINVAL
     assert L.qe_allreduce_stats(None, 16, C.c_void_p(64), None) == _lib.QE_EINVAL
     assert L.qe_allreduce_stats(C.c_void_p(64), 16, None, None) == _lib.QE_EINVAL
     assert L.qe_allreduce_stats(C.c_void_p(64), 0, C.c_void_p(64), None) == _lib.QE_EINVAL

@@ -48,3 +48,36 @@ def test_allreduce_stats_world_size_one(eng):
         assert int(eng.stats_dict(folded)["groups"]) == 100_000
     finally:
         eng.check("qe_comm_destroy", L.qe_comm_destroy(comm))
+
+
+def test_bounded_init_world_size_one(eng):
+    """qe_comm_init_timeout (non-blocking communicator, polled): world size 1
+    joins at once; the all-reduce on that communicator waits for its enqueue
+    (ncclInProgress) and sums like the blocking one; qe_comm_abort frees it."""
+    L = eng._lib.lib()
+    idb = (C.c_uint8 * L.qe_comm_id_bytes())()
+    eng.check("qe_comm_unique_id", L.qe_comm_unique_id(idb))
+    comm = C.c_void_p()
+    eng.check("qe_comm_init_timeout", L.qe_comm_init_timeout(C.byref(comm), 1, 0, idb, 0, 60_000))
+    try:
+        x = torch.tensor([5, -3] + [0] * 14, dtype=torch.int64, device=DEV)
+        y = x.clone()
+        eng.check("qe_allreduce_stats", L.qe_allreduce_stats(eng._ptr(y), 16, comm,
+                                                              eng._stream(y.device)))
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+    finally:
+        eng.check("qe_comm_abort", L.qe_comm_abort(comm))
+
+
+def test_bounded_init_times_out_when_peers_never_join(eng):
+    """A 2-rank communicator whose second rank never calls init: the bound
+    ends the wait with QE_ECOMM instead of hanging (the case bench.py's
+    agreement step exists for)."""
+    L = eng._lib.lib()
+    idb = (C.c_uint8 * L.qe_comm_id_bytes())()
+    eng.check("qe_comm_unique_id", L.qe_comm_unique_id(idb))
+    comm = C.c_void_p()
+    rc = L.qe_comm_init_timeout(C.byref(comm), 2, 0, idb, 0, 3000)
+    assert rc == eng._lib.QE_ECOMM
+    assert not comm.value
