@@ -78,6 +78,11 @@ WORKLOADS = {
     "progress_send": ("16M groups x bcastAppend after a proposal (qe_progress_send to the 4 "
                       "followers, StateReplicate, Inflights F=8 with room): one MsgApp and one "
                       "ring entry per peer", 1 << 24, 5, "psend"),
+    "propose": ("16M groups x one MsgProp of 3 entries (24 B of payload) through qe_propose: the "
+                "MsgProp gates, increaseUncommittedSize, appendEntry (lastIndex + 3, the leader's "
+                "MaybeUpdate, maybeCommit) and bcastAppend to the 4 followers (StateReplicate, "
+                "Inflights F=8 with room, noLimit MaxSizePerMsg): one MsgApp and one ring entry "
+                "each", 1 << 24, 5, "propose"),
     "check_quorum": ("16M groups x 5 peers: MsgCheckQuorum on the leader over the resident "
                      "Progress words (QuorumActive over RecentActive, step-down mask, "
                      "RecentActive reset; each follower active with p = 0.7)", 1 << 24, 5, "cq"),
@@ -620,6 +625,50 @@ def setup(name, G, S, kind, d, stats):
                          lib.qe_progress_step(C.byref(p_), C.byref(m_), sp, stream))
 
         return step, bpg, G, "group-rounds", {"ps": ps, "msgs": msgs, "prepare": prepare}
+    if kind == "propose":
+        # stepLeader MsgProp -> appendEntry -> bcastAppend (raft/raft.go:
+        # 1019-1076, :621-642, :515-522) on the progress_send state, the
+        # leader in slot 0; every group proposes 3 entries each launch
+        F = 8
+        ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, extras=("self_slot",),
+                                  max_ents=0)
+        psend_state(ps)
+        ps.self_slot.fill_(0)
+        ps.term_start.copy_(ps.last_index)  # the leader's term started at its last entry
+        pr = engine.Proposals(ps, max_uncommitted=1 << 30)
+        pr.num_entries.fill_(3)
+        pr.payload.fill_(24)
+        pr.uncommitted_size.fill_(100)
+        mutable = ("match", "next", "peer", "committed", "last_index")
+        pristine = {k: getattr(ps, k).clone() for k in mutable}
+        unc0 = pr.uncommitted_size.clone()
+
+        def prepare():
+            for k in mutable:
+                getattr(ps, k).copy_(pristine[k])
+            pr.uncommitted_size.copy_(unc0)
+
+        # algorithmic bytes: the instrumented variant counts every field
+        # the reference logic reads or writes once (the
+        # oracle's count is equal, tests/test_gpu_propose.py)
+        prepare()
+        bpg = engine.propose_bytes_requested(ps, pr) / G
+        prepare()
+        import ctypes as C
+        p_, q_ = ps.struct(), pr.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            engine.check("qe_propose", lib.qe_propose(C.byref(p_), C.byref(q_), sp, stream))
+
+        def verify():
+            return bool((pr.result == 1).all())
+
+        return step, bpg, G, "group-proposals", {"ps": ps, "pr": pr, "prepare": prepare,
+                                                 "verify": verify}
+
     if kind == "psend":
         # raft.appendEntry -> bcastAppend (raft/raft.go:515-522, :432-492):
         # every follower in StateReplicate with room in its Inflights gets one

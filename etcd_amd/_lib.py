@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 5
+QE_ABI_VERSION = 6
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -118,6 +118,19 @@ class QePeerMsgs(C.Structure):
                 ("term_commit_index", vp)]
 
 
+class QeProposals(C.Structure):  # ABI 6
+    _fields_ = [("num_entries", vp), ("payload", vp), ("max_cc", u32), ("flags", u32),
+                ("cc_stride", u64), ("cc_count", vp), ("cc_pos", vp), ("cc_leave", vp),
+                ("cc_size", vp), ("applied", vp), ("pending_conf_index", vp),
+                ("uncommitted_size", vp), ("max_uncommitted", u64), ("result", vp),
+                ("cc_refused", vp), ("sent", vp), ("snap", vp), ("bytes_requested", vp)]
+
+
+QE_PROP_NONE, QE_PROP_OK, QE_PROP_DROPPED_NOT_MEMBER, QE_PROP_DROPPED_TRANSFER, \
+    QE_PROP_DROPPED_SIZE = 0, 1, 2, 3, 4
+QE_PROP_MAX_CC = 8
+QE_PROP_APPEND_ONLY = 1
+
 QE_PR_PROBE, QE_PR_REPLICATE, QE_PR_SNAPSHOT = 0, 1, 2
 QE_PF_STATE, QE_PF_PROBE_SENT, QE_PF_RECENT_ACTIVE = 3, 4, 8
 QE_PW_START_SHIFT, QE_PW_COUNT_SHIFT = 8, 16
@@ -193,6 +206,7 @@ PROTOTYPES = {
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp]),
     "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
     "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp, vp]),
+    "qe_propose": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeProposals), vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),

@@ -460,6 +460,44 @@ int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_em
   return dispatch_progress(p->num_slots, a, 1, false, false, static_cast<hipStream_t>(stream));
 }
 
+int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, void *stream) {
+  PArgs a;
+  int rc = progress_args(p, a);
+  if (rc) return rc;
+  if (!prop || (prop->flags & ~QE_PROP_APPEND_ONLY)) return QE_EINVAL;
+  if (prop->max_cc > QE_PROP_MAX_CC) return QE_ERANGE;
+  if (p->num_groups == 0) return QE_OK;
+  if (!prop->num_entries || !prop->result) return QE_EINVAL;
+  if (prop->max_cc && (!prop->cc_count || !prop->cc_pos || !prop->cc_leave || !prop->cc_size ||
+                       !prop->applied || !prop->pending_conf_index ||
+                       prop->cc_stride < p->num_groups))
+    return QE_EINVAL;
+  if (!prop->uncommitted_size && prop->max_uncommitted) return QE_EINVAL;
+  a.prop_n = prop->num_entries;
+  a.prop_payload = prop->payload;
+  const bool append_only = (prop->flags & QE_PROP_APPEND_ONLY) != 0;
+  a.max_cc = append_only ? 0u : prop->max_cc;
+  a.prop_flags = prop->flags;
+  a.cc_stride = prop->cc_stride;
+  a.cc_count = prop->cc_count;
+  a.cc_pos = prop->cc_pos;
+  a.cc_leave = prop->cc_leave;
+  a.cc_size = prop->cc_size;
+  a.applied = prop->applied;
+  a.pci = prop->pending_conf_index;
+  a.unc = prop->uncommitted_size;
+  a.max_unc = prop->max_uncommitted;
+  a.prop_result = prop->result;
+  a.cc_refused = prop->cc_refused;
+  a.sent = prop->sent;
+  a.snap = prop->snap;
+  a.acct = prop->bytes_requested;
+  a.last_index_rw = const_cast<uint64_t *>(p->last_index);
+  a.stats = stats;
+  return dispatch_progress(p->num_slots, a, prop->bytes_requested ? 6 : 5, p->inc_mask != nullptr,
+                           p->out_mask != nullptr, static_cast<hipStream_t>(stream));
+}
+
 int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
                   uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream) {
   if (!p) return QE_EINVAL;

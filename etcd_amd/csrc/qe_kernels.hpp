@@ -741,6 +741,18 @@ struct PArgs {
   uint32_t chunk;  // k_progress_send: tiles per wave chunk
   // check quorum
   uint8_t *qactive;
+  // propose (qe_propose, ABI 6)
+  const uint32_t *prop_n;
+  const uint64_t *prop_payload;
+  uint32_t max_cc, prop_flags;
+  uint64_t cc_stride;
+  const uint8_t *cc_count, *cc_leave;
+  const uint32_t *cc_pos, *cc_size;
+  const uint64_t *applied;
+  uint64_t *pci, *unc;
+  uint64_t max_unc;
+  uint8_t *prop_result, *cc_refused;
+  uint64_t *last_index_rw;
 };
 
 struct PR {
@@ -829,6 +841,7 @@ __device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t i
 }
 
 enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_READ, P_CSUM, P_N };
+enum { Q_GROUPS, Q_SUM, Q_ADV, Q_CSUM, Q_N };  // k_propose
 
 // k_progress_step: qe_progress.hpp
 

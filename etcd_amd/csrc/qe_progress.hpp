@@ -1208,6 +1208,241 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
   }
 }
 
+// qe_propose (ABI 6): MsgProp on every group's leader (stepLeader,
+// raft/raft.go:1019-1076), appendEntry (:621-642) and the bcastAppend that
+// follows (:515-522).  One lane per group, a wave per 64-group tile: the
+// proposal, the gates (no Progress of its own, a transfer in progress, the
+// conf-change refusals against pendingConfIndex / the joint state, the
+// uncommitted-size limit), then for the groups that append every slot's
+// Match (Committed) and the tracked slots' Next and word in one batch of
+// loads, the leader's own MaybeUpdate(lastIndex) and maybeCommit in
+// registers, and one sendAppend per other tracked peer (memory-form ring
+// append, as qe_progress_send).  Proposals arrive as a batch and a group
+// appends once per launch, so a launch is one MsgProp per group.
+constexpr uint64_t kPropSalt = 0x9E6C63D0676A9A99ull;
+
+template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT>
+__global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr uint32_t MB = sizeof(MT);
+  uint64_t cnt[Q_N] = {0, 0, 0, 0};
+  Acct<ACCT> ac;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  const uint64_t maxu = a.max_unc ? a.max_unc : ~0ull;  // 0 = noLimit
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = t * 64;
+    const uint32_t n = tile_n(a.G, t);
+    const bool live = lane < n;
+    const uint32_t o8 = lane * 8, o4 = lane * 4;
+    const uint32_t ne = bld32(mk_rsrc(a.prop_n + g0, n * 4), o4);
+    const bool prop = ne != 0;
+    // lastIndex and committed of every group (the checksum covers them)
+    const rsrc_t r_li = mk_rsrc(a.last_index_rw + g0, n * 8), r_c = mk_rsrc(a.committed + g0, n * 8);
+    uint64_t li = bld64(r_li, o8);
+    const uint64_t c0 = bld64(r_c, o8);
+    uint64_t c = c0;
+    ac.add(live, 4);
+    uint32_t res = QE_PROP_NONE, refused = 0, sentm = 0, snapm = 0;
+    if (__builtin_amdgcn_ballot_w64(prop)) {
+      const uint32_t trk =
+          a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * MB), lane) & kFull)
+                    : kFull;
+      const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
+      const uint32_t ltr = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), lane) : 0xFFu;
+      const uint32_t mi =
+          MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * MB), lane) & kFull)
+                 : kFull;
+      const uint32_t mo =
+          JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * MB), lane) & kFull)
+                : 0u;
+      ac.add(prop, (a.self_slot ? 1 : 0) + (a.tracked ? MB : 0) + (a.transferee ? 1 : 0));
+      const bool member = self < static_cast<uint32_t>(S) && ((trk >> self) & 1u) != 0;
+      // (appendEntry alone skips the MsgProp gates but needs the leader's
+      // Progress: the reference's MaybeUpdate on a missing one panics)
+      const bool app_only = (a.prop_flags & QE_PROP_APPEND_ONLY) != 0;
+      res = !prop ? QE_PROP_NONE
+                  : (!member ? QE_PROP_DROPPED_NOT_MEMBER
+                             : ((!app_only && ltr < static_cast<uint32_t>(S)) ? QE_PROP_DROPPED_TRANSFER
+                                                                              : QE_PROP_OK));
+      const bool go = res == QE_PROP_OK;
+      uint64_t sz = a.prop_payload ? bld64(mk_rsrc(a.prop_payload + g0, n * 8), go ? o8 : kOOB) : 0;
+      ac.add(go, (a.prop_payload ? 8 : 0) + (a.max_cc ? 1 : 0));
+      // conf-change entries (:1034-1072): refused ones become empty
+      // EntryNormal entries (no payload), an accepted one sets
+      // pendingConfIndex to its index
+      uint32_t ncc = a.max_cc ? bld8(mk_rsrc(a.cc_count + g0, n), go ? lane : kOOB) : 0u;
+      ncc = ncc < a.max_cc ? ncc : a.max_cc;
+      bool out_counted = false;
+      if (__builtin_amdgcn_ballot_w64(ncc > 0)) {
+        const bool cl = ncc > 0;
+        const rsrc_t r_pci = mk_rsrc(a.pci + g0, n * 8);
+        uint64_t pci = bld64(r_pci, cl ? o8 : kOOB);
+        const uint64_t pci0 = pci;
+        const uint64_t applied = bld64(mk_rsrc(a.applied + g0, n * 8), cl ? o8 : kOOB);
+        const bool joint = mo != 0u;  // len(Voters[1]) > 0
+        ac.add(cl, (a.out ? MB : 0) + 16);
+        out_counted = cl && a.out != nullptr;
+        for (uint32_t k = 0; k < a.max_cc; k++) {
+          const bool on = k < ncc;
+          if (!__builtin_amdgcn_ballot_w64(on)) break;
+          const uint64_t row = static_cast<uint64_t>(k) * a.cc_stride + g0;
+          const uint32_t pos = bld32(mk_rsrc(a.cc_pos + row, n * 4), on ? o4 : kOOB);
+          const bool leave = bld8(mk_rsrc(a.cc_leave + row, n), on ? lane : kOOB) != 0;
+          const uint32_t csz = bld32(mk_rsrc(a.cc_size + row, n * 4), on ? o4 : kOOB);
+          ac.add(on, 9);
+          if (on) {
+            const bool pending = pci > applied;  // alreadyPending
+            if (pending || (joint && !leave) || (!joint && leave)) {
+              refused |= 1u << k;
+            } else {
+              pci = li + pos + 1;
+              sz += csz;
+            }
+          }
+        }
+        const bool wpci = cl && pci != pci0;
+        bst64(pci, r_pci, wpci ? o8 : kOOB);
+        ac.add(wpci, 8);
+      }
+      // appendEntry -> increaseUncommittedSize (:1761-1779)
+      const rsrc_t r_unc = opt_rsrc(a.unc, g0, n);
+      const uint64_t us = bld64(r_unc, go ? o8 : kOOB);
+      ac.add(go && a.unc, 8);
+      const bool drop = go && us > 0 && sz > 0 && us + sz > maxu;
+      res = drop ? QE_PROP_DROPPED_SIZE : res;
+      const bool ok = go && !drop;
+      bst64(us + sz, r_unc, (ok && sz) ? o8 : kOOB);
+      ac.add(ok && a.unc && sz, 8);
+      const uint64_t li2 = li + ne;  // raftLog.append
+      bst64(li2, r_li, ok ? o8 : kOOB);
+      ac.add(ok, 16 + 8 + 8 + (app_only ? 0 : 8 + (a.snap_index ? 8 : 0)) + (MASKED ? MB : 0) +
+                     ((JOINT && !out_counted) ? MB : 0));
+      if (__builtin_amdgcn_ballot_w64(ok)) {
+        const uint32_t k8 = ok ? o8 : kOOB;
+        const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), k8);
+        const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), k8);
+        const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
+        uint64_t mt[S], nx[S];
+        uint32_t pw[S];
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+          const bool ld = ok && ((trk >> s) & 1u) && (!app_only || self == static_cast<uint32_t>(s));
+          mt[s] = bld64(mk_rsrc(a.match + row, n * 8), k8);
+          nx[s] = bld64(mk_rsrc(a.next + row, n * 8), ld ? o8 : kOOB);
+          pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), ld ? o4 : kOOB);
+        }
+        ac.add(ok, 8 * S + 12);  // every Match; the leader's Next + word
+        // Progress[r.id].MaybeUpdate(lastIndex) (progress.go:144-153)
+        uint64_t sm = 0, sx = 0;
+        uint32_t sw = 0;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          const bool is = self == static_cast<uint32_t>(s);
+          sm = is ? mt[s] : sm;
+          sx = is ? nx[s] : sx;
+          sw = is ? pw[s] : sw;
+        }
+        PR ps;
+        ps.match = sm;
+        ps.next = sx;
+        pr_unpack(ps, sw);
+        const bool up = sm < li2;
+        if (up) {
+          ps.match = li2;
+          ps.probe_sent = 0;
+        }
+        if (ps.next < li2 + 1) ps.next = li2 + 1;
+        const uint32_t nws = pr_pack(ps);
+        // maybeCommit (raft.go:585-588, log.go:325-331)
+        uint64_t vals[S];
+#pragma unroll
+        for (int s = 0; s < S; s++) vals[s] = self == static_cast<uint32_t>(s) ? ps.match : mt[s];
+        const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
+        if (ok && mci > c && mci >= ts && mci <= li2) c = mci;
+        // bcastAppend: one sendAppend per other tracked peer; the leader's
+        // own slot takes its MaybeUpdate in the same row stores
+        PSend x;
+        x.F = a.F;
+        x.me = a.max_ents;
+        x.fi = fi;
+        x.li = li2;
+        x.snap = sn;
+        x.lb = lane * a.FP * 4;
+        x.row = false;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+          const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+          const bool is_self = ok && self == static_cast<uint32_t>(s);
+          const bool tgt = ok && !app_only && ((trk >> s) & 1u) && self != static_cast<uint32_t>(s);
+          PR p;
+          p.match = mt[s];
+          p.next = nx[s];
+          pr_unpack(p, pw[s]);
+          p.pending = 0;
+          p.reset = 0;
+          {
+            const uint64_t rb = row * a.FP;
+            x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
+            x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+          }
+          x.count_msgs = 0;
+          x.first_index = 0;
+          x.snapped = false;
+          PRun run{0, 0, 0};
+          if (__builtin_amdgcn_ballot_w64(tgt)) send_burst<ACCT>(p, true, tgt ? 1u : 0u, x, run, ac);
+          const uint32_t nw = pr_pack(p);
+          const bool wn = tgt && p.next != nx[s], ww = tgt && nw != pw[s], wp = tgt && x.snapped;
+          const bool sn_ = is_self && ps.next != sx, sw_ = is_self && nws != sw;
+          if (__builtin_amdgcn_ballot_w64(is_self && up))
+            bst64(ps.match, mk_rsrc(a.match + row, n * 8), (is_self && up) ? o8 : kOOB);
+          if (__builtin_amdgcn_ballot_w64(wn || sn_))
+            bst64(is_self ? ps.next : p.next, mk_rsrc(a.next + row, n * 8), (wn || sn_) ? o8 : kOOB);
+          if (__builtin_amdgcn_ballot_w64(ww || sw_))
+            bst32(is_self ? nws : nw, mk_rsrc(a.pw + row, n * 4), (ww || sw_) ? o4 : kOOB);
+          if (__builtin_amdgcn_ballot_w64(wp))
+            bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
+          ac.add(tgt, 12);
+          ac.add(wn, 8);
+          ac.add(tgt && ((nw ^ pw[s]) & ~QE_PW_RING_MASK) != 0, 4);
+          ac.add(wp, 8);
+          ac.add(is_self && up, 8);
+          ac.add(sn_, 8);
+          ac.add(is_self && ((nws ^ sw) & ~QE_PW_RING_MASK) != 0, 4);
+          sentm |= (tgt && x.count_msgs) ? (1u << s) : 0u;
+          snapm |= (tgt && x.snapped) ? (1u << s) : 0u;
+        }
+        bst64(c, r_c, c != c0 ? o8 : kOOB);
+        ac.add(c != c0, 8);
+        li = ok ? li2 : li;
+      }
+    }
+    bst8(res, mk_rsrc(a.prop_result + g0, n), lane);
+    if (a.cc_refused) bst8(refused, mk_rsrc(a.cc_refused + g0, n), lane);
+    if (a.sent) bst_mask<MT>(sentm, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+    if (a.snap) bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+    ac.add(live, 1 + (a.cc_refused ? 1 : 0) + (a.sent ? MB : 0) + (a.snap ? MB : 0));
+    if (live) {
+      const uint64_t gh = (a.goff + g0 + lane) * kPhi;
+      cnt[Q_GROUPS] += 1;
+      cnt[Q_SUM] += c;
+      cnt[Q_ADV] += c != c0;
+      cnt[Q_CSUM] += mix64(gh ^ kPropSalt ^ (static_cast<uint64_t>(res) << 60) ^ li) +
+                     mix64(gh ^ c ^ (static_cast<uint64_t>(sentm) << 40));
+    }
+  }
+  if (a.stats) {
+    const int idx[Q_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
+                          QE_STAT_CHECKSUM};
+    block_stats_add<Q_N, kBlock>(cnt, idx, a.stats);
+  }
+  acct_flush<ACCT>(ac, a.acct);
+}
+
 // qe_check_quorum: MsgCheckQuorum (raft/raft.go:997-1018) over the resident
 // Progress words.  One lane per group; each wave owns a chunk of up to
 // kSendTPW tiles (as qe_progress_send): the chunk's masks (Voters[0] |

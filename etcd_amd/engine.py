@@ -376,10 +376,13 @@ class ProgressState:
         place (their ring representation bits are recomputed).  Without
         `ibuf`, rewritten peer words keep describing the resident rings: the
         rings are decoded with the old words and packed again with the new
-        ones (a new Inflights.start / count selects other live entries)."""
+        ones (a new Inflights.start / count selects other live entries) --
+        unless raw `ilo` / `ihi` words are passed too, which are then taken
+        as they are."""
         ibuf = arrays.pop("ibuf", None)
         fields = {k: arrays.pop(k) for k in ("flags", "istart", "icount") if k in arrays}
-        if ibuf is None and (fields or "peer" in arrays):
+        raw_rings = "ilo" in arrays or "ihi" in arrays  # the caller's ring words stand
+        if ibuf is None and not raw_rings and (fields or "peer" in arrays):
             ibuf = self.rings()  # decoded with the words in place now
         if fields:
             n = max(np.asarray(v).size for v in fields.values())
@@ -585,6 +588,68 @@ def check_quorum(ps, quorum_active=None, stats=None):
     check("qe_check_quorum", _lib.lib().qe_check_quorum(C.byref(p), _ptr(quorum_active),
                                                          _ptr(stats), _stream(ps.device)))
     return quorum_active
+
+
+class Proposals:
+    """One MsgProp per group for qe_propose (qe_proposals, ABI 6):
+    num_entries [G] (0 = none), payload [G] (sum of the non-conf-change
+    entries' PayloadSize), up to max_cc conf-change entries per proposal
+    ([max_cc][G]: position, leave-joint flag, size), applied /
+    pending_conf_index / uncommitted_size [G], and the outputs result,
+    cc_refused, sent, snap [G]."""
+
+    def __init__(self, ps, max_cc=0, max_uncommitted=0, track_uncommitted=True, flags=0):
+        G, dev = ps.G, ps.device
+        self.G, self.max_cc, self.max_uncommitted = G, int(max_cc), int(max_uncommitted)
+        self.flags = int(flags)  # QE_PROP_APPEND_ONLY: appendEntry alone
+        i64 = torch.int64
+        self.num_entries = torch.zeros(G, dtype=torch.int32, device=dev)
+        self.payload = torch.zeros(G, dtype=i64, device=dev)
+        c = max(1, self.max_cc)
+        self.cc_count = torch.zeros(G, dtype=torch.uint8, device=dev)
+        self.cc_pos = torch.zeros(c * G, dtype=torch.int32, device=dev)
+        self.cc_leave = torch.zeros(c * G, dtype=torch.uint8, device=dev)
+        self.cc_size = torch.zeros(c * G, dtype=torch.int32, device=dev)
+        self.applied = torch.zeros(G, dtype=i64, device=dev)
+        self.pending_conf_index = torch.zeros(G, dtype=i64, device=dev)
+        self.uncommitted_size = torch.zeros(G, dtype=i64, device=dev) if track_uncommitted else None
+        self.result = torch.zeros(G, dtype=torch.uint8, device=dev)
+        self.cc_refused = torch.zeros(G, dtype=torch.uint8, device=dev)
+        md = mask_torch_dtype(ps.S)
+        self.sent = torch.zeros(G, dtype=md, device=dev)
+        self.snap = torch.zeros(G, dtype=md, device=dev)
+        self.bytes_requested = None
+
+    def struct(self):
+        cc = self.max_cc > 0
+        return _lib.QeProposals(
+            _ptr(self.num_entries), _ptr(self.payload), self.max_cc, self.flags, self.G,
+            _ptr(self.cc_count) if cc else None, _ptr(self.cc_pos) if cc else None,
+            _ptr(self.cc_leave) if cc else None, _ptr(self.cc_size) if cc else None,
+            _ptr(self.applied), _ptr(self.pending_conf_index), _ptr(self.uncommitted_size),
+            self.max_uncommitted, _ptr(self.result), _ptr(self.cc_refused), _ptr(self.sent),
+            _ptr(self.snap), _ptr(self.bytes_requested))
+
+
+def propose(ps, props, stats=None):
+    """qe_propose: stepLeader's MsgProp + appendEntry + bcastAppend
+    (raft/raft.go:1019-1076, :621-642, :515-522) for every group with
+    num_entries > 0; advances ps.last_index."""
+    p, q = ps.struct(), props.struct()
+    check("qe_propose", _lib.lib().qe_propose(C.byref(p), C.byref(q), _ptr(stats),
+                                               _stream(ps.device)))
+
+
+def propose_bytes_requested(ps, props):
+    """The algorithmic bytes of one qe_propose launch (instrumented variant,
+    field granularity); mutates the state like propose."""
+    acct = torch.zeros(1, dtype=torch.int64, device=ps.device)
+    props.bytes_requested = acct
+    try:
+        propose(ps, props)
+    finally:
+        props.bytes_requested = None
+    return int(acct.item())
 
 
 class ConfState:

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 5  /* 5: see INTEGRATION.md "ABI 5" (layout changes listed there) */
+#define QE_ABI_VERSION 6  /* 6: see INTEGRATION.md "ABI 6" (changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -544,6 +544,82 @@ int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stat
  * outcome. */
 int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_empty,
                      void *sent, void *snap, void *stream);
+
+/* ---- MsgProp: appendEntry + bcastAppend (ABI 6) ------------------------- */
+
+/* qe_proposals.result */
+#define QE_PROP_NONE 0                /* no proposal for the group             */
+#define QE_PROP_OK 1                  /* appended and bcastAppend done          */
+#define QE_PROP_DROPPED_NOT_MEMBER 2  /* ErrProposalDropped: the leader has no
+                                         Progress of its own (raft.go:1023-1028) */
+#define QE_PROP_DROPPED_TRANSFER 3    /* ErrProposalDropped: leadership transfer
+                                         in progress (raft.go:1029-1032)       */
+#define QE_PROP_DROPPED_SIZE 4        /* ErrProposalDropped: the uncommitted
+                                         size limit (raft.go:627-633, 1761-1779) */
+#define QE_PROP_MAX_CC 8              /* conf-change entries per proposal      */
+/* qe_proposals.flags: appendEntry alone, as the reference calls it outside
+ * MsgProp (the auto-leave entry of advance, raft.go:555-569; tests'
+ * mustAppendEntry): no MsgProp gates except the leader's own Progress, no
+ * conf-change checks (max_cc ignored), no bcastAppend */
+#define QE_PROP_APPEND_ONLY 1u
+
+/* One MsgProp per group (a launch is one batch of proposals). */
+typedef struct qe_proposals {
+  const uint32_t *num_entries;   /* [G] len(m.Entries); 0 = no MsgProp         */
+  const uint64_t *payload;       /* [G] sum of PayloadSize (len(Data), util.go)
+                                    over the entries that are NOT conf
+                                    changes; NULL = all of them empty       */
+  uint32_t max_cc;               /* conf-change entries per proposal at most,
+                                    <= QE_PROP_MAX_CC (0: no conf changes)  */
+  uint32_t flags;                /* QE_PROP_APPEND_ONLY or 0                  */
+  uint64_t cc_stride;            /* >= num_groups                            */
+  const uint8_t *cc_count;       /* [G] conf-change entries of the proposal  */
+  const uint32_t *cc_pos;        /* [max_cc][cc_stride] position in m.Entries,
+                                    ascending, < num_entries                */
+  const uint8_t *cc_leave;       /* [max_cc][cc_stride] 1: a ConfChangeV2
+                                    without Changes (wantsLeaveJoint)        */
+  const uint32_t *cc_size;       /* [max_cc][cc_stride] its PayloadSize      */
+  const uint64_t *applied;       /* [G] raftLog.applied (read when a group has
+                                    conf-change entries)                    */
+  uint64_t *pending_conf_index;  /* [G] rw r.pendingConfIndex (ditto)        */
+  uint64_t *uncommitted_size;    /* [G] rw r.uncommittedSize; NULL = not
+                                    tracked (max_uncommitted must be 0)     */
+  uint64_t max_uncommitted;      /* Config.MaxUncommittedEntriesSize; 0 =
+                                    noLimit (raft.go:356-358)               */
+  uint8_t *result;               /* [G] out QE_PROP_*                         */
+  uint8_t *cc_refused;           /* [G] out (may be NULL): bit k = conf-change
+                                    entry k was refused and replaced by an
+                                    empty EntryNormal (raft.go:1063-1065)   */
+  void *sent;                    /* [G] out mask (may be NULL): peers sent a
+                                    MsgApp / MsgSnap by the bcastAppend     */
+  void *snap;                    /* [G] out mask (may be NULL): a MsgSnap     */
+  uint64_t *bytes_requested;     /* measurement aid, normally NULL: adds the
+                                    algorithmic bytes (DESIGN.md §3 rules)  */
+} qe_proposals;
+
+/* stepLeader's MsgProp arm (raft/raft.go:1019-1076) for every group with
+ * num_entries > 0, on the leader-side state p:
+ *   the leader has no Progress of its own (self_slot untracked) -> dropped;
+ *   a leadership transfer is in progress (lead_transferee < S) -> dropped;
+ *   each conf-change entry in order: refused (replaced by an empty
+ *     EntryNormal) when pendingConfIndex > applied, or it enters a change
+ *     while Voters[1] is non-empty, or it leaves a joint state that does not
+ *     exist; otherwise pendingConfIndex = its index (set even when the
+ *     proposal is then dropped for its size, as the reference does);
+ *   appendEntry (:621-642): increaseUncommittedSize -> dropped when the
+ *     uncommitted tail is non-empty, the proposal's payload is non-zero and
+ *     the sum would exceed max_uncommitted; else lastIndex += num_entries
+ *     (the entries take the leader's term: the log model's current run,
+ *     [term_start, last_index], grows), Progress[self].MaybeUpdate(lastIndex)
+ *     and maybeCommit (the term gate of qe_progress_step);
+ *   bcastAppend (:515-522): sendAppend (maybeSendAppend(to, true)) to every
+ *     tracked slot but self_slot, as qe_progress_send.
+ * Writes p->last_index (declared const in qe_progress because the other
+ * entry points only read it), p->committed, the leader's Match/Next/word and
+ * the peers' Next/word/PendingSnapshot/Inflights.  The reference's
+ * reduceUncommittedSize on apply (:544) stays with the host, which owns the
+ * applied entries.  stats: groups, commit sum, commit advanced, checksum. */
+int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, void *stream);
 
 /* ABI 4, HOST pointers: Inflights rings between plain uint64 buffers
  * (Inflights.buffer of each peer, raft/tracker/inflights.go:25-37, peer-major

@@ -62,6 +62,8 @@ def _declare(L):
         "orc_check_quorum_batch": (None, [C.POINTER(OrcProg), vp, vp]),
         "orc_read_index_batch": (None, [C.POINTER(OrcProg), vp, u32, vp, vp, vp]),
         "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
+        "orc_propose_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcProps), vp]),
+        "orc_checksum_prop": (u64, [u64, u32, u64, u64, u32]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
         "orc_pr_maybe_decr_to": (i32, [u32, vp, vp, u64, u64]),
@@ -181,6 +183,17 @@ class OrcMsgs(C.Structure):
                 ("msg_index", C.c_void_p), ("read_ctx", C.c_void_p),
                 ("read_released", C.c_void_p), ("term_commit", C.c_void_p),
                 ("term_commit_index", C.c_void_p), ("bytes", C.c_void_p)]
+
+
+class OrcProps(C.Structure):
+    """orc_props (oracle/quorum_oracle.c), the oracle's mirror of qe_proposals."""
+    _fields_ = [("num_entries", C.c_void_p), ("payload", C.c_void_p), ("max_cc", C.c_uint32),
+                ("flags", C.c_uint32), ("cc_stride", C.c_uint64), ("cc_count", C.c_void_p),
+                ("cc_pos", C.c_void_p), ("cc_leave", C.c_void_p), ("cc_size", C.c_void_p),
+                ("applied", C.c_void_p), ("pending_conf_index", C.c_void_p),
+                ("uncommitted_size", C.c_void_p), ("max_uncommitted", C.c_uint64),
+                ("result", C.c_void_p), ("cc_refused", C.c_void_p), ("sent", C.c_void_p),
+                ("snap", C.c_void_p), ("bytes", C.c_void_p)]
 
 
 PF_STATE, PF_PROBE_SENT, PF_RECENT_ACTIVE = 3, 4, 8
@@ -339,3 +352,42 @@ def check_quorum(pb, goff=0):
     s = pb.struct(goff)
     lib().orc_check_quorum_batch(C.byref(s), P(qa), P(stats))
     return qa, stats
+
+
+class ProposeOut:
+    def __init__(self, pb):
+        md = mask_dtype(pb.S)
+        self.result = np.zeros(pb.G, np.uint8)
+        self.cc_refused = np.zeros(pb.G, np.uint8)
+        self.sent = np.zeros(pb.G, md)
+        self.snap = np.zeros(pb.G, md)
+        self.stats = np.zeros(NSTAT, np.uint64)
+        self.bytes = np.zeros(1, np.uint64)
+
+
+def propose(pb, num_entries, payload=None, cc=None, applied=None, pending_conf_index=None,
+            uncommitted_size=None, max_uncommitted=0, goff=0, flags=0):
+    """MsgProp + appendEntry + bcastAppend on every group with
+    num_entries[g] > 0 (oracle).  cc: None or (max_cc, count[G],
+    pos[max_cc][G], leave[max_cc][G], size[max_cc][G]).  pending_conf_index
+    and uncommitted_size (uint64[G]) and pb are updated in place.  Returns
+    ProposeOut (o.bytes[0] = the algorithmic bytes).  flags 1: appendEntry
+    alone (QE_PROP_APPEND_ONLY)."""
+    o = ProposeOut(pb)
+    ne = np.ascontiguousarray(num_entries, np.uint32)
+    pl = None if payload is None else np.ascontiguousarray(payload, np.uint64)
+    if cc is None:
+        mc, cnt, pos, lv, sz = 0, None, None, None, None
+    else:
+        mc, cnt, pos, lv, sz = cc
+        cnt = np.ascontiguousarray(cnt, np.uint8)
+        pos = np.ascontiguousarray(pos, np.uint32)
+        lv = np.ascontiguousarray(lv, np.uint8)
+        sz = np.ascontiguousarray(sz, np.uint32)
+    ap = None if applied is None else np.ascontiguousarray(applied, np.uint64)
+    q = OrcProps(P(ne), P(pl), mc, flags, pb.G, P(cnt), P(pos), P(lv), P(sz), P(ap),
+                 P(pending_conf_index), P(uncommitted_size), max_uncommitted, P(o.result),
+                 P(o.cc_refused), P(o.sent), P(o.snap), P(o.bytes))
+    s = pb.struct(goff)
+    lib().orc_propose_batch(C.byref(s), C.byref(q), P(o.stats))
+    return o

@@ -1585,6 +1585,166 @@ void orc_progress_send_batch(const orc_prog *a, const void *want, uint32_t send_
   }
 }
 
+/* MsgProp on each group's leader (stepLeader, raft/raft.go:1019-1076), its
+ * appendEntry (:621-642) and the bcastAppend that follows (:515-522).  The
+ * proposal of group g is num_entries[g] entries; payload[g] = the sum of
+ * PayloadSize (len(Data), util.go) over the entries that are not conf
+ * changes; its conf-change entries are listed (position in m.Entries, a
+ * ConfChangeV2 without Changes = wantsLeaveJoint, PayloadSize).
+ * result: 0 no proposal, 1 appended + bcastAppend, 2 dropped (no Progress
+ * of its own, :1023-1028), 3 dropped (leadership transfer, :1029-1032),
+ * 4 dropped (increaseUncommittedSize, :627-633 / :1761-1779). */
+typedef struct orc_props {
+  const uint32_t *num_entries;
+  const uint64_t *payload;
+  uint32_t max_cc, flags;       /* flags 1: appendEntry alone (QE_PROP_APPEND_ONLY) */
+  uint64_t cc_stride;
+  const uint8_t *cc_count;
+  const uint32_t *cc_pos;
+  const uint8_t *cc_leave;
+  const uint32_t *cc_size;
+  const uint64_t *applied;
+  uint64_t *pending_conf_index;
+  uint64_t *uncommitted_size;
+  uint64_t max_uncommitted;     /* 0 = noLimit (raft.go:356-358) */
+  uint8_t *result;
+  uint8_t *cc_refused;
+  void *sent, *snap;
+  uint64_t *bytes;              /* byte accounting (DESIGN.md §3 rules), or NULL */
+} orc_props;
+
+uint64_t orc_checksum_prop(uint64_t gid, uint32_t result, uint64_t last_index, uint64_t committed,
+                           uint32_t sent) {
+  uint64_t h = gid * PHI;
+  return orc_mix64(h ^ 0x9E6C63D0676A9A99ull ^ ((uint64_t)result << 60) ^ last_index) +
+         orc_mix64(h ^ committed ^ ((uint64_t)sent << 40));
+}
+
+void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  uint64_t *last_index = (uint64_t *)a->last_index; /* appendEntry advances it */
+  uint64_t maxu = q->max_uncommitted ? q->max_uncommitted : UINT64_MAX;
+  uint64_t st[NSTAT];
+  memset(st, 0, sizeof(st));
+  uint64_t bytes = 0;
+  for (uint64_t g = 0; g < a->G; g++) {
+    uint32_t n = q->num_entries[g];
+    uint32_t res = 0, refused = 0, sentm = 0, snapm = 0;
+    uint64_t li = last_index[g], cm = a->committed[g], c0 = cm;
+    uint64_t B = 4;                                          /* num_entries */
+    int out_counted = 0;
+    if (n) {
+      uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+      uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+      uint32_t lt = a->lead_transferee ? a->lead_transferee[g] : 0xFFu;
+      B += (a->self_slot ? 1 : 0) + (a->tracked ? mb : 0) + (a->lead_transferee ? 1 : 0);
+      int app_only = (q->flags & 1u) != 0;                  /* appendEntry alone: no MsgProp gates, no bcast */
+      if (!(self < S && ((trk >> self) & 1u))) res = 2;      /* Progress[r.id] == nil */
+      else if (!app_only && lt < S) res = 3;                 /* leadTransferee != None */
+      else {
+        uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+        uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+        uint64_t s = q->payload ? q->payload[g] : 0;
+        uint32_t mcc = app_only ? 0 : q->max_cc;
+        B += (q->payload ? 8 : 0) + (mcc ? 1 : 0);
+        uint32_t ncc = mcc ? q->cc_count[g] : 0;
+        if (ncc > mcc) ncc = mcc;
+        if (ncc) {
+          uint64_t pci = q->pending_conf_index[g], pci0 = pci, applied = q->applied[g];
+          int joint = mo != 0;                               /* len(Voters[1]) > 0 */
+          B += (a->out ? mb : 0) + 16;                       /* out mask, applied, pendingConfIndex */
+          out_counted = a->out != NULL;
+          for (uint32_t k = 0; k < ncc; k++) {
+            uint64_t o = (uint64_t)k * q->cc_stride + g;
+            int leave = q->cc_leave[o] != 0;
+            B += 9;                                          /* position, kind, size */
+            int already_pending = pci > applied;
+            if (already_pending || (joint && !leave) || (!joint && leave)) {
+              refused |= 1u << k;                            /* -> pb.Entry{Type: EntryNormal} */
+            } else {
+              pci = li + q->cc_pos[o] + 1;
+              s += q->cc_size[o];
+            }
+          }
+          q->pending_conf_index[g] = pci;
+          B += pci != pci0 ? 8 : 0;
+        }
+        /* appendEntry -> increaseUncommittedSize (:1761-1779) */
+        uint64_t us = q->uncommitted_size ? q->uncommitted_size[g] : 0;
+        B += q->uncommitted_size ? 8 : 0;
+        if (us > 0 && s > 0 && us + s > maxu) {
+          res = 4;
+        } else {
+          res = 1;
+          if (q->uncommitted_size) {
+            q->uncommitted_size[g] = us + s;
+            B += s ? 8 : 0;
+          }
+          li += n;                                           /* raftLog.append */
+          last_index[g] = li;
+          B += 16 + 8 + 8 + (app_only ? 0 : 8 + (a->snap_index ? 8 : 0)); /* lastIndex rw, term_start, committed, firstIndex */
+          B += (a->inc ? mb : 0) + (a->out && !out_counted ? mb : 0);
+          orc_gctx c;
+          c.a = a;
+          c.m = NULL;
+          c.g = g;
+          c.fi = a->first_index[g];
+          c.li = li;
+          c.snap = a->snap_index ? a->snap_index[g] : c.fi - 1;
+          c.me = a->max_ents;
+          c.sent = c.snapm = 0;
+          orc_pr prs[16];
+          uint64_t vals[16];
+          for (uint32_t t = 0; t < S; t++) {
+            pr_load2(&prs[t], a, t, g);
+            B += 8;                                          /* Match (Committed) */
+          }
+          /* Progress[r.id].MaybeUpdate(li) */
+          orc_pr *me = &prs[self];
+          uint64_t m0 = me->match, n0 = me->next;
+          uint32_t w0 = pr_word(me);
+          pr_maybe_update(me, li);
+          B += 12 + (me->match != m0 ? 8 : 0) + (me->next != n0 ? 8 : 0) + (pr_word(me) != w0 ? 4 : 0);
+          for (uint32_t t = 0; t < S; t++) vals[t] = prs[t].match;
+          uint64_t mci = orc_joint_committed(S, mi, mo, vals);
+          orc_maybe_commit(mci, &cm, a->term_start[g], li);
+          B += cm != c0 ? 8 : 0;
+          /* bcastAppend: sendAppend to every Progress but the leader's */
+          for (uint32_t t = 0; t < S; t++) {
+            if (app_only || !((trk >> t) & 1u) || t == self) continue;
+            orc_pr *p = &prs[t];
+            uint64_t nx0 = p->next;
+            uint32_t pw0 = pr_word(p);
+            if (q->bytes) p->acct = &B;                      /* appended entries: 4 B each */
+            send_append(&c, p, t, 1);
+            p->acct = NULL;
+            B += 12 + (p->next != nx0 ? 8 : 0) + (pr_word(p) != pw0 ? 4 : 0) +
+                 (p->reset ? 8 : 0);                         /* Next + word; PendingSnapshot written */
+          }
+          for (uint32_t t = 0; t < S; t++) pr_store2(&prs[t], a, t, g);
+          a->committed[g] = cm;
+          sentm = c.sent;
+          snapm = c.snapm;
+        }
+      }
+    }
+    q->result[g] = (uint8_t)res;
+    if (q->cc_refused) q->cc_refused[g] = (uint8_t)refused;
+    if (q->sent) st_mask(q->sent, mb, g, sentm);
+    if (q->snap) st_mask(q->snap, mb, g, snapm);
+    B += 1 + (q->cc_refused ? 1 : 0) + (q->sent ? mb : 0) + (q->snap ? mb : 0);
+    bytes += B;
+    st[ST_GROUPS] += 1;
+    st[ST_COMMIT_ADVANCED] += cm != c0;
+    st[ST_COMMIT_SUM] += cm;
+    st[ST_CHECKSUM] += orc_checksum_prop(a->goff + g, res, li, cm, sentm);
+  }
+  if (stats)
+    for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+  if (q->bytes) *q->bytes += bytes;
+}
+
 /* Scalar helpers for the golden tables (tests only). */
 int orc_pr_maybe_decr_to(uint32_t state, uint64_t *match, uint64_t *next, uint64_t rejected,
                          uint64_t hint) {

@@ -59,6 +59,7 @@ DOMINANT = {
     "ready_collect": (("void qe::k_collect_count", "void qe::k_collect_scan",
                        "void qe::k_collect_scatter"), 2),
     "progress_send": ("void qe::k_progress_send<5,", 2),
+    "propose": ("void qe::k_propose<5, unsigned char, false, false, false>", 2),
     "progress_step_n7": ("void qe::k_progress_step<7, unsigned char, false, false, 4, false,", 2),
     "progress_step_joint": ("void qe::k_progress_step<6, unsigned char, true, true, 4, false,", 2),
 }

@@ -20,7 +20,8 @@ tests).  Expectations are what each reference test asserts; the rest of
 its message flow (proposals, appends, acks) is executed, not assumed."""
 import numpy as np
 
-from tests.progress_scenarios import F_CAP, PF_RECENT_ACTIVE, bits, initial_arrays
+from tests.progress_scenarios import (F_CAP, PF_RECENT_ACTIVE, bits, initial_arrays,
+                                      oracle_propose, peer_view)
 
 REPLICATE = 1
 
@@ -46,13 +47,13 @@ def _leader_after_hup(S):
 
 
 def _propose(be, S, voters_acking):
-    """One MsgProp (raft.go:1070-1076): appendEntry (lastIndex + 1, the
-    leader's own Match) + bcastAppend to every follower, then the followers'
-    MsgAppResp for the new entry -- the network of the reference test
-    delivers them synchronously."""
-    be.append()
+    """One MsgProp (raft.go:1019-1076) through qe_propose: appendEntry
+    (lastIndex + 1, the leader's own MaybeUpdate, maybeCommit) + bcastAppend
+    to every follower, then the followers' MsgAppResp for the new entry --
+    the network of the reference test delivers them synchronously."""
+    out = be.propose(1)
+    assert out["result"] == 1, out
     li = be.last_index()
-    be.send(sum(1 << s for s in range(1, S)), 1)
     t = np.zeros(S, np.uint8)
     idx = np.zeros(S, np.uint64)
     for s in voters_acking:
@@ -182,9 +183,8 @@ def read_only_for_new_leader(be):
     # recover; heartbeat responses (no read pending: no context) -> probes
     out = _heartbeat_round(be, S, (1, 2))
     assert bits(out["sent"]) == [1, 2] and out["term_commit"] == 0
-    be.append()  # MsgProp: 4@2; the followers are paused again
-    out = be.send(0b110, 1)
-    assert out["sent"] == 0
+    out = be.propose(1)  # MsgProp: 4@2; the followers are paused again
+    assert out["result"] == 1 and out["sent"] == 0
     # the followers append [3, 4] and accept; slot 1's accept commits 4
     t = np.array([0, 1, 1], np.uint8)
     idx = np.array([0, 4, 4], np.uint64)
@@ -466,7 +466,7 @@ class OracleRoundBackend:
     def __init__(self, orc):
         self.orc = orc
 
-    def load(self, sc, a, inc=None, tracked=None):
+    def load(self, sc, a, inc=None, tracked=None, out=None):
         S = sc["S"]
         pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
         a = dict(a)
@@ -478,8 +478,11 @@ class OracleRoundBackend:
             pb.inc = np.array([inc], md)
         if tracked is not None:
             pb.tracked = np.array([tracked], md)
+        if out is not None:
+            pb.out = np.array([out], md)
         pb.track_reads()
         self.pb, self.sc = pb, sc
+        self.pci = self.unc = self.applied = self.max_unc = 0  # MsgProp state (qe_propose)
 
     def step(self, t, idx, hint, lt, ctx=None):
         o = self.orc.progress_step(self.pb, t, idx, hint, lt, read_ctx=ctx)
@@ -507,14 +510,18 @@ class OracleRoundBackend:
         return {"sent": sent[0], "snap": snap[0]}
 
     def append(self):
-        pb = self.pb
-        pb.last_index[0] += 1
-        s = self.sc["self"]
-        pb.match[s] = pb.last_index[0]
-        pb.next[s] = max(int(pb.next[s]), int(pb.last_index[0]) + 1)
+        out = self.propose(1, append_only=True)
+        assert out["result"] == 1, out
+
+    def propose(self, n, payload=0, append_only=False, cc=None):
+        return oracle_propose(self, n, payload, append_only, cc)
 
     def last_index(self):
         return int(self.pb.last_index[0])
+
+    def peer(self, s):
+        pb = self.pb
+        return peer_view(pb.match, pb.next, pb.pending, pb.flags, pb.icount, s)
 
     def committed(self):
         return int(self.pb.committed[0])

@@ -6,8 +6,9 @@ A scenario is one group: slot s is node id s+1 and `self` is the leader's
 slot.  Ops:
   step    one round of peer messages through qe_progress_step (stepLeader)
   send    qe_progress_send: sendAppend / bcastAppend to the `want` slots
-  append  appendEntry: lastIndex += 1, the leader's own Match = lastIndex
-          (no scenario's append moves the commit index)
+  append  appendEntry of one empty entry (qe_propose with
+          QE_PROP_APPEND_ONLY: lastIndex + 1, the leader's own MaybeUpdate,
+          maybeCommit; no bcast -- the tests call sendAppend themselves)
   check   expectations only
 The same runner drives the oracle (CPU tests) and the HIP engine (GPU tests)
 through a small backend interface.
@@ -124,6 +125,36 @@ def run_scenario(sc, be):
         check_expect(sc, st.get("expect", {}), be, out, where)
 
 
+def cc_arrays(cc, max_cc=2):
+    """(max_cc, count[1], pos[max_cc], leave[max_cc], size[max_cc]) of one
+    group's conf-change entries [(position, leave_joint, size), ...]."""
+    cc = cc or []
+    m = max(max_cc, len(cc))
+    pos = np.zeros(m, np.uint32)
+    lv = np.zeros(m, np.uint8)
+    sz = np.zeros(m, np.uint32)
+    for k, (p, leave, size) in enumerate(cc):
+        pos[k], lv[k], sz[k] = p, int(bool(leave)), size
+    return m, np.array([len(cc)], np.uint8), pos, lv, sz
+
+
+def oracle_propose(be, n, payload=0, append_only=False, cc=None):
+    """Backend helper: orc_propose_batch on be.pb (one group) with the
+    backend-held pendingConfIndex / uncommittedSize / applied."""
+    for k, v in (("pci", 0), ("unc", 0), ("applied", 0), ("max_unc", 0)):
+        if not hasattr(be, k):
+            setattr(be, k, v)
+    pci = np.array([be.pci], np.uint64)
+    unc = np.array([be.unc], np.uint64)
+    o = be.orc.propose(be.pb, np.array([n], np.uint32), np.array([payload], np.uint64),
+                       cc=cc_arrays(cc), applied=np.array([be.applied], np.uint64),
+                       pending_conf_index=pci, uncommitted_size=unc,
+                       max_uncommitted=be.max_unc, flags=1 if append_only else 0)
+    be.pci, be.unc = int(pci[0]), int(unc[0])
+    return {"result": int(o.result[0]), "sent": int(o.sent[0]), "snap": int(o.snap[0]),
+            "cc_refused": int(o.cc_refused[0])}
+
+
 def peer_view(match, nxt, pending, flags, icount, s):
     f = int(flags[s])
     return {"match": int(match[s]), "next": int(nxt[s]), "pending": int(pending[s]),
@@ -145,6 +176,7 @@ class OracleBackend:
         for k, v in a.items():
             setattr(pb, k, v.copy())
         self.pb, self.sc = pb, sc
+        self.pci = self.unc = self.applied = self.max_unc = 0  # MsgProp state (qe_propose)
 
     def step(self, t, idx, hint, lt):
         o = self.orc.progress_step(self.pb, t, idx, hint, lt)
@@ -157,11 +189,15 @@ class OracleBackend:
         return {"sent": sent[0], "snap": snap[0]}
 
     def append(self):
-        pb = self.pb
-        pb.last_index[0] += 1
-        s = self.sc["self"]
-        pb.match[s] = pb.last_index[0]
-        pb.next[s] = max(int(pb.next[s]), int(pb.last_index[0]) + 1)
+        out = self.propose(1, append_only=True)
+        assert out["result"] == 1, out
+
+    def propose(self, n, payload=0, append_only=False, cc=None):
+        """One MsgProp (or appendEntry alone) through the oracle's
+        orc_propose_batch; cc: list of (position, leave_joint, size).
+        pendingConfIndex / uncommittedSize / applied live in the backend
+        (self.pci, self.unc, self.applied, self.max_unc)."""
+        return oracle_propose(self, n, payload, append_only, cc)
 
     def peer(self, s):
         pb = self.pb

@@ -29,7 +29,7 @@ def test_header_declares_expected_surface():
               "qe_mask_bytes", "qe_tune", "qe_allreduce_stats", "qe_comm_init",
               "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes", "qe_check_quorum",
               "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange",
-              "qe_read_index"]:
+              "qe_read_index", "qe_propose", "qe_comm_init_timeout", "qe_comm_abort"]:
         assert f in fns
 
 
@@ -69,6 +69,8 @@ int main(void) {
   Z(qe_conf) F(qe_conf, slot_ids) F(qe_conf, tracked) F(qe_conf, auto_leave)
   Z(qe_conf_changes) F(qe_conf_changes, stride) F(qe_conf_changes, node_id)
   F(qe_conf_changes, new_progress)
+  Z(qe_proposals) F(qe_proposals, max_cc) F(qe_proposals, cc_stride) F(qe_proposals, cc_size)
+  F(qe_proposals, max_uncommitted) F(qe_proposals, cc_refused) F(qe_proposals, bytes_requested)
   return 0;
 }
 """
@@ -79,7 +81,7 @@ CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
           "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams,
           "qe_confstate_csr": _lib.QeConfStateCSR, "qe_progress": _lib.QeProgress,
           "qe_peer_msgs": _lib.QePeerMsgs, "qe_conf": _lib.QeConf,
-          "qe_conf_changes": _lib.QeConfChanges}
+          "qe_conf_changes": _lib.QeConfChanges, "qe_proposals": _lib.QeProposals}
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -98,7 +100,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 5
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 6
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0

@@ -366,6 +366,30 @@ def test_progress_long_rings_and_bcasts(eng):
         ps.last_index.copy_(torch.from_numpy(pb.last_index.view(np.int64)).to(DEV))
 
 
+def gpu_propose(be, n, payload=0, append_only=False, cc=None):
+    from tests.progress_scenarios import cc_arrays
+    for k, v in (("pci", 0), ("unc", 0), ("applied", 0), ("max_unc", 0)):
+        if not hasattr(be, k):
+            setattr(be, k, v)
+    m, cnt, pos, lv, sz = cc_arrays(cc)
+    pr = be.eng.Proposals(be.ps, max_cc=m, max_uncommitted=be.max_unc,
+                          flags=be.eng._lib.QE_PROP_APPEND_ONLY if append_only else 0)
+    pr.num_entries.fill_(n)
+    pr.payload.fill_(payload)
+    pr.cc_count.copy_(torch.from_numpy(cnt).to(DEV))
+    pr.cc_pos.copy_(torch.from_numpy(pos.view(np.int32)).to(DEV))
+    pr.cc_leave.copy_(torch.from_numpy(lv).to(DEV))
+    pr.cc_size.copy_(torch.from_numpy(sz.view(np.int32)).to(DEV))
+    pr.applied.fill_(be.applied)
+    pr.pending_conf_index.fill_(be.pci)
+    pr.uncommitted_size.fill_(be.unc)
+    be.eng.propose(be.ps, pr)
+    be.pci = int(pr.pending_conf_index[0])
+    be.unc = int(pr.uncommitted_size[0])
+    return {"result": int(pr.result[0]), "sent": int(pr.sent[0]), "snap": int(pr.snap[0]),
+            "cc_refused": int(pr.cc_refused[0])}
+
+
 class GpuBackend:
     """tests/progress_scenarios.py / leader_round_scenarios.py backend over
     the HIP engine (one group)."""
@@ -373,11 +397,11 @@ class GpuBackend:
     def __init__(self, eng):
         self.eng = eng
 
-    def load(self, sc, a, inc=None, tracked=None):
+    def load(self, sc, a, inc=None, tracked=None, out=None):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
+        masks = (("inc",) if inc is not None else ()) + (("out",) if out is not None else ())
         ps = self.eng.ProgressState(1, sc["S"], cap(sc), len(sc["log"]["runs"]), DEV, stride=1,
-                                    extras=READS, max_ents=sc["max_ents"],
-                                    masks=("inc",) if inc is not None else ())
+                                    extras=READS, max_ents=sc["max_ents"], masks=masks)
         if tracked is None:
             ps.tracked = None  # every slot holds a Progress (as the oracle backend)
         else:
@@ -387,7 +411,10 @@ class GpuBackend:
         ps.load_host(**a)
         if inc is not None:
             ps.inc.fill_(inc)
+        if out is not None:
+            ps.out.fill_(out)
         self.ps, self.sc = ps, sc
+        self.pci = self.unc = self.applied = self.max_unc = 0  # MsgProp state (qe_propose)
 
     def step(self, t, idx, hint, lt, ctx=None):
         msgs = load_msgs(self.eng, self.ps, t, idx, hint, lt)
@@ -433,11 +460,13 @@ class GpuBackend:
         return int(qa[0]), ra
 
     def append(self):
-        ps, s = self.ps, self.sc["self"]
-        ps.last_index += 1
-        li = int(ps.last_index[0])
-        ps.match[s * ps.stride] = li
-        ps.next[s * ps.stride] = max(int(ps.next[s * ps.stride]), li + 1)
+        out = self.propose(1, append_only=True)
+        assert out["result"] == 1, out
+
+    def propose(self, n, payload=0, append_only=False, cc=None):
+        """qe_propose on the one group (the backend holds pendingConfIndex,
+        uncommittedSize and applied, as the oracle backend does)."""
+        return gpu_propose(self, n, payload, append_only, cc)
 
     def peer(self, s):
         h = self.ps.host()
