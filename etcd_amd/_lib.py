@@ -207,6 +207,7 @@ PROTOTYPES = {
     "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
     "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp, vp]),
     "qe_propose": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeProposals), vp, vp]),
+    "qe_heartbeat": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),

@@ -498,6 +498,29 @@ int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, 
                            p->out_mask != nullptr, static_cast<hipStream_t>(stream));
 }
 
+int qe_heartbeat(const qe_progress *p, uint64_t *commit, uint32_t *ctx, void *sent, void *stream) {
+  if (!p) return QE_EINVAL;
+  if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
+    return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (p->stride < p->num_groups || !p->match || !p->committed || !commit) return QE_EINVAL;
+  if (p->read_acks && (!p->read_head || !p->read_count)) return QE_EINVAL;
+  PArgs a{};
+  a.G = p->num_groups;
+  a.stride = p->stride;
+  a.match = p->match;
+  a.committed = p->committed;
+  a.tracked = p->tracked;
+  a.self_slot = p->self_slot;
+  a.read_acks = p->read_acks;
+  a.read_head = p->read_head;
+  a.read_count = p->read_count;
+  a.hb_commit = commit;
+  a.hb_ctx = ctx;
+  a.sent = sent;
+  return dispatch_progress(p->num_slots, a, 7, false, false, static_cast<hipStream_t>(stream));
+}
+
 int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
                   uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream) {
   if (!p) return QE_EINVAL;

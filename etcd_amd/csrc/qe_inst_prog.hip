@@ -101,10 +101,16 @@ static int launch_propose(const PArgs &a, bool masked, bool joint, hipStream_t s
   return hip_status(hipGetLastError());
 }
 
+static int launch_heartbeat(const PArgs &a, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  hipLaunchKernelGGL((k_heartbeat<S, MT>), grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 // kind 0: qe_progress_step, 1: qe_progress_send, 2: qe_progress_step with
 // byte accounting (instrumented variant, measurement only), 3:
 // qe_check_quorum, 4: qe_read_index, 5: qe_propose, 6: qe_propose with byte
-// accounting
+// accounting, 7: qe_heartbeat
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
   if (kind == 1) return launch_progress_send(a, st);
@@ -112,6 +118,7 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
   if (kind == 4) return launch_read_index(a, masked, joint, st);
   if (kind == 5) return launch_propose<false>(a, masked, joint, st);
   if (kind == 6) return launch_propose<true>(a, masked, joint, st);
+  if (kind == 7) return launch_heartbeat(a, st);
   // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
   // or two older terms before the current one); 8 keep the block's LDS at
   // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);

@@ -753,6 +753,9 @@ struct PArgs {
   uint64_t max_unc;
   uint8_t *prop_result, *cc_refused;
   uint64_t *last_index_rw;
+  // heartbeat (qe_heartbeat, ABI 6)
+  uint64_t *hb_commit;
+  uint32_t *hb_ctx;
 };
 
 struct PR {

@@ -1443,6 +1443,52 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
   acct_flush<ACCT>(ac, a.acct);
 }
 
+// qe_heartbeat (ABI 6): MsgBeat -> bcastHeartbeat (raft/raft.go:524-541):
+// per group the context of the newest pending ReadIndex request, per peer
+// (every tracked slot but the leader's) Commit = min(Match, committed)
+// (sendHeartbeat :494-510).  One lane per group, a wave per tile; the Match
+// rows of the peers sent to are read, their commit rows written.
+template <int S, typename MT>
+__global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = t * 64;
+    const uint32_t n = tile_n(a.G, t);
+    const uint32_t o8 = lane * 8;
+    const uint32_t trk =
+        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * sizeof(MT)), lane) &
+                     kFull)
+                  : kFull;
+    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
+    const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
+    const uint32_t to = lane < n ? (trk & ~selfb) : 0u;
+    const uint64_t c = bld64(mk_rsrc(a.committed + g0, n * 8), o8);
+    if (a.hb_ctx) {
+      uint32_t cx = 0;
+      if (a.read_acks) {
+        const uint32_t qn = bld8(mk_rsrc(a.read_count + g0, n), lane);
+        const uint32_t qh = bld32(mk_rsrc(a.read_head + g0, n * 4), lane * 4);
+        const uint32_t q = qn < QE_READ_QUEUE ? qn : QE_READ_QUEUE;
+        cx = q ? qh + q - 1u : 0u;  // lastPendingRequestCtx
+      }
+      bst32(cx, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      const uint32_t off = bit_off(to, s, o8);
+      const uint64_t m = bld64(mk_rsrc(a.match + row, n * 8), off);
+      bst64(m < c ? m : c, mk_rsrc(a.hb_commit + row, n * 8), off);
+    }
+    if (a.sent) bst_mask<MT>(to, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+  }
+}
+
 // qe_check_quorum: MsgCheckQuorum (raft/raft.go:997-1018) over the resident
 // Progress words.  One lane per group; each wave owns a chunk of up to
 // kSendTPW tiles (as qe_progress_send): the chunk's masks (Voters[0] |

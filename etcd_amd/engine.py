@@ -590,6 +590,22 @@ def check_quorum(ps, quorum_active=None, stats=None):
     return quorum_active
 
 
+def heartbeat(ps, commit=None, ctx=None, sent=None):
+    """qe_heartbeat: MsgBeat -> bcastHeartbeat (raft/raft.go:524-541) ->
+    (commit int64 [S][stride]: min(Match, committed) of every slot sent to,
+    ctx int32 [G]: the newest pending ReadIndex context, sent mask [G])."""
+    if commit is None:
+        commit = torch.zeros(ps.S * ps.stride, dtype=torch.int64, device=ps.device)
+    if ctx is None:
+        ctx = torch.zeros(ps.G, dtype=torch.int32, device=ps.device)
+    if sent is None:
+        sent = torch.zeros(ps.G, dtype=mask_torch_dtype(ps.S), device=ps.device)
+    p = ps.struct()
+    check("qe_heartbeat", _lib.lib().qe_heartbeat(C.byref(p), _ptr(commit), _ptr(ctx), _ptr(sent),
+                                                   _stream(ps.device)))
+    return commit, ctx, sent
+
+
 class Proposals:
     """One MsgProp per group for qe_propose (qe_proposals, ABI 6):
     num_entries [G] (0 = none), payload [G] (sum of the non-conf-change

@@ -530,6 +530,19 @@ int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_b
 int qe_check_quorum(const qe_progress *p, uint8_t *quorum_active, uint64_t *stats,
                     void *stream);
 
+/* ABI 6: MsgBeat on every group's leader (stepLeader, raft/raft.go:991-993):
+ * bcastHeartbeat (:524-541) -- one MsgHeartbeat to every tracked slot but
+ * self_slot, each carrying Commit = min(Progress.Match, raftLog.committed)
+ * (sendHeartbeat :494-510: a follower is never told a commit beyond what it
+ * matched) and the context of the newest pending ReadIndex request
+ * (lastPendingRequestCtx, read_only.go:114-121).  commit[s*stride + g]
+ * (DEVICE, [S][stride]) is written for every slot sent to; ctx[g] (may be
+ * NULL) = that context number, 0 when nothing is pending or p->read_acks is
+ * NULL; sent[g] (mask-typed, may be NULL) = the slots sent to.  Reads
+ * match, committed, tracked, self_slot and the ReadIndex queue's head and
+ * count; writes nothing of p. */
+int qe_heartbeat(const qe_progress *p, uint64_t *commit, uint32_t *ctx, void *sent, void *stream);
+
 /* raft.sendAppend / maybeSendAppend(to, send_if_empty) once for the slots of
  * want[g] (raft.go:432-492; bcastAppend after a proposal is want = every
  * tracked slot but the leader's, send_if_empty = 1): paused peers get

@@ -64,6 +64,7 @@ def _declare(L):
         "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
         "orc_propose_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcProps), vp]),
         "orc_checksum_prop": (u64, [u64, u32, u64, u64, u32]),
+        "orc_heartbeat_batch": (None, [C.POINTER(OrcProg), vp, vp, vp]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
         "orc_pr_maybe_decr_to": (i32, [u32, vp, vp, u64, u64]),
@@ -391,3 +392,15 @@ def propose(pb, num_entries, payload=None, cc=None, applied=None, pending_conf_i
     s = pb.struct(goff)
     lib().orc_propose_batch(C.byref(s), C.byref(q), P(o.stats))
     return o
+
+
+def heartbeat(pb):
+    """MsgBeat -> bcastHeartbeat on every group's leader (oracle) ->
+    (commit uint64 [S][stride] (0 where nothing was sent), ctx uint32 [G],
+    sent mask [G])."""
+    commit = np.zeros(pb.S * pb.stride, np.uint64)
+    ctx = np.zeros(pb.G, np.uint32)
+    sent = np.zeros(pb.G, mask_dtype(pb.S))
+    s = pb.struct()
+    lib().orc_heartbeat_batch(C.byref(s), P(commit), P(ctx), P(sent))
+    return commit, ctx, sent

@@ -1745,6 +1745,39 @@ void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
   if (q->bytes) *q->bytes += bytes;
 }
 
+/* MsgBeat on each group's leader (stepLeader, raft/raft.go:991-993):
+ * bcastHeartbeat (:524-541) -> sendHeartbeat (:494-510) to every Progress
+ * but the leader's, Commit = min(Match, committed), Context =
+ * lastPendingRequestCtx (read_only.go:114-121; here the context number of
+ * the newest pending request, 0 = none).  commit [S][stride] is written
+ * for the slots sent to. */
+void orc_heartbeat_batch(const orc_prog *a, uint64_t *commit, uint32_t *ctx, void *sent) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  for (uint64_t g = 0; g < a->G; g++) {
+    uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+    uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+    uint32_t to = 0;
+    uint64_t c = a->committed[g];
+    for (uint32_t s = 0; s < S; s++) {
+      if (!((trk >> s) & 1u) || s == self) continue;
+      uint64_t m = a->match[s * a->stride + g];
+      commit[s * a->stride + g] = m < c ? m : c;
+      to |= 1u << s;
+    }
+    if (ctx) {
+      uint32_t cx = 0;
+      if (a->read_acks) {
+        orc_ro ro;
+        ro_load(&ro, ro_word_get(a->read_acks, mb, g), a->read_head[g], a->read_count[g], mb);
+        cx = ro.n ? ro.ctx[ro.n - 1] : 0;
+      }
+      ctx[g] = cx;
+    }
+    if (sent) st_mask(sent, mb, g, to);
+  }
+}
+
 /* Scalar helpers for the golden tables (tests only). */
 int orc_pr_maybe_decr_to(uint32_t state, uint64_t *match, uint64_t *next, uint64_t rejected,
                          uint64_t hint) {

@@ -3,7 +3,7 @@
 # append through it, the bench workload, then its rocprofv3 passes.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r05b}; mkdir -p "$O"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_propose.py tests/test_gpu_progress.py -m gpu -x -q -p no:cacheprovider \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_propose.py tests/test_gpu_trace_replay.py tests/test_gpu_progress.py -m gpu -x -q -p no:cacheprovider \
   --timeout 120 --timeout-method thread > "$O/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$O/tests.log"; exit 2; }
 tail -2 "$O/tests.log"
 timeout -k 10 300 python -u bench.py --workload propose --no-aux --no-cpu-baseline --steps 20 --warmup 5 > "$O/bench_propose.log" 2>&1 || { echo bench failed; tail -20 "$O/bench_propose.log"; exit 3; }

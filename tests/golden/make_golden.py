@@ -40,6 +40,12 @@ Outputs (data only: inputs + expected outputs):
     raft_snap_test.go's five tests, and the leader side of
     TestLeaderTransferToSlowFollower -- state set up by the tests' code is
     restated per scenario (see progress_scenarios()).
+  tests/golden/interaction_traces.json  raft/testdata/{probe_and_replicate,
+    snapshot_succeed_via_app_resp,campaign,campaign_learner_must_vote}.txt
+    (raft/interaction_test.go): per command its printed blocks -- the
+    messages each node received, the Ready it handled (HardState commit,
+    entries, messages sent: DescribeMessage fields) and `status` Progress
+    strings; tests/trace_replay.py replays the leaders' side.
   tests/golden/election_scenarios.json  scripted election steps:
     TestLeaderElectionInOneRoundRPC (table), TestLeaderStepdownWhenQuorumLost,
     TestPreVoteWithSplitVote (node views derived from the test's flow).
@@ -649,6 +655,117 @@ def confchange_files():
     return files
 
 
+# ---------------------------------------------------------------------------
+# raft/testdata/*.txt interaction traces (raft/interaction_test.go:24-34,
+# raft/rafttest/interaction_env*.go): what every node received and sent, as
+# the reference printed it.  Only the printed data is extracted; the
+# replay (tests/trace_replay.py) restates each leader's side.
+# ---------------------------------------------------------------------------
+TRACE_FILES = ("probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt", "campaign.txt",
+               "campaign_learner_must_vote.txt")
+_MSG_RE = re.compile(r"^([0-9a-f]+)->([0-9a-f]+) (Msg\w+) Term:(\d+) Log:(\d+)/(\d+)(.*)$")
+
+
+def parse_message(text):
+    """A DescribeMessage line (raft/util.go:133-156) -> dict."""
+    m = _MSG_RE.match(text)
+    assert m, text
+    rest = m.group(7)
+    d = {"from": int(m.group(1), 16), "to": int(m.group(2), 16), "type": m.group(3),
+         "term": int(m.group(4)), "logterm": int(m.group(5)), "index": int(m.group(6)),
+         "reject": False, "hint": 0, "commit": 0, "entries": [], "snap_index": None}
+    r = re.search(r" Rejected \(Hint: (\d+)\)", rest)
+    if r:
+        d["reject"], d["hint"] = True, int(r.group(1))
+    c = re.search(r" Commit:(\d+)", rest)
+    if c:
+        d["commit"] = int(c.group(1))
+    e = re.search(r" Entries:\[(.*)\]", rest)
+    if e:
+        d["entries"] = [[int(a), int(b)] for a, b in re.findall(r"(\d+)/(\d+) Entry\w+", e.group(1))]
+    sn = re.search(r" Snapshot: Index:(\d+) Term:(\d+)", rest)
+    if sn:
+        d["snap_index"] = int(sn.group(1))
+    return d
+
+
+def parse_trace_output(out):
+    """The output lines of one command -> blocks: recv (messages a node
+    received, with its DEBUG progress lines), ready (HardState commit, state,
+    entries, messages sent) and status (Progress strings)."""
+    blocks, cur = [], None
+    for raw in out:
+        line = raw.strip()
+        h = re.match(r"^> (\d+) (receiving messages|handling Ready)$", line)
+        if h:
+            cur = {"node": int(h.group(1)),
+                   "kind": "recv" if h.group(2).startswith("receiving") else "ready",
+                   "msgs": [], "debug": []}
+            blocks.append(cur)
+            continue
+        if line.startswith("Ready MustSync") and (cur is None or cur["kind"] != "ready"):
+            cur = {"node": None, "kind": "ready", "msgs": [], "debug": []}  # process-ready
+            blocks.append(cur)
+            continue
+        st = re.match(r"^(\d+): (State\w+ match=\d+ next=\d+.*)$", line)
+        if st and not raw.startswith(" "):
+            if cur is None or cur["kind"] != "status":
+                cur = {"node": None, "kind": "status", "progress": {}}
+                blocks.append(cur)
+            cur["progress"][st.group(1)] = st.group(2)
+            continue
+        if cur is None or cur["kind"] == "status":
+            continue
+        if _MSG_RE.match(line):
+            cur["msgs"].append(parse_message(line))
+        elif line.startswith("HardState"):
+            cur["commit"] = int(re.search(r"Commit:(\d+)", line).group(1))
+            t = re.search(r"Term:(\d+)", line)
+            cur["term"] = int(t.group(1)) if t else None
+        elif line.startswith("Lead:"):
+            cur["lead_state"] = line
+        elif re.match(r"^\d+/\d+ Entry\w+", line):
+            cur.setdefault("entries", []).append([int(x) for x in line.split()[0].split("/")])
+        elif line.startswith("DEBUG") or line.startswith("INFO"):
+            cur["debug"].append(line)
+    return blocks
+
+
+def interaction_traces():
+    out = {}
+    for name in TRACE_FILES:
+        path = os.path.join(REF, "testdata", name)
+        with open(path, encoding="utf-8") as f:
+            lines = f.read().split("\n")
+        cmds, i = [], 0
+        while i < len(lines):
+            if lines[i] == "----":
+                # the command is the non-comment block above, its output the
+                # lines up to the next blank line
+                j = i - 1
+                cmd = []
+                while j >= 0 and lines[j] != "" and not lines[j].startswith("#"):
+                    cmd.insert(0, lines[j])
+                    j -= 1
+                k = i + 1
+                body = []
+                while k < len(lines) and lines[k] != "":
+                    body.append(lines[k])
+                    k += 1
+                c = {"line": j + 2, "cmd": cmd[0], "input": cmd[1:],
+                     "blocks": parse_trace_output(body)}
+                if cmd[0].startswith("raft-log"):  # the node's log: term/index per entry
+                    c["log"] = [[int(a), int(b)] for a, b in
+                                (re.match(r"^(\d+)/(\d+) Entry", x).groups() for x in body
+                                 if re.match(r"^\d+/\d+ Entry", x))]
+                cmds.append(c)
+                i = k
+            else:
+                i += 1
+        out[name] = {"source": f"raft/testdata/{name}", "commands": cmds}
+    return out
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are already committed")
@@ -693,6 +810,11 @@ def main():
         for r in tables["TestLeaderElectionInOneRoundRPC"]["rows"]:
             votes = ",".join(f"{i}:{int(v)}" for i, v in r["votes"])
             f.write(f"{r['size']} {r['state']} votes={votes}\n")
+    traces = interaction_traces()
+    with open(os.path.join(HERE, "interaction_traces.json"), "w", encoding="utf-8") as f:
+        json.dump(traces, f, indent=1)
+    print("wrote", sum(len(v["commands"]) for v in traces.values()), "trace commands from",
+          len(traces), "interaction files")
     cc = confchange_files()
     with open(os.path.join(HERE, "confchange_testdata.json"), "w", encoding="utf-8") as f:
         json.dump(cc, f, indent=1)

@@ -487,8 +487,14 @@ class OracleRoundBackend:
     def step(self, t, idx, hint, lt, ctx=None):
         o = self.orc.progress_step(self.pb, t, idx, hint, lt, read_ctx=ctx)
         return {"sent": o.sent[0], "bcast": o.bcast[0], "timeout_now": o.timeout_now[0],
+                "snap": o.snap[0], "msg_count": o.msg_count, "msg_index": o.msg_index,
                 "read_released": int(o.read_released[0]), "term_commit": int(o.term_commit[0]),
                 "term_commit_index": int(o.term_commit_index[0])}
+
+    def heartbeat(self):
+        """MsgBeat (orc_heartbeat_batch) -> (commit per slot, ctx, sent mask)."""
+        commit, ctx, sent = self.orc.heartbeat(self.pb)
+        return [int(x) for x in commit[: self.sc["S"]]], int(ctx[0]), int(sent[0])
 
     def read_index(self, lease_based=False):
         r, c, i = self.orc.read_index(self.pb, np.ones(1, np.uint8), lease_based)

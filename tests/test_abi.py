@@ -29,7 +29,8 @@ def test_header_declares_expected_surface():
               "qe_mask_bytes", "qe_tune", "qe_allreduce_stats", "qe_comm_init",
               "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes", "qe_check_quorum",
               "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange",
-              "qe_read_index", "qe_propose", "qe_comm_init_timeout", "qe_comm_abort"]:
+              "qe_read_index", "qe_propose", "qe_comm_init_timeout", "qe_comm_abort",
+              "qe_heartbeat"]:
         assert f in fns
 
 

@@ -429,6 +429,13 @@ class GpuBackend:
                 "term_commit": int(msgs.term_commit[0]),
                 "term_commit_index": int(msgs.term_commit_index[0])}
 
+    def heartbeat(self):
+        """qe_heartbeat -> (commit per slot, ctx, sent mask)."""
+        commit, ctx, sent = self.eng.heartbeat(self.ps)
+        st = self.ps.stride
+        c = commit.cpu().numpy().view(np.uint64)[: self.sc["S"] * st: st]
+        return [int(x) for x in c], int(ctx[0]) & 0xFFFFFFFF, int(sent[0])
+
     def read_index(self, lease_based=False):
         req = torch.ones(1, dtype=torch.uint8, device=DEV)
         r, c, i = self.eng.read_index(self.ps, req, lease_based)

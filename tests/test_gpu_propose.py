@@ -175,3 +175,31 @@ def test_propose_full_size_bench_state(eng):
     cnt1 = (ps.peer.view(S, -1)[1:, :G].to(torch.int64) >> 16) & 0xFF
     assert bool((cnt1 == cnt0 + 1).all())
     assert bool((pr.sent.to(torch.int32) == 0b11110).all())
+
+
+@pytest.mark.parametrize("S,masks,extras,reads", [(3, (), (), False), (5, ("inc",), EXTRAS, True),
+                                                   (12, (), EXTRAS, True)])
+def test_heartbeat_matches_oracle(eng, S, masks, extras, reads):
+    """qe_heartbeat (MsgBeat -> bcastHeartbeat, raft.go:524-541, sendHeartbeat
+    :494-510) against the oracle: the slots sent to (tracked, not the
+    leader), Commit = min(Match, committed) per slot, and the context of the
+    newest pending ReadIndex request."""
+    from tests.test_gpu_progress import random_queue
+    rng = np.random.default_rng(4100 + S)
+    G = 3001
+    pb = random_state(rng, G, S, 8, 2, masks, extras)
+    ext = extras
+    if reads:
+        random_queue(rng, pb)
+        ext = extras + ("reads",)
+    ps = to_device(eng, pb, masks, ext)
+    commit, ctx, sent = eng.heartbeat(ps)
+    o_commit, o_ctx, o_sent = orc.heartbeat(pb)
+    md = orc.mask_dtype(S)
+    np.testing.assert_array_equal(sent.cpu().numpy().view(md), o_sent)
+    np.testing.assert_array_equal(ctx.cpu().numpy().view(np.uint32), o_ctx)
+    got = commit.cpu().numpy().view(np.uint64).reshape(S, -1)[:, :G]
+    want = o_commit.reshape(S, -1)[:, :G]
+    to = (o_sent.astype(np.int64)[None, :] >> np.arange(S)[:, None]) & 1
+    np.testing.assert_array_equal(got[to == 1], want[to == 1])
+    assert to.any() and (not reads or o_ctx.any())

@@ -1,0 +1,61 @@
+"""The reference's interaction traces (raft/testdata/probe_and_replicate.txt,
+snapshot_succeed_via_app_resp.txt, campaign.txt,
+campaign_learner_must_vote.txt) replayed from the leader's side through the
+oracle (tests/trace_replay.py); tests/test_gpu_trace_replay.py runs the same
+replay through the HIP engine."""
+import numpy as np
+import pytest
+
+from tests.leader_round_scenarios import OracleRoundBackend
+from tests.trace_replay import (F_TRACE, TRACES, Leader, parse_progress, progress_string,
+                                traces)
+
+
+def oracle_elector(orc):
+    def make(S, self_slot, term0):
+        md = orc.mask_dtype(S)
+        term = np.array([term0], np.uint64)
+        state = np.zeros(1, np.uint8)
+        voted, granted = np.zeros(1, md), np.zeros(1, md)
+        self_a = np.array([self_slot], np.uint8)
+        inc = np.array([(1 << S) - 1], md)
+        k = [0]
+
+        def step(resp, grant, hup):
+            script = (np.array([resp], md), np.array([grant], md), np.array([hup], np.uint8), 1)
+            orc.election_steps(1, 0, S, term, state, voted, granted, self_a, inc, None,
+                               np.zeros(1, md), 0, k[0], 1, 0, 0, script=script)
+            k[0] += 1
+            return int(term[0]), int(state[0])
+        return step
+    return make
+
+
+@pytest.mark.parametrize("trace", TRACES, ids=lambda f: f.__name__)
+def test_trace_replay_on_oracle(orc, trace):
+    checked = trace(lambda node, S: Leader(OracleRoundBackend(orc), node, S),
+                    oracle_elector(orc))
+    assert checked["rounds"] > 0 and checked["sends"] > 0
+
+
+def test_trace_fixture_counts():
+    t = traces()
+    assert set(t) == {"probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt",
+                      "campaign.txt", "campaign_learner_must_vote.txt"}
+    pr = t["probe_and_replicate.txt"]["commands"]
+    rejects = [m for c in pr for b in c["blocks"] if b["kind"] == "recv" and b["node"] == 1
+               for m in b["msgs"] if m["type"] == "MsgAppResp" and m["reject"]]
+    # followers 2, 3, 5, 6, 7 reject the new leader's first probe (4 accepts)
+    assert sorted(m["from"] for m in rejects) >= [2, 3, 5, 6, 7]
+
+
+def test_progress_string_round_trip():
+    """progress_string restates tracker.Progress.String; the status lines of
+    the snapshot trace parse and render back to themselves."""
+    for c in traces()["snapshot_succeed_via_app_resp.txt"]["commands"]:
+        for b in c["blocks"]:
+            if b["kind"] == "status":
+                for text in b["progress"].values():
+                    p = parse_progress(text)
+                    view = dict(p, inflights=len(p["ring"]))
+                    assert progress_string(view, F_TRACE) == text

@@ -1,0 +1,403 @@
+"""Replay of the reference's interaction traces (raft/testdata/*.txt, run by
+raft/interaction_test.go:24-34) from the leader's side, through the batch
+engine's entry points on one group:
+
+  probe_and_replicate.txt            7 voters: election at term 8, then every
+                                     follower probed back: rejections with
+                                     hints, findConflictByTerm, MaybeDecrTo,
+                                     the MsgApps that answer them
+  snapshot_succeed_via_app_resp.txt  heartbeats, a MsgSnap for a compacted
+                                     log, the MsgAppResp that ends it
+  campaign.txt                       an election and the first commit
+  campaign_learner_must_vote.txt     an election won with a voter the
+                                     candidate's config has, then its catch-up
+
+The fixture tests/golden/interaction_traces.json holds what the reference
+printed (tests/golden/make_golden.py extracts it: no reference code runs).
+Each leader's state at the point the printed part begins is restated from
+the trace itself (raft-log dumps, status lines, HardState, the INFO lines of
+the election) -- see the *_setup functions -- and the leader's transitions
+the engine does not model (becomeCandidate's term bump is the election
+kernel's; becomeLeader's reset() of every Progress, raft.go:590-613, is host
+bookkeeping here) are written out where they occur.  Everything else is
+executed by the engine and compared with the trace:
+
+  * every "> L receiving messages" block is one or more rounds of
+    qe_progress_step (messages in slot order; a block whose senders are not
+    ascending is split where they descend, so the order is the trace's), or
+    for MsgVoteResp one scripted qe_election_steps step;
+  * every "> L handling Ready" block: per destination the number of
+    MsgApp/MsgSnap sent since the previous Ready and the Log index of the
+    first (msg_count / msg_index; a MsgSnap's snapshot index), the follower's
+    Next after them (the entries they carried: Probe keeps Next at the
+    probe, Replicate moves it past the last entry), the Commit they carry
+    and the HardState commit; MsgHeartbeat commits (qe_heartbeat);
+  * `status L` blocks: every Progress rendered as progress.go:214-236 does;
+  * "decreased progress of X to [...]" DEBUG lines: X's state, match and next.
+"""
+import json
+import os
+import re
+
+import numpy as np
+
+from tests.golden_util import GOLDEN
+from tests.progress_scenarios import initial_arrays
+
+STATE = {"StateProbe": 0, "StateReplicate": 1, "StateSnapshot": 2}
+STATE_NAME = {v: k for k, v in STATE.items()}
+# MaxInflightMsgs of the interaction env is math.MaxInt32 and MaxSizePerMsg
+# math.MaxUint64 (raft/rafttest/interaction_env.go:96-97): no trace holds more
+# than a few MsgApps in flight, so the slot model's 255 never binds
+F_TRACE = 255
+
+
+def traces():
+    with open(os.path.join(GOLDEN, "interaction_traces.json"), encoding="utf-8") as f:
+        return json.load(f)
+
+
+def progress_string(p, F=F_TRACE):
+    """tracker.Progress.String (raft/tracker/progress.go:214-236) of a peer
+    view (tests/progress_scenarios.peer_view) with its Inflights capacity."""
+    paused = (p["probe_sent"] if p["state"] == 0 else
+              (p["inflights"] == F if p["state"] == 1 else True))
+    s = f"{STATE_NAME[p['state']]} match={p['match']} next={p['next']}"
+    if paused:
+        s += " paused"
+    if p["pending"] > 0:
+        s += f" pendingSnap={p['pending']}"
+    if not p["recent_active"]:
+        s += " inactive"
+    if p["inflights"] > 0:
+        s += f" inflight={p['inflights']}"
+        if p["inflights"] == F:
+            s += "[full]"
+    return s
+
+
+def parse_progress(text):
+    """The fields a Progress string shows -> a peer dict (scenario form)."""
+    m = re.match(r"(State\w+) match=(\d+) next=(\d+)", text)
+    state = STATE[m.group(1)]
+    pend = re.search(r"pendingSnap=(\d+)", text)
+    infl = re.search(r"inflight=(\d+)", text)
+    paused = " paused" in text
+    return {"match": int(m.group(2)), "next": int(m.group(3)),
+            "pending": int(pend.group(1)) if pend else 0, "state": state,
+            "probe_sent": paused and state == 0, "recent_active": " inactive" not in text,
+            "ring": [0] * (int(infl.group(1)) if infl else 0)}
+
+
+def log_runs(entries, dummy):
+    """[[term, index], ...] of a log (ascending) after a dummy (snapshot)
+    entry [term, index] -> term runs [[first, term], ...]."""
+    runs = [[dummy[1], dummy[0]]]
+    for t, i in entries:
+        if t != runs[-1][1]:
+            runs.append([i, t])
+    return runs
+
+
+class Leader:
+    """The replayed leader: backend `be` (oracle or GPU, the interface of
+    tests/leader_round_scenarios.py plus heartbeat() and election()), node
+    id -> slot = id - 1.  The log's term runs end with the leader's own
+    term (term_start = its first index: on a fresh cluster that can be the
+    snapshot index, whose term the first leader shares)."""
+
+    def __init__(self, be, node, S, F=F_TRACE):
+        self.be, self.node, self.S, self.F = be, node, S, F
+        self.self = node - 1
+        self.pending = {}   # slot -> [(index, is_snap)] sent since the last Ready
+        self.hb = {}        # slot -> heartbeat commit since the last Ready
+        self.c_before = None
+        self.checked = {"rounds": 0, "sends": 0, "status": 0, "heartbeats": 0, "progress": 0}
+
+    def slot(self, node_id):
+        return node_id - 1
+
+    # -- state set-up ------------------------------------------------------
+    def load(self, li, committed, runs, first_index, peers, snap_index=None, term_start=None):
+        lg = {"runs": runs, "committed": committed, "first_index": first_index,
+              "last_index": li,
+              "term_start": term_start if term_start is not None else runs[-1][0]}
+        if snap_index is not None:
+            lg["snap_index"] = snap_index
+        sc = {"name": "", "S": self.S, "self": self.self, "max_ents": 0, "log": lg,
+              "peers": peers}
+        self.be.load(sc, initial_arrays(sc))
+
+    def become_leader(self, li, committed, runs, first_index):
+        """becomeLeader (raft.go:724-759) after a won election: reset()
+        (:590-613) gives every Progress Match 0, Next = lastIndex + 1, the
+        leader's own Match = lastIndex, which BecomeReplicate makes Replicate;
+        pendingConfIndex = lastIndex; then appendEntry(empty) through
+        qe_propose (QE_PROP_APPEND_ONLY) and stepCandidate's bcastAppend
+        (:1405-1407) through qe_progress_send."""
+        peers = []
+        for s in range(self.S):
+            if s == self.self:
+                peers.append({"match": li, "next": li + 1, "pending": 0, "state": 1,
+                              "probe_sent": False, "recent_active": False, "ring": []})
+            else:
+                peers.append({"match": 0, "next": li + 1, "pending": 0, "state": 0,
+                              "probe_sent": False, "recent_active": False, "ring": []})
+        self.load(li, committed, runs, first_index, peers)
+        self.be.pci = li
+        out = self.be.propose(1, append_only=True)
+        assert out["result"] == 1
+        self.bcast()
+
+    def bcast(self):
+        """bcastAppend: sendAppend to every peer but the leader."""
+        nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
+        want = sum(1 << s for s in range(self.S) if s != self.self)
+        out = self.be.send(want, 1)
+        for s in range(self.S):
+            if (out["sent"] >> s) & 1:
+                snap = bool((out["snap"] >> s) & 1)
+                idx = self.be.peer(s)["pending"] if snap else nxt[s] - 1
+                self.pending.setdefault(s, []).append((idx, snap))
+
+    # -- replay --------------------------------------------------------------
+    def recv(self, block):
+        msgs = [m for m in block["msgs"] if m["to"] == self.node and m["type"] != "MsgVoteResp"]
+        if not msgs:
+            return
+        rounds, cur = [], []
+        for m in msgs:
+            if cur and self.slot(m["from"]) <= self.slot(cur[-1]["from"]):
+                rounds.append(cur)
+                cur = []
+            cur.append(m)
+        rounds.append(cur)
+        if self.c_before is None:
+            self.c_before = self.be.committed()
+        for rnd in rounds:
+            t = np.zeros(self.S, np.uint8)
+            idx = np.zeros(self.S, np.uint64)
+            hint = np.zeros(self.S, np.uint64)
+            lt = np.zeros(self.S, np.uint64)
+            for m in rnd:
+                s = self.slot(m["from"])
+                if m["type"] == "MsgAppResp":
+                    t[s] = 2 if m["reject"] else 1
+                    idx[s], hint[s], lt[s] = m["index"], m["hint"], m["logterm"]
+                elif m["type"] == "MsgHeartbeatResp":
+                    t[s] = 3
+                else:
+                    raise AssertionError(f"unexpected message at the leader: {m}")
+            out = self.be.step(t, idx, hint, lt)
+            self.checked["rounds"] += 1
+            for s in range(self.S):
+                n = int(out["msg_count"][s])
+                if n:
+                    snap = bool((out["snap"] >> s) & 1)
+                    self.pending.setdefault(s, []).extend(
+                        [(int(out["msg_index"][s]), snap)] + [(None, False)] * (n - 1))
+        for line in block.get("debug", []):
+            d = re.search(r"decreased progress of (\d+) to \[(.*)\]", line)
+            if d:
+                want = parse_progress(d.group(2))
+                got = self.be.peer(self.slot(int(d.group(1))))
+                for k in ("state", "match", "next"):
+                    assert got[k] == want[k], (line, got)
+                self.checked["progress"] += 1
+
+    def heartbeat(self):
+        commit, _, sent = self.be.heartbeat()
+        for s in range(self.S):
+            if (sent >> s) & 1:
+                self.hb[s] = int(commit[s])
+
+    def ready(self, block, where):
+        sends = {}
+        hbs = {}
+        for m in block["msgs"]:
+            if m["from"] != self.node:
+                continue
+            s = self.slot(m["to"])
+            if m["type"] in ("MsgApp", "MsgSnap"):
+                sends.setdefault(s, []).append(m)
+            elif m["type"] == "MsgHeartbeat":
+                hbs[s] = m["commit"]
+        got_slots = {s for s, v in self.pending.items() if v}
+        assert got_slots == set(sends), (where, "destinations", sorted(got_slots), sorted(sends))
+        for s, ms in sends.items():
+            got = self.pending[s]
+            assert len(got) == len(ms), (where, s, got, ms)
+            first = ms[0]
+            want_ix = first["snap_index"] if first["type"] == "MsgSnap" else first["index"]
+            assert got[0] == (want_ix, first["type"] == "MsgSnap"), (where, s, got[0], first)
+            li = self.be.last_index()
+            for m in ms:  # MaxSizePerMsg noLimit: a MsgApp carries every entry after its Log index
+                if m["type"] == "MsgApp":
+                    assert [e[1] for e in m["entries"]] == list(range(m["index"] + 1, li + 1)), \
+                        (where, s, m, li)
+            p = self.be.peer(s)
+            if first["type"] == "MsgSnap":
+                assert p["state"] == 2 and p["pending"] == first["snap_index"], (where, p)
+            elif p["state"] == 0:  # a probe does not move Next
+                assert p["next"] == first["index"] + 1, (where, s, p)
+            elif p["state"] == 1:  # Replicate: past the last entry sent
+                last = ms[-1]
+                end = last["entries"][-1][1] if last["entries"] else last["index"]
+                assert p["next"] == end + 1, (where, s, p, last)
+            self.checked["sends"] += len(ms)
+        c = self.be.committed()
+        apps = [m for ms in sends.values() for m in ms if m["type"] == "MsgApp"]
+        if apps:
+            assert max(m["commit"] for m in apps) == c, (where, c, apps)
+        if block.get("commit") is not None and block.get("node") == self.node:
+            assert block["commit"] == c, (where, block["commit"], c)
+        assert self.hb == hbs, (where, self.hb, hbs)
+        self.checked["heartbeats"] += len(hbs)
+        self.pending, self.hb, self.c_before = {}, {}, None
+
+    def status(self, block, where):
+        for k, text in block["progress"].items():
+            got = progress_string(self.be.peer(self.slot(int(k))), self.F)
+            assert got == text, (where, k, got, text)
+            self.checked["status"] += 1
+
+    def replay(self, cmds, start_line, stop_line=None, on_election=None):
+        """Walk the commands of a trace from start_line: the leader's recv /
+        Ready / status blocks and its tick-heartbeat commands."""
+        for c in cmds:
+            if c["line"] < start_line or (stop_line is not None and c["line"] >= stop_line):
+                continue
+            where = f"line {c['line']} `{c['cmd']}`"
+            if c["cmd"] == f"tick-heartbeat {self.node}":
+                self.heartbeat()
+            for b in c["blocks"]:
+                if b["kind"] == "status":
+                    if c["cmd"] == f"status {self.node}":
+                        self.status(b, where)
+                    continue
+                node = b["node"]
+                if node is None and c["cmd"] == f"process-ready {self.node}":
+                    node = self.node
+                if node != self.node:
+                    continue
+                if b["kind"] == "recv":
+                    votes = [m for m in b["msgs"] if m["type"] == "MsgVoteResp"]
+                    if votes and on_election:
+                        on_election(votes)
+                    self.recv(b)
+                else:
+                    if any(m["type"] == "MsgVote" for m in b["msgs"]):
+                        continue  # the candidate's vote requests
+                    self.ready(b, where)
+        assert not any(self.pending.values()), ("sends never reported", self.pending)
+        return self.checked
+
+
+def command(cmds, text):
+    return next(c for c in cmds if c["cmd"] == text)
+
+
+def election(elector, S, self_slot, term0, votes, want_term):
+    """The candidate side through scripted qe_election_steps on one group
+    (a follower at term0, every slot a voter): a MsgHup step
+    (becomeCandidate: term + 1, the self-vote), then one step with the vote
+    responses the trace shows -> StateLeader at want_term.
+    elector(S, self_slot, term0) -> step(resp, grant, hup) -> (term, state)."""
+    step = elector(S, self_slot, term0)
+    term, state = step(0, 0, 1)
+    assert (term, state) == (want_term, 1), (term, state)  # StateCandidate
+    resp = sum(1 << (m["from"] - 1) for m in votes)
+    grant = sum(1 << (m["from"] - 1) for m in votes if not m["reject"])
+    term, state = step(resp, grant, 0)
+    assert (term, state) == (want_term, 2), (term, state)  # StateLeader
+
+
+def _info(cmds, pattern):
+    for c in cmds:
+        for b in c["blocks"]:
+            for line in b.get("debug", []):
+                m = re.search(pattern, line)
+                if m:
+                    return m
+    return None
+
+
+def probe_and_replicate(leader_factory, elector):
+    """raft/testdata/probe_and_replicate.txt from `campaign 1` (Figure 7 of
+    the Raft paper, shifted by 10).  Node 1's log is the trace's `raft-log 1`
+    dump after the snapshot at index 10 (term 1, add-nodes index=10);
+    committed 18 is the HardState of the candidate's first Ready; the term
+    before the campaign is 7 (its INFO line)."""
+    cmds = traces()["probe_and_replicate.txt"]["commands"]
+    log = command(cmds, "raft-log 1")["log"]
+    li = log[-1][1]
+    camp = command(cmds, "campaign 1")
+    L = leader_factory(1, 7)
+    runs = log_runs(log, [1, 10])
+    assert runs == [[10, 1], [14, 4], [16, 5], [18, 6]] and li == 20
+    state = {}
+
+    def won(votes):
+        election(elector, 7, 0, 7, votes, 8)
+        L.become_leader(li, 18, runs + [[li + 1, 8]], 11)
+        state["won"] = True
+
+    checked = L.replay(cmds, camp["line"] + 1, on_election=won)
+    assert state.get("won")
+    return checked
+
+
+def snapshot_succeed_via_app_resp(leader_factory, elector):
+    """raft/testdata/snapshot_succeed_via_app_resp.txt from its first
+    `status 1`: the state is the one that status prints (3 voters, node 3
+    paused in StateProbe, inactive); node 1's log is the snapshot at 10
+    (term 1) plus its empty entry 11 (term 1), compacted through 11
+    (`compact 1 11`: firstIndex 12, snapshot index 11), committed 11."""
+    cmds = traces()["snapshot_succeed_via_app_resp.txt"]["commands"]
+    st = command(cmds, "status 1")
+    L = leader_factory(1, 3)
+    peers = [parse_progress(st["blocks"][0]["progress"][str(k)]) for k in (1, 2, 3)]
+    L.load(11, 11, [[11, 1]], 12, peers, snap_index=11, term_start=11)
+    return L.replay(cmds, st["line"])
+
+
+def campaign(leader_factory, elector):
+    """raft/testdata/campaign.txt: 3 voters, each log the snapshot at 2
+    (term 1; newRaft's INFO: commit 2, lastindex 2, lastterm 1), node 1
+    campaigns from term 0."""
+    cmds = traces()["campaign.txt"]["commands"]
+    L = leader_factory(1, 3)
+    state = {}
+
+    def won(votes):
+        election(elector, 3, 0, 0, votes, 1)
+        L.become_leader(2, 2, [[2, 1]], 3)
+        state["won"] = True
+
+    checked = L.replay(cmds, command(cmds, "campaign 1")["line"], on_election=won)
+    assert state.get("won")
+    return checked
+
+
+def campaign_learner_must_vote(leader_factory, elector):
+    """raft/testdata/campaign_learner_must_vote.txt from `campaign 2`: node
+    2's config has voters 1, 2, 3 (the promotion of 3 is applied), its log
+    the snapshot at 2 (term 1), 3@1 (node 1's empty entry) and 4@1 (the
+    conf change), committed 4; it campaigns from term 1 (its INFO line) and
+    node 1 is down."""
+    cmds = traces()["campaign_learner_must_vote.txt"]["commands"]
+    L = leader_factory(2, 3)
+    state = {}
+
+    def won(votes):
+        election(elector, 3, 1, 1, votes, 2)
+        L.become_leader(4, 4, [[2, 1], [5, 2]], 3)
+        state["won"] = True
+
+    checked = L.replay(cmds, command(cmds, "campaign 2")["line"], on_election=won)
+    assert state.get("won")
+    return checked
+
+
+TRACES = [probe_and_replicate, snapshot_succeed_via_app_resp, campaign,
+          campaign_learner_must_vote]
