@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liborc.so")
+# QE_ORC_LIB: a sanitizer build of the same source (tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("QE_ORC_LIB", os.path.join(HERE, "build", "liborc.so"))
 INF = (1 << 64) - 1
 NSTAT = 16
 
