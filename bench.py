@@ -975,11 +975,25 @@ def valu_roofline(workload, kern_ms, units):
     if not v:
         return None
     ach = v / (kern_ms / 1000.0)
-    return {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_WIPS,
-            "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WIPS,
-            "valu_insts_per_launch": v, "valu_per_unit": v / units,
-            "lane_ops_per_unit": 64 * v / units,
-            "source": load_pmc(workload).get("profile")}
+    out = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_WIPS,
+           "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WIPS,
+           "valu_insts_per_launch": v, "valu_per_unit": v / units,
+           "lane_ops_per_unit": 64 * v / units,
+           "source": load_pmc(workload).get("profile")}
+    # the SIMD-cycle view (scripts/valu_cost.py): each opcode at its measured
+    # issue cost (v_mul_lo_u32 and v_bcnt_u32_b32 take two full-rate slots),
+    # over the kernel's own shader cycles in the same PMC pass
+    try:
+        with open(os.path.join(ROOT, "profiles", "valu_cost.json")) as f:
+            vc = json.load(f)["workloads"].get(workload)
+    except (OSError, ValueError, KeyError):
+        vc = None
+    if vc:
+        out.update(cycles_frac=vc["cycles_frac"], insts_frac_measured_clock=vc["insts_frac"],
+                   avg_cycles_per_inst=vc["avg_cycles_per_inst"],
+                   full_rate_cycles_per_inst=vc["full_rate_cycles"],
+                   cycles_source="profiles/valu_cost.json")
+    return out
 
 
 def run_workload(name, args, d, steps, warmup):

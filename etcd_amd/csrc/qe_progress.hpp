@@ -38,6 +38,9 @@
 #pragma once
 #include "qe_stream.hpp"
 
+#ifndef QE_PSTEP_PIPE  // variant build only (A/B): 1 = the pipelined slot loop
+#define QE_PSTEP_PIPE 0  // (unrolled, fixed memory-op count per slot, ring loaded
+#endif                   // with the next slot's prefetch; F <= kRingChunk only)
 namespace qe {
 
 constexpr int kRingChunk = 8;  // F <= kRingChunk: the ring lives in registers (row form)
@@ -329,10 +332,11 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
 // epoch unless the peer is wide).
 __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
                                               uint32_t (&lo)[kRingChunk],
-                                              uint32_t (&hi)[kRingChunk]) {
+                                              uint32_t (&hi)[kRingChunk],
+                                              const uint32_t *pre = nullptr) {
 #pragma unroll
-  for (int k = 0; k < kRingChunk; k++) lo[k] = 0u;
-  if (__builtin_amdgcn_ballot_w64(ld)) {
+  for (int k = 0; k < kRingChunk; k++) lo[k] = (pre && ld) ? pre[k] : 0u;
+  if (!pre && __builtin_amdgcn_ballot_w64(ld)) {
     const u32x4 a = bld128(x.rlo, ld ? x.lb : kOOB);
     lo[0] = a.x, lo[1] = a.y, lo[2] = a.z, lo[3] = a.w;
     if (FP > 4) {
@@ -348,6 +352,9 @@ __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t 
     const u32x4 a = bld128(x.rhi, w ? x.lb : kOOB);
     u32x4 b = {0, 0, 0, 0};
     if (FP > 4) b = bld128(x.rhi, w ? x.lb + 16 : kOOB);
+    if constexpr (QE_PSTEP_PIPE != 0)  // waited here, on this (rare) path only
+      asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z),
+                   "v"(b.w));
     if (w) hi[0] = a.x, hi[1] = a.y, hi[2] = a.z, hi[3] = a.w;
     if (w) hi[4] = b.x, hi[5] = b.y, hi[6] = b.z, hi[7] = b.w;
   }
@@ -389,7 +396,8 @@ __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun
                                                uint32_t (&lo)[kRingChunk],
                                                uint32_t (&hi)[kRingChunk]) {
   const bool any = (r1.n | r2.n) != 0;
-  if (!__builtin_amdgcn_ballot_w64(touched && any)) return;  // the ring stands as loaded
+  if (QE_PSTEP_PIPE == 0 && !__builtin_amdgcn_ballot_w64(touched && any))
+    return;  // the ring stands as loaded
   const bool wl = touched && any;
   {
     // Common case: every appended entry and every old one share one upper
@@ -414,7 +422,7 @@ __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun
         lo[k] = j2 < r2.n ? run_lo_at(L2, j2, x.me) : (j1 < r1.n ? run_lo_at(L1, j1, x.me) : lo[k]);
       }
       if (wl) p.rep = p.count ? QE_PW_EPOCH_BITS(h) : 0u;
-      if (__builtin_amdgcn_ballot_w64(wl)) {
+      if (QE_PSTEP_PIPE != 0 || __builtin_amdgcn_ballot_w64(wl)) {
         bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, wl ? x.lb : kOOB);
         if (FP > 4) bst128(u32x4{lo[4], lo[5], lo[6], lo[7]}, x.rlo, wl ? x.lb + 16 : kOOB);
       }
@@ -542,6 +550,7 @@ struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's tur
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
   uint32_t rc;                  // the context number a MsgHeartbeatResp carries
+  uint32_t rl[QE_PSTEP_PIPE ? kRingChunk : 1];  // PIPE: the ring's low words, prefetched
 };
 
 // Loads of slot row `row` (= s*stride + tile0): Next and the packed word of
@@ -557,6 +566,20 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
                                         bool has_ix, bool rcl, PB &b) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
+  if constexpr (QE_PSTEP_PIPE != 0) {  // fixed count: every load issued, unused lanes dropped
+    const rsrc_t rr = mk_rsrc(a.ilo + row * a.FP, n * a.FP * 4);
+    const uint32_t lb = lane * a.FP * 4;
+    const u32x4 x0 = bld128(rr, ld ? lb : kOOB);
+    const u32x4 x1 = bld128(rr, (ld && a.FP > 4) ? lb + 16 : kOOB);
+    b.rl[0] = x0.x, b.rl[1] = x0.y, b.rl[2] = x0.z, b.rl[3] = x0.w;
+    b.rl[4] = x1.x, b.rl[5] = x1.y, b.rl[6] = x1.z, b.rl[7] = x1.w;
+    b.nx = bld64(mk_rsrc(a.next + row, n * 8), ld ? lane * 8 : kOOB);
+    b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
+    b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
+    b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
+    b.rc = bld32(opt_rsrc(a.read_ctx, row, n), rcl ? lane * 4 : kOOB);
+    return;
+  }
   if (__builtin_amdgcn_ballot_w64(ld)) {
     b.nx = bld64(mk_rsrc(a.next + row, n * 8), ld ? lane * 8 : kOOB);
     b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
@@ -582,6 +605,7 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 // next slot starts (vmcnt counts stores, in issue order).  S = 7 4.89 ->
 // 4.68 ms, joint 4.26 -> 4.07 ms (profiles/r04/pstep_ab.txt).
 __device__ __forceinline__ void pb_ready(const PB &b) {
+  if constexpr (QE_PSTEP_PIPE != 0) return;  // PIPE: consumed one slot later
   asm volatile("" ::"v"(b.nx), "v"(b.w), "v"(b.hn), "v"(b.lt), "v"(b.rc));
 }
 
@@ -614,7 +638,7 @@ k_progress_step(PArgs a) {
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * WPB;
   const uint64_t ntiles = (a.G + 63) / 64;
   const uint32_t F = a.F;
-  const bool row_ring = F <= CH;  // wave-uniform
+  const bool row_ring = QE_PSTEP_PIPE != 0 || F <= CH;  // wave-uniform (PIPE: F <= CH only)
   const uint32_t o8 = lane * 8;
   // per wave: Match and m.Index of every slot (phase 1's rows, read again in
   // phase 2) and the group's term runs once a slot needs them
@@ -778,7 +802,11 @@ k_progress_step(PArgs a) {
     const uint32_t ringm = tchm & ((appm & upd) | hbm);
     // rolled over the slots (one copy of the per-peer code; the next slot's
     // loads are issued before this slot's work)
+#if QE_PSTEP_PIPE
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (uint32_t s = 0; s < static_cast<uint32_t>(S); s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const uint32_t tt = ty_of(s);
@@ -789,7 +817,7 @@ k_progress_step(PArgs a) {
                 ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
                 ((rcm >> (s + 1)) & 1u) != 0, nxt);
       }
-      if (!__builtin_amdgcn_ballot_w64(touched)) {
+      if (QE_PSTEP_PIPE == 0 && !__builtin_amdgcn_ballot_w64(touched)) {
         // no event for this slot in any group of the tile (e.g. the leader's
         // own slot): only the per-peer output
         pb_ready(nxt);
@@ -813,6 +841,7 @@ k_progress_step(PArgs a) {
       uint64_t pd0 = 0;
       if (__builtin_amdgcn_ballot_w64(need_pd)) {
         pd0 = bld64(mk_rsrc(a.pending + row, n * 8), need_pd ? o8 : kOOB);
+        if constexpr (QE_PSTEP_PIPE != 0) asm volatile("" ::"v"(pd0));  // (rare path's wait)
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
@@ -830,7 +859,8 @@ k_progress_step(PArgs a) {
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
       if (row_ring) {
-        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi);
+        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi,
+                      QE_PSTEP_PIPE != 0 ? cur.rl : nullptr);
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
@@ -996,14 +1026,23 @@ k_progress_step(PArgs a) {
       const bool fm = wm, fn = wn, fw = ww;
       // the ring representation bits are not Progress state (not counted)
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
-      if (__builtin_amdgcn_ballot_w64(wm)) bst64(p.match, mk_rsrc(a.match + row, n * 8), fm ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), fn ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(wp))
+      constexpr bool PIPE = QE_PSTEP_PIPE != 0;  // PIPE: a fixed store count per slot
+      if (PIPE || __builtin_amdgcn_ballot_w64(wm))
+        bst64(p.match, mk_rsrc(a.match + row, n * 8), fm ? o8 : kOOB);
+      if (PIPE || __builtin_amdgcn_ballot_w64(wn))
+        bst64(p.next, mk_rsrc(a.next + row, n * 8), fn ? o8 : kOOB);
+      if (PIPE || __builtin_amdgcn_ballot_w64(wp))
         bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
-      if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), fw ? lane * 4 : kOOB);
-      if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
-      if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
-        bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
+      if (PIPE || __builtin_amdgcn_ballot_w64(ww))
+        bst32(nw, mk_rsrc(a.pw + row, n * 4), fw ? lane * 4 : kOOB);
+      if (PIPE) {  // optional outputs through a descriptor with no records when NULL
+        bst8(x.count_msgs, opt_rsrc(a.msg_count, row, n), lane);
+        bst64(x.first_index, opt_rsrc(a.msg_index, row, n), x.count_msgs ? o8 : kOOB);
+      } else {
+        if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
+        if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
+          bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
+      }
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);

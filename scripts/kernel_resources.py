@@ -81,7 +81,7 @@ def main():
                             "qe::k_collect", "qe::k_election<5,"]
     res = {}
     with tempfile.TemporaryDirectory() as tmp:
-        for obj in sorted(glob.glob(os.path.join(ROOT, "etcd_amd", "build", "*.o"))):
+        for obj in sorted(glob.glob(os.path.join(ROOT, "etcd_amd", os.environ.get("QE_KR_BUILD", "build"), "*.o"))):
             try:
                 co = code_object(obj, tmp)
             except subprocess.CalledProcessError:
