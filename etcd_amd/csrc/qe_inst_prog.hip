@@ -18,19 +18,30 @@ using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
 #define QE_CAT2(a, b) a##b
 #define QE_CAT(a, b) QE_CAT2(a, b)
 
-template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64>
-static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64, bool P = false>
+static int launch_progress_step_p(const PArgs &a, bool masked, bool joint, hipStream_t st) {
   // the same waves as the 4-wave grid, in blocks of WPB waves
   const uint64_t nb = static_cast<uint64_t>(grid_for((a.G + 63) / 64, 0, 1)) * ((kBlock / 64) / WPB);
   const dim3 grid(static_cast<unsigned>(nb < 0x7FFFFFFFull ? nb : 0x7FFFFFFFull));
   const dim3 blk(64 * WPB);
   if (joint)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
   else if (masked)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, RD, WPB>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
   return hip_status(hipGetLastError());
+}
+
+// the pipelined slot loop (qe_progress.hpp) for rings in row form, up to 9
+// slots and the 4-run table (3 waves/SIMD; with the 8-run table it needs
+// 176-195 VGPRs from S = 6, 2 waves); the rolled loop otherwise
+template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64>
+static int launch_progress_step(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  if constexpr (S <= 9 && RM <= 4 && !ACCT) {
+    if (a.F <= kRingChunk) return launch_progress_step_p<RM, ACCT, RD, WPB, true>(a, masked, joint, st);
+  }
+  return launch_progress_step_p<RM, ACCT, RD, WPB, false>(a, masked, joint, st);
 }
 
 // qe_progress_send: chunks of up to kSendTPW tiles per wave (as the stream

@@ -38,9 +38,6 @@
 #pragma once
 #include "qe_stream.hpp"
 
-#ifndef QE_PSTEP_PIPE  // variant build only (A/B): 1 = the pipelined slot loop
-#define QE_PSTEP_PIPE 0  // (unrolled, fixed memory-op count per slot, ring loaded
-#endif                   // with the next slot's prefetch; F <= kRingChunk only)
 namespace qe {
 
 constexpr int kRingChunk = 8;  // F <= kRingChunk: the ring lives in registers (row form)
@@ -330,6 +327,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
 // read or rewritten (`ld`: touched, with live entries) in registers, one or
 // two 16-byte loads per lane; hi[] holds every position's upper word (the
 // epoch unless the peer is wide).
+template <bool P>
 __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
                                               uint32_t (&lo)[kRingChunk],
                                               uint32_t (&hi)[kRingChunk],
@@ -352,7 +350,7 @@ __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t 
     const u32x4 a = bld128(x.rhi, w ? x.lb : kOOB);
     u32x4 b = {0, 0, 0, 0};
     if (FP > 4) b = bld128(x.rhi, w ? x.lb + 16 : kOOB);
-    if constexpr (QE_PSTEP_PIPE != 0)  // waited here, on this (rare) path only
+    if constexpr (P)  // waited here, on this (rare) path only
       asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z),
                    "v"(b.w));
     if (w) hi[0] = a.x, hi[1] = a.y, hi[2] = a.z, hi[3] = a.w;
@@ -390,13 +388,14 @@ __device__ __forceinline__ uint32_t run_lo_at(const RunLo &L, uint32_t j, uint32
   return L.lob + (j < L.jcap ? (j + 1) * me - 1u : L.lod);
 }
 
+template <bool P>
 __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun &r1,
                                                const PRun &r2, bool touched, uint32_t rep_in,
                                                uint32_t c_old, uint32_t FP,
                                                uint32_t (&lo)[kRingChunk],
                                                uint32_t (&hi)[kRingChunk]) {
   const bool any = (r1.n | r2.n) != 0;
-  if (QE_PSTEP_PIPE == 0 && !__builtin_amdgcn_ballot_w64(touched && any))
+  if (!P && !__builtin_amdgcn_ballot_w64(touched && any))
     return;  // the ring stands as loaded
   const bool wl = touched && any;
   {
@@ -422,7 +421,7 @@ __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun
         lo[k] = j2 < r2.n ? run_lo_at(L2, j2, x.me) : (j1 < r1.n ? run_lo_at(L1, j1, x.me) : lo[k]);
       }
       if (wl) p.rep = p.count ? QE_PW_EPOCH_BITS(h) : 0u;
-      if (QE_PSTEP_PIPE != 0 || __builtin_amdgcn_ballot_w64(wl)) {
+      if (P || __builtin_amdgcn_ballot_w64(wl)) {
         bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, wl ? x.lb : kOOB);
         if (FP > 4) bst128(u32x4{lo[4], lo[5], lo[6], lo[7]}, x.rlo, wl ? x.lb + 16 : kOOB);
       }
@@ -545,12 +544,29 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint32_t (&lo)[kRingChun
 // set) runs in registers; phase 2 walks the slots, each peer's whole event
 // sequence at once, with the next slot's loads issued before this slot's
 // work.
+//
+// Two forms of the slot loop (template P):
+// - rolled (P = false; any F, the memory form of the rings): one copy of
+//   the per-peer code, loads and stores skipped by wave ballots where no lane
+//   needs them, and the next slot's loads retired before the slot's first
+//   store (pb_ready);
+// - pipelined (P = true; rings in row form, F <= kRingChunk, S <= 9): the
+//   loop spelled out over the slots, with a FIXED memory-instruction count
+//   per slot -- every load and store issued, lanes that do not need one
+//   dropped by an out-of-range offset -- and the ring's low words loaded with
+//   the slot's other Progress loads one slot ahead.  hipcc's s_waitcnt
+//   bookkeeping then sees the same instruction sequence on every path and
+//   waits, at each slot's first use, for exactly that slot's prefetch
+//   (vmcnt(N), N = the instructions issued after it: the previous slot's
+//   stores and the next slot's loads), where the rolled form's merged paths
+//   wait vmcnt(0) at the ring load: S = 5 3.30 -> 2.80 ms, joint 4.14 ->
+//   3.68, S = 7 4.74 -> 4.45 ms (profiles/r05/pstep_pipe_ab*.txt).
 // ---------------------------------------------------------------------------
 struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's turn)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
   uint32_t rc;                  // the context number a MsgHeartbeatResp carries
-  uint32_t rl[QE_PSTEP_PIPE ? kRingChunk : 1];  // PIPE: the ring's low words, prefetched
+  uint32_t rl[kRingChunk];      // pipelined loop: the ring's low words, prefetched
 };
 
 // Loads of slot row `row` (= s*stride + tile0): Next and the packed word of
@@ -561,16 +577,18 @@ struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's tur
 // A wave-level branch skips each group of loads no lane needs (an issued
 // vector memory instruction costs the CU's memory path about the same
 // whether or not its lanes are masked off).
+template <bool P>
 __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *l_mix,
                                         uint32_t n, uint32_t lane, bool ld, bool rej,
                                         bool has_ix, bool rcl, PB &b) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
-  if constexpr (QE_PSTEP_PIPE != 0) {  // fixed count: every load issued, unused lanes dropped
+  if constexpr (P) {  // fixed count: every load issued, unused lanes dropped
     const rsrc_t rr = mk_rsrc(a.ilo + row * a.FP, n * a.FP * 4);
     const uint32_t lb = lane * a.FP * 4;
-    const u32x4 x0 = bld128(rr, ld ? lb : kOOB);
-    const u32x4 x1 = bld128(rr, (ld && a.FP > 4) ? lb + 16 : kOOB);
+    const bool rl = ld;  // (P: row form only)
+    const u32x4 x0 = bld128(rr, rl ? lb : kOOB);
+    const u32x4 x1 = bld128(rr, (rl && a.FP > 4) ? lb + 16 : kOOB);
     b.rl[0] = x0.x, b.rl[1] = x0.y, b.rl[2] = x0.z, b.rl[3] = x0.w;
     b.rl[4] = x1.x, b.rl[5] = x1.y, b.rl[6] = x1.z, b.rl[7] = x1.w;
     b.nx = bld64(mk_rsrc(a.next + row, n * 8), ld ? lane * 8 : kOOB);
@@ -604,8 +622,9 @@ __device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint
 // would otherwise wait vmcnt(0) -- draining the slot's own stores before the
 // next slot starts (vmcnt counts stores, in issue order).  S = 7 4.89 ->
 // 4.68 ms, joint 4.26 -> 4.07 ms (profiles/r04/pstep_ab.txt).
+template <bool P>
 __device__ __forceinline__ void pb_ready(const PB &b) {
-  if constexpr (QE_PSTEP_PIPE != 0) return;  // PIPE: consumed one slot later
+  if constexpr (P) return;  // pipelined: consumed one slot later, waited exactly
   asm volatile("" ::"v"(b.nx), "v"(b.w), "v"(b.hn), "v"(b.lt), "v"(b.rc));
 }
 
@@ -614,9 +633,10 @@ __device__ __forceinline__ void pb_ready(const PB &b) {
 #endif
 
 // WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
-// (21 KB at S = 5) would allow one 4-wave block per CU
+// (21 KB at S = 5) would allow one 4-wave block per CU.  P: the pipelined
+// slot loop (above; the launcher picks it for row-form rings).
 template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, bool RD,
-          int WPB = kBlock / 64>
+          int WPB = kBlock / 64, bool P = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
                           amdgpu_waves_per_eu(S <= 9 ? QE_PSTEP_WAVES : 2))) void
 k_progress_step(PArgs a) {
@@ -638,7 +658,13 @@ k_progress_step(PArgs a) {
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * WPB;
   const uint64_t ntiles = (a.G + 63) / 64;
   const uint32_t F = a.F;
-  const bool row_ring = QE_PSTEP_PIPE != 0 || F <= CH;  // wave-uniform (PIPE: F <= CH only)
+  static_assert(!P || (S <= 9 && !ACCT), "pipelined form: S <= 9, no accounting");
+  const bool row_ring = P || F <= CH;  // wave-uniform (P: the launcher checked F <= CH)
+  // P: the term-run table of every group comes with round trip 1 (bit 1;
+  // not behind a ballot of the rejecting lanes after it, whose merged paths
+  // wait for everything issued); m.Index of every tracked slot with it too
+  // (bit 0) was slower (profiles/r05/pstep_head_ab.txt: S = 5 2.80 -> 2.86 ms)
+  constexpr int HD = P ? 2 : 0;
   const uint32_t o8 = lane * 8;
   // per wave: Match and m.Index of every slot (phase 1's rows, read again in
   // phase 2) and the group's term runs once a slot needs them
@@ -700,14 +726,30 @@ k_progress_step(PArgs a) {
                      ((rd && qn0) ? sizeof(QT) : 0));
     uint64_t m0[S];
     uint32_t ty[S];
+    uint64_t ix[S];
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const bool tr = (trk >> s) & 1u;
       m0[s] = bld64(mk_rsrc(a.match + row, n * 8), o8);
       ty[s] = bld8(mk_rsrc(a.mtype + row, n), tr ? lane : kOOB);
+      // HEAD1: m.Index of every tracked slot now (used only where the type
+      // says MsgAppResp; counted below where it is)
+      if constexpr ((HD & 1) != 0) ix[s] = bld64(mk_rsrc(a.mindex + row, n * 8), tr ? o8 : kOOB);
       ac.add(live, 8);
       ac.add(live && tr, 1);
+    }
+    uint64_t rr0[RM], rr1[RM];  // HEAD1: the term-run table of every group, with round trip 1
+    uint32_t rc_all = 0;
+    if constexpr ((HD & 2) != 0) {
+      rc_all = bld8(opt_rsrc(a.run_count, g0, n), lane);  // (NULL with no log runs)
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        const uint64_t rrow = static_cast<uint64_t>(r) * a.stride + g0;
+        const uint32_t off = static_cast<uint32_t>(r) < a.R ? o8 : kOOB;
+        rr0[r] = bld64(mk_rsrc(a.run_first + rrow, n * 8), off);
+        rr1[r] = bld64(mk_rsrc(a.run_term + rrow, n * 8), off);
+      }
     }
     // message kinds, 4 bits per slot, for the rolled phase-2 loop (kinds
     // above QE_MSG_UNREACHABLE are "no message")
@@ -728,12 +770,11 @@ k_progress_step(PArgs a) {
     // heartbeat responses whose context number is loaded
     const uint32_t rcm = (rd && a.read_ctx) ? (hbm & trk) : 0u;
     // ---- round trip 2: m.Index of every MsgAppResp and slot 0's peer loads ----
-    uint64_t ix[S];
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const bool has_ix = ty[s] == QE_MSG_APP_RESP || ty[s] == QE_MSG_APP_RESP_REJECT;
-      ix[s] = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? o8 : kOOB);
+      if constexpr ((HD & 1) == 0) ix[s] = bld64(mk_rsrc(a.mindex + row, n * 8), has_ix ? o8 : kOOB);
       ac.add(has_ix, 8);
       l_mix[wv][s][0][lane] = m0[s];
       l_mix[wv][s][1][lane] = ix[s];
@@ -742,7 +783,14 @@ k_progress_step(PArgs a) {
     // only user: findConflictByTerm in phase 2), loaded with round trip 2
     // and staged into LDS at once -- not a round trip of its own
     const bool need_runs = (rejm & trk) != 0;
-    if (__builtin_amdgcn_ballot_w64(need_runs)) {
+    if constexpr ((HD & 2) != 0) {
+      nr = need_runs ? (rc_all < a.R ? rc_all : a.R) : 0u;
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        l_run[wv][r][0][lane] = rr0[r];
+        l_run[wv][r][1][lane] = rr1[r];
+      }
+    } else if (__builtin_amdgcn_ballot_w64(need_runs)) {
       const uint32_t rc = bld8(mk_rsrc(a.run_count + g0, n), need_runs ? lane : kOOB);
       nr = rc < a.R ? rc : a.R;
 #pragma unroll
@@ -758,7 +806,7 @@ k_progress_step(PArgs a) {
     PB cur;
     {  // slot 0, before phase 1: every possible event
       const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
-      pb_load(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
+      pb_load<P>(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
               (rcm & 1u) != 0, cur);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
@@ -783,7 +831,7 @@ k_progress_step(PArgs a) {
         }
       }
     }
-    pb_ready(cur);  // (so no wait at the slot loop's head merges in the stores)
+    pb_ready<P>(cur);  // (so no wait at the slot loop's head merges in the stores)
     // ---- phase 2: every peer's event sequence ----
     PSend x;
     x.F = F;
@@ -802,25 +850,22 @@ k_progress_step(PArgs a) {
     const uint32_t ringm = tchm & ((appm & upd) | hbm);
     // rolled over the slots (one copy of the per-peer code; the next slot's
     // loads are issued before this slot's work)
-#if QE_PSTEP_PIPE
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
+    constexpr int kSlotUnroll = P ? S : 1;
+#pragma unroll kSlotUnroll
     for (uint32_t s = 0; s < static_cast<uint32_t>(S); s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
       const uint32_t tt = ty_of(s);
       const bool touched = ((tchm >> s) & 1u) != 0;
       PB nxt{};  // (the last slot has no next: zeros)
       if (s + 1 < static_cast<uint32_t>(S)) {
-        pb_load(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
+        pb_load<P>(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
                 ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
                 ((rcm >> (s + 1)) & 1u) != 0, nxt);
       }
-      if (QE_PSTEP_PIPE == 0 && !__builtin_amdgcn_ballot_w64(touched)) {
+      if (!P && !__builtin_amdgcn_ballot_w64(touched)) {
         // no event for this slot in any group of the tile (e.g. the leader's
         // own slot): only the per-peer output
-        pb_ready(nxt);
+        pb_ready<P>(nxt);
         if (a.msg_count) bst8(0u, mk_rsrc(a.msg_count + row, n), lane);
         ac.add(live && a.msg_count, 1);
         if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
@@ -841,7 +886,7 @@ k_progress_step(PArgs a) {
       uint64_t pd0 = 0;
       if (__builtin_amdgcn_ballot_w64(need_pd)) {
         pd0 = bld64(mk_rsrc(a.pending + row, n * 8), need_pd ? o8 : kOOB);
-        if constexpr (QE_PSTEP_PIPE != 0) asm volatile("" ::"v"(pd0));  // (rare path's wait)
+        if constexpr (P) asm volatile("" ::"v"(pd0));  // (rare path's wait)
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
@@ -859,8 +904,7 @@ k_progress_step(PArgs a) {
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
       if (row_ring) {
-        ring_load_row(x, touched && c_old > 0, rep0, a.FP, rlo, rhi,
-                      QE_PSTEP_PIPE != 0 ? cur.rl : nullptr);
+        ring_load_row<P>(x, touched && c_old > 0, rep0, a.FP, rlo, rhi, P ? cur.rl : nullptr);
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
@@ -892,7 +936,7 @@ k_progress_step(PArgs a) {
       const uint32_t k3 = bcast_target ? popc(bset & ~below & ~(1u << s)) : 0u;
       uint32_t k2 = 0;
       bool lp = false;
-      pb_ready(nxt);  // (before the sends: in memory form they append in memory)
+      pb_ready<P>(nxt);  // (before the sends: in memory form they append in memory)
       if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
@@ -1014,7 +1058,7 @@ k_progress_step(PArgs a) {
       const uint32_t km = lp ? kLoop : k2 + k3;
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      if (row_ring) ring_store_row(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
+      if (row_ring) ring_store_row<P>(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
       const bool tw = touched;
@@ -1026,7 +1070,7 @@ k_progress_step(PArgs a) {
       const bool fm = wm, fn = wn, fw = ww;
       // the ring representation bits are not Progress state (not counted)
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
-      constexpr bool PIPE = QE_PSTEP_PIPE != 0;  // PIPE: a fixed store count per slot
+      constexpr bool PIPE = P;  // a fixed store count per slot
       if (PIPE || __builtin_amdgcn_ballot_w64(wm))
         bst64(p.match, mk_rsrc(a.match + row, n * 8), fm ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(wn))

@@ -96,7 +96,8 @@ enum qe_stat {
   QE_STAT_GRANTED = 7,       /* sum of TallyVotes granted                      */
   QE_STAT_REJECTED = 8,      /* sum of TallyVotes rejected                     */
   QE_STAT_COMMIT_ADVANCED = 9,   /* replication: commit advanced this round    */
-  QE_STAT_READ_RELEASED = 10,    /* replication: ReadIndex quorum reached      */
+  QE_STAT_READ_RELEASED = 10,    /* ReadIndex requests released (a request count,
+                                    * not groups; replication: quorum reached)  */
   QE_STAT_ELECTIONS = 11,        /* election sim: campaigns started            */
   QE_STAT_LEADERS = 12,          /* election sim: elections won                */
   QE_STAT_STEPDOWNS = 13,        /* election sim: elections lost               */
@@ -487,7 +488,9 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
  *     :1731-1733: term_start <= committed <= last_index on the log model)
  *     -> QE_RI_POSTPONED (pendingReadIndexMessages; the host keeps the
  *     message and adds it again once qe_progress_step reports term_commit --
- *     its read index is that round's term_commit_index);
+ *     its read index is that round's term_commit_index, NOT the index the
+ *     re-added qe_read_index call returns: releasePendingReadIndexMessages
+ *     runs inside the commit, before later advances of the same round);
  *   lease_based (ReadOnlyLeaseBased) -> QE_RI_RESPOND at committed;
  *   ReadOnlySafe -> readOnly.addRequest(committed) + the leader's own ack
  *     (self_slot; recvAck(r.id)): QE_RI_QUEUED with context number ctx[g]

@@ -22,7 +22,7 @@ read traffic is 2 x FETCH_SIZE.  WRITE_SIZE counts whole 32-B sectors: exact for
 32-B ring (x0.125) and for 16 B of it (x0.5) -- it is the memory-side
 write traffic as is.  (Rounds 1-3 used x1 for the narrow-access kernels,
 which undercounted their reads by half; check_quorum's figure fell below
-its algorithmic bytes.)  usage: summarize_workloads.py <tag> [dir] [bench.log]:
+its algorithmic bytes.)  usage: summarize_workloads.py <tag> [dir] [bench.log ...]:
 with a bench JSON line, every workload's traffic is checked against its
 algorithmic bytes (units x bytes_per_unit) and a figure below it is refused.
 """
@@ -91,7 +91,9 @@ def algorithmic_bytes(bench_log):
 def main():
     tag = sys.argv[1]
     base = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "profw")
-    algo = algorithmic_bytes(sys.argv[3]) if len(sys.argv) > 3 else {}
+    algo = {}
+    for log in sys.argv[3:]:  # one or more bench logs
+        algo.update(algorithmic_bytes(log))
     outd = os.path.join(ROOT, "profiles", tag)
     os.makedirs(outd, exist_ok=True)
     summary, traffic = {}, {}
