@@ -78,6 +78,9 @@ WORKLOADS = {
     "progress_send": ("16M groups x bcastAppend after a proposal (qe_progress_send to the 4 "
                       "followers, StateReplicate, Inflights F=8 with room): one MsgApp and one "
                       "ring entry per peer", 1 << 24, 5, "psend"),
+    "heartbeat": ("16M groups x MsgBeat through qe_heartbeat: bcastHeartbeat to the 4 followers "
+                  "(Commit = min(Match, committed) per follower, the newest pending ReadIndex "
+                  "context of a 0..4-entry queue)", 1 << 24, 5, "heartbeat"),
     "propose": ("16M groups x one MsgProp of 3 entries (24 B of payload) through qe_propose: the "
                 "MsgProp gates, increaseUncommittedSize, appendEntry (lastIndex + 3, the leader's "
                 "MaybeUpdate, maybeCommit) and bcastAppend to the 4 followers (StateReplicate, "
@@ -668,6 +671,46 @@ def setup(name, G, S, kind, d, stats):
 
         return step, bpg, G, "group-proposals", {"ps": ps, "pr": pr, "prepare": prepare,
                                                  "verify": verify}
+
+    if kind == "heartbeat":
+        # stepLeader MsgBeat -> bcastHeartbeat -> sendHeartbeat (raft/raft.go:
+        # 524-541, :494-510): per follower min(Match, committed), the context
+        # of the last pending ReadIndex request (lastPendingRequestCtx)
+        ps = engine.ProgressState(G, S, 8, 1, d.dev, group_offset=goff,
+                                  extras=("self_slot", "reads"), max_ents=0)
+        psend_state(ps)
+        ps.self_slot.fill_(0)
+        ps.committed.copy_(ps.last_index[:G] - 32)
+        qn = counter_rows(G, 1, 0x4EAD, goff, d.dev)[:G] % (engine._lib.QE_READ_QUEUE + 1)
+        ps.read_count.copy_(qn.to(torch.uint8))
+        commit = torch.zeros(S * ps.stride, dtype=torch.int64, device=d.dev)
+        ctx = torch.zeros(G, dtype=torch.int32, device=d.dev)
+        sent = torch.zeros(G, dtype=torch.uint8, device=d.dev)
+        # algorithmic bytes per group: self slot 1, committed 8, the queue's
+        # count 1 and head 4, the context 4 and the sent mask 1 written, and
+        # per follower sent to (4) its Match read and its Commit written
+        bpg = 1 + 8 + 1 + 4 + 4 + 1 + (S - 1) * 16
+        import ctypes as C
+        p_ = ps.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        cp, xp, sp_ = engine._ptr(commit), engine._ptr(ctx), engine._ptr(sent)
+
+        def step():
+            engine.check("qe_heartbeat", lib.qe_heartbeat(C.byref(p_), cp, xp, sp_, stream))
+
+        def verify():
+            full = (1 << S) - 2
+            m = ps.match.view(S, -1)[1:, :G]
+            c = commit.view(S, -1)[1:, :G]
+            want = torch.minimum(m, ps.committed[:G].view(1, G))
+            qh = ps.read_head[:G].to(torch.int64)
+            cx = torch.where(qn > 0, qh + qn - 1, torch.zeros_like(qn))
+            return (bool((sent.to(torch.int32) == full).all()) and bool((c == want).all())
+                    and bool((ctx.to(torch.int64) & 0xFFFFFFFF == cx).all()))
+
+        return step, bpg, G, "group-heartbeats", {"ps": ps, "commit": commit, "ctx": ctx,
+                                                  "sent": sent, "verify": verify}
 
     if kind == "psend":
         # raft.appendEntry -> bcastAppend (raft/raft.go:515-522, :432-492):

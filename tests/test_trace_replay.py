@@ -59,3 +59,57 @@ def test_progress_string_round_trip():
                     p = parse_progress(text)
                     view = dict(p, inflights=len(p["ring"]))
                     assert progress_string(view, F_TRACE) == text
+
+
+def _mutated(monkeypatch, name, edit):
+    """The fixture with one printed value changed (a deep copy), installed
+    where the replay reads it."""
+    import copy
+
+    import tests.trace_replay as tr
+    t = copy.deepcopy(traces())
+    edit(t[name]["commands"])
+    monkeypatch.setattr(tr, "traces", lambda: t)
+
+
+def _first(cmds, pred):
+    for c in cmds:
+        for b in c["blocks"]:
+            for m in b.get("msgs", []):
+                if pred(b, m):
+                    return m
+    raise LookupError("no such message in the fixture")
+
+
+@pytest.mark.parametrize("what", ["reply_index", "reject_hint", "status_line"])
+def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
+    """Negative controls: the replay fails when one printed value differs
+    from what the engine computes -- the index of the MsgApp answering a
+    rejection, the hint a rejection carries (the engine then answers from a
+    different probe), a Progress line of a `status` block."""
+    from tests.trace_replay import probe_and_replicate, snapshot_succeed_via_app_resp
+    if what == "reply_index":
+        def edit(cmds):
+            m = _first(cmds, lambda b, m: b["kind"] == "ready" and b["node"] == 1
+                       and m["type"] == "MsgApp" and m["to"] == 2 and m["index"] == 19)
+            m["index"] = 18
+        name, trace = "probe_and_replicate.txt", probe_and_replicate
+    elif what == "reject_hint":
+        def edit(cmds):
+            m = _first(cmds, lambda b, m: b["kind"] == "recv" and b["node"] == 1
+                       and m["type"] == "MsgAppResp" and m["reject"])
+            m["hint"] = m["hint"] - 2
+        name, trace = "probe_and_replicate.txt", probe_and_replicate
+    else:
+        def edit(cmds):
+            for c in cmds:
+                for b in c["blocks"]:
+                    if b["kind"] == "status" and "pendingSnap=11" in b["progress"].get("3", ""):
+                        b["progress"]["3"] = b["progress"]["3"].replace("pendingSnap=11",
+                                                                        "pendingSnap=12")
+                        return
+            raise LookupError("status line not found")
+        name, trace = "snapshot_succeed_via_app_resp.txt", snapshot_succeed_via_app_resp
+    _mutated(monkeypatch, name, edit)  # (LookupError, not a pass, if the value moved)
+    with pytest.raises(AssertionError):
+        trace(lambda node, S: Leader(OracleRoundBackend(orc), node, S), oracle_elector(orc))
