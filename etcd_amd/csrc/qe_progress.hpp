@@ -560,7 +560,8 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint32_t (&lo)[kRingChun
 //   (vmcnt(N), N = the instructions issued after it: the previous slot's
 //   stores and the next slot's loads), where the rolled form's merged paths
 //   wait vmcnt(0) at the ring load: S = 5 3.30 -> 2.80 ms, joint 4.14 ->
-//   3.68, S = 7 4.74 -> 4.45 ms (profiles/r05/pstep_pipe_ab*.txt).
+//   3.68, S = 7 4.74 -> 4.45 ms (profiles/r05/pstep_pipe_ab*.txt); at S = 7
+//   the loads run two slots ahead (PF2 below).
 // ---------------------------------------------------------------------------
 struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's turn)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
@@ -804,10 +805,21 @@ k_progress_step(PArgs a) {
     bool runs_counted = false;  // ACCT: the run table counts once, when first used
     auto ty_of = [&](uint32_t s) -> uint32_t { return static_cast<uint32_t>(tys >> (4 * s)) & 15u; };
     PB cur;
+    // PF2: the pipelined loop's loads two slots ahead (Match / m.Index then
+    // come from LDS at use).  Measured (profiles/r05/pstep_pf2_ab.txt): S = 7
+    // 4.26 -> 4.07 ms; S = 5 and the joint 6 slots unchanged; at S = 8, 9 it
+    // spills (16-120 B of scratch at the 168-VGPR budget), so S = 7 only
+    constexpr bool PF2 = P && S == 7;
+    PB nx1{};  // PF2: slot s+1's loads while slot s runs
     {  // slot 0, before phase 1: every possible event
       const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
       pb_load<P>(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
               (rcm & 1u) != 0, cur);
+    }
+    if constexpr (PF2 && S > 1) {  // and slot 1
+      const bool ld = ((trk & (msgm | (self != 1u ? 2u : 0u))) & 2u) != 0;
+      pb_load<P>(a, g0 + a.stride, &l_mix[wv][1][0][0], n, lane, ld, (rejm & 2u) != 0,
+                 (ixm & 2u) != 0, (rcm & 2u) != 0, nx1);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
@@ -857,7 +869,16 @@ k_progress_step(PArgs a) {
       const uint32_t tt = ty_of(s);
       const bool touched = ((tchm >> s) & 1u) != 0;
       PB nxt{};  // (the last slot has no next: zeros)
-      if (s + 1 < static_cast<uint32_t>(S)) {
+      if constexpr (PF2) {
+        if (s + 2 < static_cast<uint32_t>(S)) {
+          pb_load<P>(a, row + 2 * a.stride, &l_mix[wv][s + 2][0][0], n, lane,
+                     ((tchm >> (s + 2)) & 1u) != 0, ((rejm >> (s + 2)) & 1u) != 0,
+                     ((ixm >> (s + 2)) & 1u) != 0, ((rcm >> (s + 2)) & 1u) != 0, nxt);
+        }
+        // Match / m.Index from the wave's LDS rows at use (not held two slots)
+        cur.mt = l_mix[wv][s][0][lane];
+        cur.ix = ((ixm >> s) & 1u) ? l_mix[wv][s][1][lane] : 0;
+      } else if (s + 1 < static_cast<uint32_t>(S)) {
         pb_load<P>(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
                 ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
                 ((rcm >> (s + 1)) & 1u) != 0, nxt);
@@ -1095,7 +1116,14 @@ k_progress_step(PArgs a) {
       ac.add(x.count_msgs && a.msg_index, 8);
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
-      if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
+      if (s + 1 < static_cast<uint32_t>(S)) {
+        if constexpr (PF2) {
+          cur = nx1;
+          nx1 = nxt;
+        } else {
+          cur = nxt;
+        }
+      }
     }
     const uint32_t bc = popc(bset);
     bst64(c, r_commit, c != c0 ? o8 : kOOB);

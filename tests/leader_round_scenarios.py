@@ -204,6 +204,39 @@ def read_only_for_new_leader(be):
     assert out["read_released"] == 1
 
 
+def postponed_read_commit_advances_twice(be):
+    """A postponed ReadIndex released in a round whose commit advances twice
+    (derived from raft.go:1259-1262 and :1813-1825; no reference test has
+    this round).  Entries 3..5 of the new term are in flight; slot 1's accept
+    of 4 commits 4 -- the term's first commit, so maybeCommit's caller runs
+    releasePendingReadIndexMessages there and addRequest takes committed = 4
+    -- then slot 2's accept of 5 commits 5 in the same round.  The step
+    reports term_commit_index 4 (the host re-adds the postponed read at it),
+    while the committed index the round ends with, and the one a later
+    MsgReadIndex is answered at, is 5."""
+    S = 3
+    sc = {"name": "", "S": S, "self": 0, "max_ents": 0,
+          "log": {"runs": [[0, 0], [1, 1], [3, 2]], "committed": 1, "term_start": 3,
+                  "first_index": 1, "last_index": 5},
+          "peers": [_peer(5, 6, REPLICATE)] + [_peer(2, 6, REPLICATE, True)
+                                              for _ in range(S - 1)]}
+    be.load(sc, initial_arrays(sc))
+    res, _, _ = be.read_index()
+    assert res == POSTPONED
+    t = np.array([0, 1, 1], np.uint8)
+    idx = np.array([0, 4, 5], np.uint64)
+    z = np.zeros(S, np.uint64)
+    out = be.step(t, idx, z, z)
+    assert out["term_commit"] == 1 and out["term_commit_index"] == 4, out
+    assert be.committed() == 5
+    # the re-added read: queued at the term_commit_index the host passes
+    # on; qe_read_index itself reports the committed index of now (5)
+    res, ctx, index = be.read_index()
+    assert res == QUEUED and index == 5
+    out = _heartbeat_round(be, S, (1, 2), ctx=ctx)
+    assert out["read_released"] == 1 and out["term_commit"] == 0
+
+
 def two_reads_in_flight(be):
     """Two pending requests (derived from readOnly.advance, read_only.go:
     81-112): a response carrying the older context releases only the older
@@ -449,7 +482,8 @@ def add_node_check_quorum(be):
 
 
 SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lease,
-             raft_frees_read_only_mem, read_only_for_new_leader, two_reads_in_flight,
+             raft_frees_read_only_mem, read_only_for_new_leader,
+             postponed_read_commit_advances_twice, two_reads_in_flight,
              read_queue_full, learner_ack_does_not_count,
              leader_stepdown_when_quorum_active, leader_stepdown_when_quorum_lost,
              add_node_check_quorum, leader_transfer_to_up_to_date_node,
