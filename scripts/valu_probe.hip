@@ -23,32 +23,45 @@ constexpr int kPerIter = 32;
 
 // one instruction of each chain: "op a_i, a_i, k" for i = 0..7
 #define R8(T) T(0) T(1) T(2) T(3) T(4) T(5) T(6) T(7)
+// 3-source kinds read a second chain's register as the third operand (three
+// distinct VGPRs, as compiled code has them; a repeated register measured
+// half rate)
+#define R8P(T) T(0, 1) T(1, 2) T(2, 3) T(3, 4) T(4, 5) T(5, 6) T(6, 7) T(7, 0)
 #define I_ADD(i) "v_add_u32 %" #i ", %" #i ", %8\n"
 #define I_XOR(i) "v_xor_b32 %" #i ", %" #i ", %8\n"
 #define I_MUL(i) "v_mul_lo_u32 %" #i ", %" #i ", %8\n"
 #define I_MUL24(i) "v_mul_u32_u24 %" #i ", %" #i ", %8\n"
 #define I_BCNT(i) "v_bcnt_u32_b32 %" #i ", %" #i ", %8\n"
-#define I_BITOP3(i) "v_bitop3_b32 %" #i ", %" #i ", %8, %" #i " bitop3:0x96\n"
+#define I_BITOP3(i, j) "v_bitop3_b32 %" #i ", %" #i ", %8, %" #j " bitop3:0x96\n"
 #define I_CND(i) "v_cndmask_b32_e64 %" #i ", %" #i ", %8, vcc\n"
 #define I_MUL16(i) "v_mul_lo_u16 %" #i ", %" #i ", %8\n"
-#define I_ADD3(i) "v_add3_u32 %" #i ", %" #i ", %8, %" #i "\n"
+#define I_ADD3(i, j) "v_add3_u32 %" #i ", %" #i ", %8, %" #j "\n"
 // 64-bit kinds: a_i are VGPR pairs
 #define I_MAD64(i) "v_mad_u64_u32 %" #i ", vcc, %8, %8, %" #i "\n"
 #define I_LSHLADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 1, %" #i "\n"
 #define I_SHR64(i) "v_lshrrev_b64 %" #i ", 1, %" #i "\n"
 #define I_MOV(i) "v_mov_b32 %" #i ", %8\n"
 #define I_CMP(i) "v_cmp_gt_u32_e64 vcc, %" #i ", %8\n"
+#define I_AND(i) "v_and_b32 %" #i ", %" #i ", %8\n"
+#define I_OR3(i, j) "v_or3_b32 %" #i ", %" #i ", %8, %" #j "\n"
+#define I_SHR(i) "v_lshrrev_b32 %" #i ", 1, %" #i "\n"
+#define I_SUB(i) "v_sub_u32 %" #i ", %" #i ", %8\n"
+#define I_CND32(i) "v_cndmask_b32_e32 %" #i ", %" #i ", %8, vcc\n"
 #define OPS(T) R8(T) R8(T) R8(T) R8(T)  // 32 instructions, 8 independent chains of 4
+#define OPS3(T) R8P(T) R8P(T) R8P(T) R8P(T)
 
 #define KINDS(X)                                                         \
   X(0, u32, I_ADD, "v_add_u32") X(1, u32, I_XOR, "v_xor_b32")           \
   X(2, u32, I_MUL, "v_mul_lo_u32") X(3, u32, I_MUL24, "v_mul_u32_u24")  \
-  X(4, u32, I_BCNT, "v_bcnt_u32_b32") X(5, u32, I_BITOP3, "v_bitop3_b32") \
+  X(4, u32, I_BCNT, "v_bcnt_u32_b32") X3(5, u32, I_BITOP3, "v_bitop3_b32") \
   X(6, u32, I_CND, "v_cndmask_b32") X(7, u32, I_MUL16, "v_mul_lo_u16")  \
-  X(8, u32, I_ADD3, "v_add3_u32") X(9, u64, I_MAD64, "v_mad_u64_u32")   \
+  X3(8, u32, I_ADD3, "v_add3_u32") X(9, u64, I_MAD64, "v_mad_u64_u32")   \
   X(10, u64, I_LSHLADD64, "v_lshl_add_u64") X(11, u64, I_SHR64, "v_lshrrev_b64") \
-  X(12, u32, I_MOV, "v_mov_b32") X(13, u32, I_CMP, "v_cmp_gt_u32")
-constexpr int kKinds = 14;
+  X(12, u32, I_MOV, "v_mov_b32") X(13, u32, I_CMP, "v_cmp_gt_u32")                 \
+  X(14, u32, I_AND, "v_and_b32") X3(15, u32, I_OR3, "v_or3_b32")                    \
+  X(16, u32, I_SHR, "v_lshrrev_b32") X(17, u32, I_SUB, "v_sub_u32")                \
+  X(18, u32, I_CND32, "v_cndmask_b32_e32")
+constexpr int kKinds = 19;
 
 template <int KIND, typename T>
 __device__ __forceinline__ void body(T &a0, T &a1, T &a2, T &a3, T &a4, T &a5, T &a6, T &a7,
@@ -59,8 +72,15 @@ __device__ __forceinline__ void body(T &a0, T &a1, T &a2, T &a3, T &a4, T &a5, T
                  "+v"(a7)                                                                      \
                  : "v"(k)                                                                      \
                  : "vcc");
+#define X3(K, TY, I, NAME)                                                                     \
+  if constexpr (KIND == K)                                                                     \
+    asm volatile(OPS3(I) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5),         \
+                 "+v"(a6), "+v"(a7)                                                            \
+                 : "v"(k)                                                                      \
+                 : "vcc");
   KINDS(X)
 #undef X
+#undef X3
 }
 
 template <int KIND, typename T>
@@ -95,8 +115,10 @@ int main() {
     name = NAME;                                                                      \
     hipLaunchKernelGGL((k_valu<K, TY>), dim3(blocks), dim3(256), 0, 0, sink, 3u);     \
     break;
+#define X3 X
         KINDS(X)
 #undef X
+#undef X3
       }
       hipEventRecord(e1);
       hipEventSynchronize(e1);
