@@ -1344,48 +1344,108 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
   const uint64_t ntiles = (a.G + 63) / 64;
   const uint64_t maxu = a.max_unc ? a.max_unc : ~0ull;  // 0 = noLimit
+  const bool app_only = (a.prop_flags & QE_PROP_APPEND_ONLY) != 0;
+  // Loads in three stages per tile, software-pipelined across the wave's
+  // tiles so one round trip per tile is exposed: A (the proposal count,
+  // lastIndex, committed) and B (the masks, self slot, transferee, payload,
+  // conf-change count and uncommitted size of the proposing groups) of tile
+  // t+1 are issued during tile t, before any of tile t's stores (vmcnt
+  // counts loads and stores in one issue order); C (term start, firstIndex,
+  // every slot's Match, Next and word of the groups that pass the MsgProp
+  // gates) at the top of tile t.  Size-dropped proposals (decided after C
+  // is issued) load C rows they do not use; nothing is counted for them.
+  // (1.618 -> 1.602 ms, profiles/r05/propose_pipe_ab.txt: the round trips
+  // are not what bounds it; its ring appends write whole sectors, as the
+  // send kernel's do)
+  struct PA {
+    uint32_t ne;
+    uint64_t li, c0;
+  };
+  struct PBk {
+    uint32_t trk, self, ltr, mi, mo, ncc;
+    uint64_t sz, us;
+  };
+  auto load_a = [&](uint64_t t, PA &x) {
+    const uint32_t n = t < ntiles ? tile_n(a.G, t) : 0u;  // past the end: nothing
+    const uint64_t g0 = t * 64;
+    x.ne = bld32(mk_rsrc(a.prop_n + g0, n * 4), lane * 4);
+    x.li = bld64(mk_rsrc(a.last_index_rw + g0, n * 8), lane * 8);
+    x.c0 = bld64(mk_rsrc(a.committed + g0, n * 8), lane * 8);
+  };
+  auto load_b = [&](uint64_t t, const PA &x, PBk &y) {
+    const uint32_t n = t < ntiles ? tile_n(a.G, t) : 0u;
+    const uint64_t g0 = t * 64;
+    const bool prop = x.ne != 0;
+    const uint32_t o1 = prop ? lane : kOOB;
+    y.trk = a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * MB), lane) & kFull)
+                      : kFull;
+    y.self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), o1) : 0xFFu;
+    y.ltr = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), o1) : 0xFFu;
+    y.mi = MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * MB), lane) & kFull)
+                  : kFull;
+    y.mo = JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * MB), lane) & kFull)
+                 : 0u;
+    y.sz = a.prop_payload ? bld64(mk_rsrc(a.prop_payload + g0, n * 8), prop ? lane * 8 : kOOB) : 0;
+    y.ncc = a.max_cc ? bld8(mk_rsrc(a.cc_count + g0, n), o1) : 0u;
+    y.us = bld64(opt_rsrc(a.unc, g0, n), prop ? lane * 8 : kOOB);
+  };
+  PA ha;
+  PBk hb;
+  load_a(wave, ha);
+  load_b(wave, ha, hb);
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
     const bool live = lane < n;
     const uint32_t o8 = lane * 8, o4 = lane * 4;
-    const uint32_t ne = bld32(mk_rsrc(a.prop_n + g0, n * 4), o4);
+    const uint32_t ne = ha.ne;
     const bool prop = ne != 0;
     // lastIndex and committed of every group (the checksum covers them)
     const rsrc_t r_li = mk_rsrc(a.last_index_rw + g0, n * 8), r_c = mk_rsrc(a.committed + g0, n * 8);
-    uint64_t li = bld64(r_li, o8);
-    const uint64_t c0 = bld64(r_c, o8);
+    uint64_t li = ha.li;
+    const uint64_t c0 = ha.c0;
     uint64_t c = c0;
     ac.add(live, 4);
     uint32_t res = QE_PROP_NONE, refused = 0, sentm = 0, snapm = 0;
+    const uint32_t trk = hb.trk, self = hb.self, ltr = hb.ltr, mi = hb.mi, mo = hb.mo;
+    const bool member = self < static_cast<uint32_t>(S) && ((trk >> self) & 1u) != 0;
+    // (appendEntry alone skips the MsgProp gates but needs the leader's
+    // Progress: the reference's MaybeUpdate on a missing one panics)
+    res = !prop ? QE_PROP_NONE
+                : (!member ? QE_PROP_DROPPED_NOT_MEMBER
+                           : ((!app_only && ltr < static_cast<uint32_t>(S)) ? QE_PROP_DROPPED_TRANSFER
+                                                                            : QE_PROP_OK));
+    const bool go = res == QE_PROP_OK;
+    // stage C of this tile
+    const uint32_t k8 = go ? o8 : kOOB;
+    const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), k8);
+    const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), k8);
+    const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
+    uint64_t mt[S], nx[S];
+    uint32_t pw[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      const bool ld = go && ((trk >> s) & 1u) && (!app_only || self == static_cast<uint32_t>(s));
+      mt[s] = bld64(mk_rsrc(a.match + row, n * 8), k8);
+      nx[s] = bld64(mk_rsrc(a.next + row, n * 8), ld ? o8 : kOOB);
+      pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), ld ? o4 : kOOB);
+    }
+    // this tile's stage-B values the gates below still use (named before the
+    // next tile's loads take the struct)
+    const uint64_t sz_ld = hb.sz, us = hb.us;
+    const uint32_t ncc_ld = hb.ncc;
+    // stages A and B of the wave's next tile, before this tile's stores
+    load_a(t + nwaves, ha);
+    load_b(t + nwaves, ha, hb);
     if (__builtin_amdgcn_ballot_w64(prop)) {
-      const uint32_t trk =
-          a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * MB), lane) & kFull)
-                    : kFull;
-      const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
-      const uint32_t ltr = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), lane) : 0xFFu;
-      const uint32_t mi =
-          MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * MB), lane) & kFull)
-                 : kFull;
-      const uint32_t mo =
-          JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * MB), lane) & kFull)
-                : 0u;
       ac.add(prop, (a.self_slot ? 1 : 0) + (a.tracked ? MB : 0) + (a.transferee ? 1 : 0));
-      const bool member = self < static_cast<uint32_t>(S) && ((trk >> self) & 1u) != 0;
-      // (appendEntry alone skips the MsgProp gates but needs the leader's
-      // Progress: the reference's MaybeUpdate on a missing one panics)
-      const bool app_only = (a.prop_flags & QE_PROP_APPEND_ONLY) != 0;
-      res = !prop ? QE_PROP_NONE
-                  : (!member ? QE_PROP_DROPPED_NOT_MEMBER
-                             : ((!app_only && ltr < static_cast<uint32_t>(S)) ? QE_PROP_DROPPED_TRANSFER
-                                                                              : QE_PROP_OK));
-      const bool go = res == QE_PROP_OK;
-      uint64_t sz = a.prop_payload ? bld64(mk_rsrc(a.prop_payload + g0, n * 8), go ? o8 : kOOB) : 0;
+      uint64_t sz = go ? sz_ld : 0;
       ac.add(go, (a.prop_payload ? 8 : 0) + (a.max_cc ? 1 : 0));
       // conf-change entries (:1034-1072): refused ones become empty
       // EntryNormal entries (no payload), an accepted one sets
       // pendingConfIndex to its index
-      uint32_t ncc = a.max_cc ? bld8(mk_rsrc(a.cc_count + g0, n), go ? lane : kOOB) : 0u;
+      uint32_t ncc = go ? ncc_ld : 0u;
       ncc = ncc < a.max_cc ? ncc : a.max_cc;
       bool out_counted = false;
       if (__builtin_amdgcn_ballot_w64(ncc > 0)) {
@@ -1421,7 +1481,6 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
       }
       // appendEntry -> increaseUncommittedSize (:1761-1779)
       const rsrc_t r_unc = opt_rsrc(a.unc, g0, n);
-      const uint64_t us = bld64(r_unc, go ? o8 : kOOB);
       ac.add(go && a.unc, 8);
       const bool drop = go && us > 0 && sz > 0 && us + sz > maxu;
       res = drop ? QE_PROP_DROPPED_SIZE : res;
@@ -1433,20 +1492,6 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
       ac.add(ok, 16 + 8 + 8 + (app_only ? 0 : 8 + (a.snap_index ? 8 : 0)) + (MASKED ? MB : 0) +
                      ((JOINT && !out_counted) ? MB : 0));
       if (__builtin_amdgcn_ballot_w64(ok)) {
-        const uint32_t k8 = ok ? o8 : kOOB;
-        const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), k8);
-        const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), k8);
-        const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
-        uint64_t mt[S], nx[S];
-        uint32_t pw[S];
-#pragma unroll
-        for (int s = 0; s < S; s++) {
-          const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
-          const bool ld = ok && ((trk >> s) & 1u) && (!app_only || self == static_cast<uint32_t>(s));
-          mt[s] = bld64(mk_rsrc(a.match + row, n * 8), k8);
-          nx[s] = bld64(mk_rsrc(a.next + row, n * 8), ld ? o8 : kOOB);
-          pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), ld ? o4 : kOOB);
-        }
         ac.add(ok, 8 * S + 12);  // every Match; the leader's Next + word
         // Progress[r.id].MaybeUpdate(lastIndex) (progress.go:144-153)
         uint64_t sm = 0, sx = 0;

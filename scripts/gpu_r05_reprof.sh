@@ -4,6 +4,12 @@
 # distinct registers) with its PMC pass.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r05x}; mkdir -p "$O"
+# the pipelined propose kernel: its parity tests and bench line first
+timeout -k 10 600 python -u -m pytest tests/test_gpu_propose.py tests/test_gpu_trace_replay.py tests/test_gpu_progress.py -m gpu -x -q -p no:cacheprovider \
+  --timeout 120 --timeout-method thread > "$O/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$O/tests.log"; exit 5; }
+tail -1 "$O/tests.log"
+timeout -k 10 300 python -u bench.py --workload propose --no-aux --no-cpu-baseline --steps 20 --warmup 5 > "$O/bench_propose.log" 2>&1 || { echo bench failed; tail -20 "$O/bench_propose.log"; exit 6; }
+tail -1 "$O/bench_propose.log" | cut -c1-300
 WLS=${WLS:-"config5_elec config5_prevote_cq progress_send propose progress_step_n7"} bash scripts/gpu_profile_workloads.sh || exit 2
 timeout -k 10 120 ./scripts/valu_probe > "$O/valu_probe.txt" 2>&1 || { echo valu probe failed; cat "$O/valu_probe.txt"; exit 3; }
 cat "$O/valu_probe.txt"
