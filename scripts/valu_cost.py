@@ -44,7 +44,9 @@ PROBE_KINDS = {  # k_valu<KIND, T> -> opcode prefix it issues
     4: "v_bcnt_u32_b32", 5: "v_bitop3_b32", 6: "v_cndmask_b32", 7: "v_mul_lo_u16",
     8: "v_add3_u32", 9: "v_mad_u64_u32", 10: "v_lshl_add_u64", 11: "v_lshrrev_b64",
     12: "v_mov_b32", 13: "v_cmp_gt_u32", 14: "v_and_b32", 15: "v_or3_b32", 16: "v_lshrrev_b32",
-    17: "v_sub_u32", 18: "v_cndmask_b32_e32"}
+    17: "v_sub_u32", 18: "v_cndmask_b32_e32", 19: "v_readlane_b32", 20: "v_writelane_b32",
+    21: "v_min_u32", 22: "v_max_u32", 23: "v_lshlrev_b32", 24: "v_alignbit_b32",
+    25: "v_and_or_b32"}
 # opcodes priced as a probed one of the same form: every 32-bit compare
 # writes a lane mask as v_cmp_gt_u32 does
 ALIASES = (("v_cmp_", "v_cmp_gt_u32"),)

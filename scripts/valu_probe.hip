@@ -47,6 +47,13 @@ constexpr int kPerIter = 32;
 #define I_SHR(i) "v_lshrrev_b32 %" #i ", 1, %" #i "\n"
 #define I_SUB(i) "v_sub_u32 %" #i ", %" #i ", %8\n"
 #define I_CND32(i) "v_cndmask_b32_e32 %" #i ", %" #i ", %8, vcc\n"
+#define I_MIN(i) "v_min_u32 %" #i ", %" #i ", %8\n"
+#define I_MAX(i) "v_max_u32 %" #i ", %" #i ", %8\n"
+#define I_SHL(i) "v_lshlrev_b32 %" #i ", 1, %" #i "\n"
+#define I_ALIGN(i, j) "v_alignbit_b32 %" #i ", %" #i ", %" #j ", 3\n"
+#define I_ANDOR(i, j) "v_and_or_b32 %" #i ", %" #i ", %8, %" #j "\n"
+#define I_RDL(i) "v_readlane_b32 s" #i "6, %" #i ", 5\n"    // SGPR spill reload shape
+#define I_WRL(i) "v_writelane_b32 %" #i ", s" #i "6, 7\n"   // SGPR spill store shape
 #define OPS(T) R8(T) R8(T) R8(T) R8(T)  // 32 instructions, 8 independent chains of 4
 #define OPS3(T) R8P(T) R8P(T) R8P(T) R8P(T)
 
@@ -60,8 +67,12 @@ constexpr int kPerIter = 32;
   X(12, u32, I_MOV, "v_mov_b32") X(13, u32, I_CMP, "v_cmp_gt_u32")                 \
   X(14, u32, I_AND, "v_and_b32") X3(15, u32, I_OR3, "v_or3_b32")                    \
   X(16, u32, I_SHR, "v_lshrrev_b32") X(17, u32, I_SUB, "v_sub_u32")                \
-  X(18, u32, I_CND32, "v_cndmask_b32_e32")
-constexpr int kKinds = 19;
+  X(18, u32, I_CND32, "v_cndmask_b32_e32")                                        \
+  XS(19, u32, I_RDL, "v_readlane_b32") XS(20, u32, I_WRL, "v_writelane_b32")        \
+  X(21, u32, I_MIN, "v_min_u32") X(22, u32, I_MAX, "v_max_u32")                    \
+  X(23, u32, I_SHL, "v_lshlrev_b32") X3(24, u32, I_ALIGN, "v_alignbit_b32")        \
+  X3(25, u32, I_ANDOR, "v_and_or_b32")
+constexpr int kKinds = 26;
 
 template <int KIND, typename T>
 __device__ __forceinline__ void body(T &a0, T &a1, T &a2, T &a3, T &a4, T &a5, T &a6, T &a7,
@@ -78,9 +89,16 @@ __device__ __forceinline__ void body(T &a0, T &a1, T &a2, T &a3, T &a4, T &a5, T
                  "+v"(a6), "+v"(a7)                                                            \
                  : "v"(k)                                                                      \
                  : "vcc");
+#define XS(K, TY, I, NAME)                                                                     \
+  if constexpr (KIND == K)                                                                     \
+    asm volatile(OPS(I) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), \
+                 "+v"(a7)                                                                      \
+                 : "v"(k)                                                                      \
+                 : "s6", "s16", "s26", "s36", "s46", "s56", "s66", "s76");
   KINDS(X)
 #undef X
 #undef X3
+#undef XS
 }
 
 template <int KIND, typename T>
@@ -116,9 +134,11 @@ int main() {
     hipLaunchKernelGGL((k_valu<K, TY>), dim3(blocks), dim3(256), 0, 0, sink, 3u);     \
     break;
 #define X3 X
+#define XS X
         KINDS(X)
 #undef X
 #undef X3
+#undef XS
       }
       hipEventRecord(e1);
       hipEventSynchronize(e1);
