@@ -578,8 +578,44 @@ struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's tur
 // A wave-level branch skips each group of loads no lane needs (an issued
 // vector memory instruction costs the CU's memory path about the same
 // whether or not its lanes are masked off).
+// The arguments the slot loop reads (a PArgs subset with the same names).
+struct SlotArgs {
+  uint64_t stride;
+  uint32_t F, FP;
+  uint64_t *match, *next, *pending;
+  uint32_t *pw, *ilo, *ihi;
+  const uint64_t *mhint, *mlogterm;
+  const uint32_t *read_ctx;
+  uint8_t *msg_count;
+  uint64_t *msg_index;
+};
+
+// The pipelined loop reads the slot's arguments again from the kernarg
+// segment in every slot (scalar loads behind an opaque copy of the segment
+// pointer, so they are not hoisted): the kernel's ~40 argument pointers and
+// the per-slot descriptors exceed the 102 SGPRs, and hipcc otherwise keeps
+// the arguments in VGPR lanes and reloads them with v_readlane (VALU, half
+// rate) -- 1173 of them in the S = 5 code object, 751 with the reloads.
+// joint 5+5 over 6 slots 3.57 -> 3.33 ms, S = 7 4.13 -> 4.08, S = 5 equal
+// (profiles/r05/pstep_karg_ab.txt).  The rolled loop keeps the arguments
+// (re-reading them there was 12 % slower in round 4).
 template <bool P>
-__device__ __forceinline__ void pb_load(const PArgs &a, uint64_t row, const uint64_t *l_mix,
+__device__ __forceinline__ SlotArgs slot_args(const PArgs &a) {
+  if constexpr (P) {
+    typedef const PArgs __attribute__((address_space(4))) KA;
+    KA *ka = (KA *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    return SlotArgs{ka->stride, ka->F, ka->FP, ka->match, ka->next, ka->pending, ka->pw,
+                    ka->ilo, ka->ihi, ka->mhint, ka->mlogterm, ka->read_ctx, ka->msg_count,
+                    ka->msg_index};
+  } else {
+    return SlotArgs{a.stride, a.F, a.FP, a.match, a.next, a.pending, a.pw, a.ilo, a.ihi,
+                    a.mhint, a.mlogterm, a.read_ctx, a.msg_count, a.msg_index};
+  }
+}
+
+template <bool P, class A>
+__device__ __forceinline__ void pb_load(const A &a, uint64_t row, const uint64_t *l_mix,
                                         uint32_t n, uint32_t lane, bool ld, bool rej,
                                         bool has_ix, bool rcl, PB &b) {
   b.mt = l_mix[lane];
@@ -865,13 +901,14 @@ k_progress_step(PArgs a) {
     constexpr int kSlotUnroll = P ? S : 1;
 #pragma unroll kSlotUnroll
     for (uint32_t s = 0; s < static_cast<uint32_t>(S); s++) {
-      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      const SlotArgs sa = slot_args<P>(a);
+      const uint64_t row = static_cast<uint64_t>(s) * sa.stride + g0;
       const uint32_t tt = ty_of(s);
       const bool touched = ((tchm >> s) & 1u) != 0;
       PB nxt{};  // (the last slot has no next: zeros)
       if constexpr (PF2) {
         if (s + 2 < static_cast<uint32_t>(S)) {
-          pb_load<P>(a, row + 2 * a.stride, &l_mix[wv][s + 2][0][0], n, lane,
+          pb_load<P>(sa, row + 2 * sa.stride, &l_mix[wv][s + 2][0][0], n, lane,
                      ((tchm >> (s + 2)) & 1u) != 0, ((rejm >> (s + 2)) & 1u) != 0,
                      ((ixm >> (s + 2)) & 1u) != 0, ((rcm >> (s + 2)) & 1u) != 0, nxt);
         }
@@ -879,7 +916,7 @@ k_progress_step(PArgs a) {
         cur.mt = l_mix[wv][s][0][lane];
         cur.ix = ((ixm >> s) & 1u) ? l_mix[wv][s][1][lane] : 0;
       } else if (s + 1 < static_cast<uint32_t>(S)) {
-        pb_load<P>(a, row + a.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
+        pb_load<P>(sa, row + sa.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
                 ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
                 ((rcm >> (s + 1)) & 1u) != 0, nxt);
       }
@@ -887,8 +924,8 @@ k_progress_step(PArgs a) {
         // no event for this slot in any group of the tile (e.g. the leader's
         // own slot): only the per-peer output
         pb_ready<P>(nxt);
-        if (a.msg_count) bst8(0u, mk_rsrc(a.msg_count + row, n), lane);
-        ac.add(live && a.msg_count, 1);
+        if (sa.msg_count) bst8(0u, mk_rsrc(sa.msg_count + row, n), lane);
+        ac.add(live && sa.msg_count, 1);
         if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
         continue;
       }
@@ -906,15 +943,15 @@ k_progress_step(PArgs a) {
       const bool need_pd = touched && p.state == QE_PR_SNAPSHOT;
       uint64_t pd0 = 0;
       if (__builtin_amdgcn_ballot_w64(need_pd)) {
-        pd0 = bld64(mk_rsrc(a.pending + row, n * 8), need_pd ? o8 : kOOB);
+        pd0 = bld64(mk_rsrc(sa.pending + row, n * 8), need_pd ? o8 : kOOB);
         if constexpr (P) asm volatile("" ::"v"(pd0));  // (rare path's wait)
         ac.add(need_pd, 8);
       }
       p.pending = pd0;
       {
-        const uint64_t rb = (static_cast<uint64_t>(s) * a.stride + g0) * a.FP;
-        x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
-        x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+        const uint64_t rb = (static_cast<uint64_t>(s) * sa.stride + g0) * sa.FP;
+        x.rlo = mk_rsrc(sa.ilo + rb, n * sa.FP * 4);
+        x.rhi = mk_rsrc(sa.ihi + rb, n * sa.FP * 4);
       }
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
@@ -925,7 +962,7 @@ k_progress_step(PArgs a) {
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
       if (row_ring) {
-        ring_load_row<P>(x, touched && c_old > 0, rep0, a.FP, rlo, rhi, P ? cur.rl : nullptr);
+        ring_load_row<P>(x, touched && c_old > 0, rep0, sa.FP, rlo, rhi, P ? cur.rl : nullptr);
       } else {
 #pragma unroll
         for (int k = 0; k < CH; k++) rlo[k] = rhi[k] = 0;
@@ -1034,7 +1071,7 @@ k_progress_step(PArgs a) {
           // nothing recorded); once its acks win the vote, readOnly.advance
           // dequeues every request through it (read_only.go:81-112)
           if (rd) {
-            const uint32_t cx = a.read_ctx ? cur.rc : dctx;
+            const uint32_t cx = sa.read_ctx ? cur.rc : dctx;
             const uint32_t j = cx - qh;
             if (cx != 0 && j < qn) {
               q |= static_cast<QT>(1u << s) << (EW * j);
@@ -1079,7 +1116,7 @@ k_progress_step(PArgs a) {
       const uint32_t km = lp ? kLoop : k2 + k3;
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      if (row_ring) ring_store_row<P>(p, x, r1, r2, touched, rep0, c_old, a.FP, rlo, rhi);
+      if (row_ring) ring_store_row<P>(p, x, r1, r2, touched, rep0, c_old, sa.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
       const bool tw = touched;
@@ -1093,27 +1130,27 @@ k_progress_step(PArgs a) {
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
       constexpr bool PIPE = P;  // a fixed store count per slot
       if (PIPE || __builtin_amdgcn_ballot_w64(wm))
-        bst64(p.match, mk_rsrc(a.match + row, n * 8), fm ? o8 : kOOB);
+        bst64(p.match, mk_rsrc(sa.match + row, n * 8), fm ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(wn))
-        bst64(p.next, mk_rsrc(a.next + row, n * 8), fn ? o8 : kOOB);
+        bst64(p.next, mk_rsrc(sa.next + row, n * 8), fn ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(wp))
-        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
+        bst64(p.pending, mk_rsrc(sa.pending + row, n * 8), wp ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(ww))
-        bst32(nw, mk_rsrc(a.pw + row, n * 4), fw ? lane * 4 : kOOB);
+        bst32(nw, mk_rsrc(sa.pw + row, n * 4), fw ? lane * 4 : kOOB);
       if (PIPE) {  // optional outputs through a descriptor with no records when NULL
-        bst8(x.count_msgs, opt_rsrc(a.msg_count, row, n), lane);
-        bst64(x.first_index, opt_rsrc(a.msg_index, row, n), x.count_msgs ? o8 : kOOB);
+        bst8(x.count_msgs, opt_rsrc(sa.msg_count, row, n), lane);
+        bst64(x.first_index, opt_rsrc(sa.msg_index, row, n), x.count_msgs ? o8 : kOOB);
       } else {
-        if (a.msg_count) bst8(x.count_msgs, mk_rsrc(a.msg_count + row, n), lane);  // optional outputs
-        if (a.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
-          bst64(x.first_index, mk_rsrc(a.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
+        if (sa.msg_count) bst8(x.count_msgs, mk_rsrc(sa.msg_count + row, n), lane);  // optional outputs
+        if (sa.msg_index && __builtin_amdgcn_ballot_w64(x.count_msgs != 0))
+          bst64(x.first_index, mk_rsrc(sa.msg_index + row, n * 8), x.count_msgs ? o8 : kOOB);
       }
       ac.add(wm, 8);
       ac.add(wn, 8);
       ac.add(wp, 8);
       ac.add(wc, 4);
-      ac.add(live && a.msg_count, 1);
-      ac.add(x.count_msgs && a.msg_index, 8);
+      ac.add(live && sa.msg_count, 1);
+      ac.add(x.count_msgs && sa.msg_index, 8);
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
       if (s + 1 < static_cast<uint32_t>(S)) {
