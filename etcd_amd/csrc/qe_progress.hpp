@@ -490,11 +490,14 @@ __device__ __forceinline__ void free_le(PR &p, uint64_t to, uint32_t c_old, uint
 __device__ __forceinline__ uint32_t row_prefix_le(const uint32_t (&lo)[kRingChunk],
                                                   const uint32_t (&hi)[kRingChunk], uint32_t F,
                                                   uint32_t start, uint32_t c_old, uint64_t to) {
+  // every position compared, the ones past F masked off after (a per-k
+  // "k < F" test in the loop is a wave-uniform lane mask per k that hipcc
+  // keeps in SGPR pairs -- spilled, and reloaded with v_readlane)
   uint32_t pm = 0;
 #pragma unroll
-  for (int k = 0; k < kRingChunk; k++)
-    pm |= (static_cast<uint32_t>(k) < F && ent64(hi[k], lo[k]) <= to) ? (1u << k) : 0u;
+  for (int k = 0; k < kRingChunk; k++) pm |= ent64(hi[k], lo[k]) <= to ? (1u << k) : 0u;
   const uint32_t full = (1u << F) - 1u;
+  pm &= full;
   const uint32_t st = start < F ? start : 0u;
   const uint32_t rk = ((pm >> st) | (pm << (F - st))) & full;  // bit k: entry of rank k
   const uint32_t run = __builtin_ctz(~rk);                     // <= F
@@ -1121,7 +1124,12 @@ k_progress_step(PArgs a) {
       const uint32_t nw = pr_pack(p);
       const bool tw = touched;
       const bool wm = tw && up, wn = tw && p.next != cur.nx;
-      const bool wp = tw && (p.pending != pd0 || p.reset);
+      // PendingSnapshot is 0 outside StateSnapshot in every reachable state
+      // (ResetState clears it on each state change, progress.go:119-126, and
+      // only BecomeSnapshot sets it; the ABI requires it of the input): it is
+      // written only where its value changes -- a rare path, so the store
+      // stays behind its ballot in both loop forms
+      const bool wp = tw && p.pending != pd0;
       const bool ww = tw && nw != cur.w;
       // (storing a changed row for every touched lane, whole sectors, made
       // no difference here: profiles/r03/cq_fullrow_ab.txt)
@@ -1133,7 +1141,7 @@ k_progress_step(PArgs a) {
         bst64(p.match, mk_rsrc(sa.match + row, n * 8), fm ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(wn))
         bst64(p.next, mk_rsrc(sa.next + row, n * 8), fn ? o8 : kOOB);
-      if (PIPE || __builtin_amdgcn_ballot_w64(wp))
+      if (__builtin_amdgcn_ballot_w64(wp))
         bst64(p.pending, mk_rsrc(sa.pending + row, n * 8), wp ? o8 : kOOB);
       if (PIPE || __builtin_amdgcn_ballot_w64(ww))
         bst32(nw, mk_rsrc(sa.pw + row, n * 4), fw ? lane * 4 : kOOB);

@@ -355,7 +355,11 @@ typedef struct qe_progress {
   uint32_t inflight_cap;        /* F = MaxInflightMsgs, 1..QE_MAX_INFLIGHT  */
   uint64_t stride;
   uint64_t *match, *next;       /* [S][stride]                               */
-  uint64_t *pending_snapshot;   /* [S][stride]                               */
+  uint64_t *pending_snapshot;   /* [S][stride]; 0 for a peer not in
+                                 * StateSnapshot (every reachable Progress:
+                                 * ResetState clears it on each state change,
+                                 * tracker/progress.go:119-126) -- the kernels
+                                 * write it only where its value changes      */
   uint32_t *peer;               /* [S][stride] packed per-peer word (ABI 3):
                                    StateType, ProbeSent, RecentActive,
                                    Inflights.start / count (QE_PW_*)         */

@@ -1412,7 +1412,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
             B += state0[s] == PR_SNAPSHOT ? 8 : 0;            /* PendingSnapshot         */
             B += p->match != match0[s] ? 8 : 0;
             B += p->next != next0[s] ? 8 : 0;
-            B += (p->reset || (state0[s] == PR_SNAPSHOT && p->pending != pend0[s])) ? 8 : 0;
+            B += p->pending != pend0[s] ? 8 : 0;              /* (0 outside StateSnapshot) */
             B += pr_word(p) != word0[s] ? 4 : 0;
           }
           B += m->msg_count ? 1 : 0;

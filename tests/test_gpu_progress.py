@@ -58,10 +58,12 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0, base=0):
     fi = np.tile(pb.first_index, S)
     low = rng.random(n) < 0.08  # compacted: Next < firstIndex (snapshot path)
     pb.next[low] = (rng.random(int(low.sum())) * fi[low]).astype(np.uint64)
-    pb.pending[:] = rng.integers(0, 70, n).astype(np.uint64)
-    pb.set_peer(flags=(rng.integers(0, 3, n) | (rng.integers(0, 2, n) * 4) |
-                       (rng.integers(0, 2, n) * 8)).astype(np.uint8),
-                istart=rng.integers(0, F, n).astype(np.uint8),
+    flags = (rng.integers(0, 3, n) | (rng.integers(0, 2, n) * 4) |
+             (rng.integers(0, 2, n) * 8)).astype(np.uint8)
+    # PendingSnapshot only in StateSnapshot (reachable states; the ABI's
+    # precondition: ResetState clears it on every state change)
+    pb.pending[:] = np.where((flags & 3) == 2, rng.integers(0, 70, n), 0).astype(np.uint64)
+    pb.set_peer(flags=flags, istart=rng.integers(0, F, n).astype(np.uint8),
                 icount=rng.integers(0, F + 1, n).astype(np.uint8))
     m0 = pb.match.copy()
     for k in range(F):  # entry-major rings: entry k of slot s at (s*F + k)*stride + g
@@ -85,9 +87,11 @@ def random_state(rng, G, S, F, R, masks, extras=(), max_ents=0, base=0):
         pb.snap_index = (pb.first_index - 1 + rng.integers(0, 3, G)).astype(np.uint64)
     if base:
         b = np.uint64(base)
-        for k in ("match", "next", "pending", "ibuf", "committed", "term_start", "first_index",
+        for k in ("match", "next", "ibuf", "committed", "term_start", "first_index",
                   "last_index", "run_first"):
             setattr(pb, k, (getattr(pb, k) + b).astype(np.uint64))
+        # (a StateSnapshot peer's PendingSnapshot shifts; every other stays 0)
+        pb.pending = np.where(pb.pending != 0, pb.pending + b, pb.pending).astype(np.uint64)
         if pb.snap_index is not None:
             pb.snap_index = (pb.snap_index + b).astype(np.uint64)
     return pb
@@ -349,6 +353,7 @@ def test_progress_long_rings_and_bcasts(eng):
     pb = random_state(rng, G, S, F, R, (), EXTRAS, max_ents=1)
     pb.term_start[:] = 0
     pb.set_peer(flags=1 | 8)  # Replicate, RecentActive
+    pb.pending[:] = 0  # (no StateSnapshot peer: PendingSnapshot 0)
     ps = to_device(eng, pb, (), EXTRAS)
     for _ in range(4):
         n = S * G
