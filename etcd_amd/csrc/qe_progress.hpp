@@ -1125,7 +1125,7 @@ k_progress_step(PArgs a) {
       const bool tw = touched;
       const bool wm = tw && up, wn = tw && p.next != cur.nx;
       // PendingSnapshot is 0 outside StateSnapshot in every reachable state
-      // (ResetState clears it on each state change, progress.go:119-126, and
+      // (ResetState clears it on each state change, progress.go:84-89, and
       // only BecomeSnapshot sets it; the ABI requires it of the input): it is
       // written only where its value changes -- a rare path, so the store
       // stays behind its ballot in both loop forms

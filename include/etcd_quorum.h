@@ -358,7 +358,7 @@ typedef struct qe_progress {
   uint64_t *pending_snapshot;   /* [S][stride]; 0 for a peer not in
                                  * StateSnapshot (every reachable Progress:
                                  * ResetState clears it on each state change,
-                                 * tracker/progress.go:119-126) -- the kernels
+                                 * tracker/progress.go:84-89) -- the kernels
                                  * write it only where its value changes      */
   uint32_t *peer;               /* [S][stride] packed per-peer word (ABI 3):
                                    StateType, ProbeSent, RecentActive,
