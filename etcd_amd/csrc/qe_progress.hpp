@@ -850,15 +850,37 @@ k_progress_step(PArgs a) {
     // spills (16-120 B of scratch at the 168-VGPR budget), so S = 7 only
     constexpr bool PF2 = P && S == 7;
     PB nx1{};  // PF2: slot s+1's loads while slot s runs
-    {  // slot 0, before phase 1: every possible event
-      const bool ld = ((trk & (msgm | (self != 0u ? 1u : 0u))) & 1u) != 0;
-      pb_load<P>(a, g0, &l_mix[wv][0][0][0], n, lane, ld, (rejm & 1u) != 0, (ixm & 1u) != 0,
-              (rcm & 1u) != 0, cur);
+    // SKIP: the pipelined loop walks S - 1 slots when one slot is untouched
+    // in every group of the tile whatever phase 1 decides (no tracked
+    // peer's message, not a bcast target: untracked or the leader's own) --
+    // its only output is MsgCount = 0.  The walked slots keep slot order.
+    // (the leader's slot in a steady round: profiles/r05/pstep_skip_ab.txt,
+    // S = 5 2.54 -> 2.49 ms, S = 7 3.64 -> 3.62, joint 3.22 -> 3.17)
+    constexpr bool SKIP = P && S >= 2;
+    uint32_t skip = S;  // wave-uniform: the slot not walked (S: none)
+    if constexpr (SKIP) {
+      uint32_t um = 0;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const bool may = live && ((((trk & msgm) >> s) & 1u) != 0 ||
+                                  (((trk >> s) & 1u) != 0 && self != static_cast<uint32_t>(s)));
+        um |= __builtin_amdgcn_ballot_w64(may) ? 0u : (1u << s);
+      }
+      skip = um ? static_cast<uint32_t>(__builtin_ctz(um)) : static_cast<uint32_t>(S);
     }
-    if constexpr (PF2 && S > 1) {  // and slot 1
-      const bool ld = ((trk & (msgm | (self != 1u ? 2u : 0u))) & 2u) != 0;
-      pb_load<P>(a, g0 + a.stride, &l_mix[wv][1][0][0], n, lane, ld, (rejm & 2u) != 0,
-                 (ixm & 2u) != 0, (rcm & 2u) != 0, nx1);
+    // the walked slot after slot s (S and above: none)
+    auto after = [&](uint32_t s) -> uint32_t { return s + 1 + (s + 1 == skip ? 1u : 0u); };
+    const uint32_t p0 = skip == 0 ? 1u : 0u;
+    {  // the first walked slot, before phase 1: every possible event
+      const bool ld = (((trk & (msgm | (self != p0 ? (1u << p0) : 0u))) >> p0) & 1u) != 0;
+      pb_load<P>(a, static_cast<uint64_t>(p0) * a.stride + g0, &l_mix[wv][p0][0][0], n, lane, ld,
+                 ((rejm >> p0) & 1u) != 0, ((ixm >> p0) & 1u) != 0, ((rcm >> p0) & 1u) != 0, cur);
+    }
+    if constexpr (PF2 && S > 2) {  // and the second
+      const uint32_t p1 = after(p0);
+      const bool ld = (((trk & (msgm | (self != p1 ? (1u << p1) : 0u))) >> p1) & 1u) != 0;
+      pb_load<P>(a, static_cast<uint64_t>(p1) * a.stride + g0, &l_mix[wv][p1][0][0], n, lane, ld,
+                 ((rejm >> p1) & 1u) != 0, ((ixm >> p1) & 1u) != 0, ((rcm >> p1) & 1u) != 0, nx1);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
     uint64_t c = c0;
@@ -901,27 +923,36 @@ k_progress_step(PArgs a) {
     const uint32_t ringm = tchm & ((appm & upd) | hbm);
     // rolled over the slots (one copy of the per-peer code; the next slot's
     // loads are issued before this slot's work)
+    if constexpr (SKIP) {
+      if (skip < static_cast<uint32_t>(S)) {
+        const SlotArgs sa = slot_args<P>(a);
+        bst8(0u, opt_rsrc(sa.msg_count, static_cast<uint64_t>(skip) * sa.stride + g0, n), lane);
+      }
+    }
     constexpr int kSlotUnroll = P ? S : 1;
 #pragma unroll kSlotUnroll
     for (uint32_t s = 0; s < static_cast<uint32_t>(S); s++) {
+      if (SKIP && s == skip) continue;  // (wave-uniform)
+      const uint32_t s1 = SKIP ? after(s) : s + 1;  // the next walked slots
+      const uint32_t s2 = SKIP ? after(s1) : s + 2;
       const SlotArgs sa = slot_args<P>(a);
       const uint64_t row = static_cast<uint64_t>(s) * sa.stride + g0;
       const uint32_t tt = ty_of(s);
       const bool touched = ((tchm >> s) & 1u) != 0;
       PB nxt{};  // (the last slot has no next: zeros)
       if constexpr (PF2) {
-        if (s + 2 < static_cast<uint32_t>(S)) {
-          pb_load<P>(sa, row + 2 * sa.stride, &l_mix[wv][s + 2][0][0], n, lane,
-                     ((tchm >> (s + 2)) & 1u) != 0, ((rejm >> (s + 2)) & 1u) != 0,
-                     ((ixm >> (s + 2)) & 1u) != 0, ((rcm >> (s + 2)) & 1u) != 0, nxt);
+        if (s2 < static_cast<uint32_t>(S)) {
+          pb_load<P>(sa, static_cast<uint64_t>(s2) * sa.stride + g0, &l_mix[wv][s2][0][0], n, lane,
+                     ((tchm >> s2) & 1u) != 0, ((rejm >> s2) & 1u) != 0, ((ixm >> s2) & 1u) != 0,
+                     ((rcm >> s2) & 1u) != 0, nxt);
         }
         // Match / m.Index from the wave's LDS rows at use (not held two slots)
         cur.mt = l_mix[wv][s][0][lane];
         cur.ix = ((ixm >> s) & 1u) ? l_mix[wv][s][1][lane] : 0;
-      } else if (s + 1 < static_cast<uint32_t>(S)) {
-        pb_load<P>(sa, row + sa.stride, &l_mix[wv][s + 1][0][0], n, lane, ((tchm >> (s + 1)) & 1u) != 0,
-                ((rejm >> (s + 1)) & 1u) != 0, ((ixm >> (s + 1)) & 1u) != 0,
-                ((rcm >> (s + 1)) & 1u) != 0, nxt);
+      } else if (s1 < static_cast<uint32_t>(S)) {
+        pb_load<P>(sa, static_cast<uint64_t>(s1) * sa.stride + g0, &l_mix[wv][s1][0][0], n, lane,
+                   ((tchm >> s1) & 1u) != 0, ((rejm >> s1) & 1u) != 0, ((ixm >> s1) & 1u) != 0,
+                   ((rcm >> s1) & 1u) != 0, nxt);
       }
       if (!P && !__builtin_amdgcn_ballot_w64(touched)) {
         // no event for this slot in any group of the tile (e.g. the leader's
@@ -929,7 +960,7 @@ k_progress_step(PArgs a) {
         pb_ready<P>(nxt);
         if (sa.msg_count) bst8(0u, mk_rsrc(sa.msg_count + row, n), lane);
         ac.add(live && sa.msg_count, 1);
-        if (s + 1 < static_cast<uint32_t>(S)) cur = nxt;
+        if (s1 < static_cast<uint32_t>(S)) cur = nxt;
         continue;
       }
       ac.add(touched, 12);  // Next + the packed word
@@ -1161,7 +1192,7 @@ k_progress_step(PArgs a) {
       ac.add(x.count_msgs && sa.msg_index, 8);
       sent |= x.count_msgs ? (1u << s) : 0u;
       snapm |= x.snapped ? (1u << s) : 0u;
-      if (s + 1 < static_cast<uint32_t>(S)) {
+      if (s1 < static_cast<uint32_t>(S)) {  // a walked slot follows
         if constexpr (PF2) {
           cur = nx1;
           nx1 = nxt;

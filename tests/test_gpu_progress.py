@@ -287,6 +287,56 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
             assert_same(ps, pb)
 
 
+@pytest.mark.parametrize("F", [3, 8])
+@pytest.mark.parametrize("S,masks", [(3, ()), (5, ()), (5, ("inc",)), (6, ("inc", "out")),
+                                     (7, ("inc",)), (9, ())])
+def test_progress_quiet_slot_tiles(eng, S, masks, F):
+    """Tiles (64 groups) in which one slot is quiet in every group -- no
+    message, and the leader's own slot or an untracked one -- as the
+    leader's slot is in a steady round: the pipelined loop (rings in row
+    form, up to 9 slots) walks the other slots only and writes MsgCount = 0
+    for that one.  Tile t's quiet slot is t % (S + 1) (S: none); in every
+    fourth tile one group breaks it (a message from a tracked follower in
+    that slot: every slot walked), and the last tile is partial."""
+    rng = np.random.default_rng(700 + 13 * S + F + len(masks))
+    G = 64 * 23 + 17
+    pb = random_state(rng, G, S, F, 3, masks, EXTRAS)
+    random_queue(rng, pb)
+    tile = np.arange(G) // 64
+    q = tile % (S + 1)
+    quiet = q < S
+    own = quiet & (rng.random(G) < 0.6)  # the leader's slot; otherwise untracked
+    pb.self_slot[own] = q[own]
+    md = orc.mask_dtype(S)
+    unt = quiet & ~own
+    pb.tracked[unt] &= np.array(~(1 << q[unt]) & ((1 << S) - 1)).astype(md)
+    pb.self_slot[unt & (pb.self_slot == q)] = 0xFF
+    brk = np.zeros(G, bool)
+    for t in range(0, tile[-1] + 1, 4):  # one group per fourth tile breaks the quiet slot
+        g = t * 64 + int(rng.integers(0, min(64, G - t * 64)))
+        if quiet[g]:
+            brk[g] = True
+            pb.tracked[g] |= np.array(1 << q[g]).astype(md)
+            pb.self_slot[g] = (q[g] + 1) % S
+    ps = to_device(eng, pb, masks, EXTRAS + ("reads",))
+    gq = np.flatnonzero(quiet)
+    for rnd in range(4):
+        mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
+        mt = mtype.reshape(S, G)
+        mt[q[gq], gq] = 0
+        b = np.flatnonzero(brk)
+        mt[q[b], b] = rng.choice([1, 2, 3], b.size)  # (accept / reject / heartbeat response)
+        msgs = load_msgs(eng, ps, mtype, mindex, mhint, mlogterm)
+        ctx = random_read_ctx(rng, pb)
+        msgs.set_read_ctx(ps, ctx)
+        eng.progress_step(ps, msgs, eng.stats_buffer(DEV))
+        o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, read_ctx=ctx)
+        assert_same(ps, pb)
+        assert_outputs(msgs, o, S)
+        gk = np.flatnonzero(quiet & ~brk)
+        assert not msgs.msg_count.cpu().numpy().reshape(S, -1)[q[gk], gk].any()
+
+
 @pytest.mark.parametrize("F", [3, 5, 8, 32])
 @pytest.mark.parametrize("base", [(1 << 32) - 37, (1 << 43) - 29, 3 * (1 << 44) + 11])
 def test_progress_rings_across_epochs(eng, base, F):
