@@ -578,9 +578,10 @@ struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's tur
 // touches), RejectHint/LogTerm of a reject and the context number of a
 // heartbeat response (`rcl`).  The byte accounting is done
 // by the caller, on the lanes the round actually touches.
-// A wave-level branch skips each group of loads no lane needs (an issued
-// vector memory instruction costs the CU's memory path about the same
-// whether or not its lanes are masked off).
+// The rolled loop skips each group of loads no lane needs with a wave-level
+// branch; the pipelined one issues them all (fixed wait counts), and a
+// fully dropped load costs nothing measurable there
+// (profiles/r05/pstep_rc_ab.txt).
 // The arguments the slot loop reads (a PArgs subset with the same names).
 struct SlotArgs {
   uint64_t stride;
@@ -617,7 +618,7 @@ __device__ __forceinline__ SlotArgs slot_args(const PArgs &a) {
   }
 }
 
-template <bool P, class A>
+template <bool P, bool RD, class A>
 __device__ __forceinline__ void pb_load(const A &a, uint64_t row, const uint64_t *l_mix,
                                         uint32_t n, uint32_t lane, bool ld, bool rej,
                                         bool has_ix, bool rcl, PB &b) {
@@ -635,7 +636,11 @@ __device__ __forceinline__ void pb_load(const A &a, uint64_t row, const uint64_t
     b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
-    b.rc = bld32(opt_rsrc(a.read_ctx, row, n), rcl ? lane * 4 : kOOB);
+    // (the heartbeat contexts: only in the variant that tracks ReadIndex;
+    // the always-issued, fully dropped load it replaces cost nothing
+    // measurable, profiles/r05/pstep_rc_ab.txt)
+    if constexpr (RD) b.rc = bld32(opt_rsrc(a.read_ctx, row, n), rcl ? lane * 4 : kOOB);
+    else b.rc = 0;
     return;
   }
   if (__builtin_amdgcn_ballot_w64(ld)) {
@@ -873,13 +878,13 @@ k_progress_step(PArgs a) {
     const uint32_t p0 = skip == 0 ? 1u : 0u;
     {  // the first walked slot, before phase 1: every possible event
       const bool ld = (((trk & (msgm | (self != p0 ? (1u << p0) : 0u))) >> p0) & 1u) != 0;
-      pb_load<P>(a, static_cast<uint64_t>(p0) * a.stride + g0, &l_mix[wv][p0][0][0], n, lane, ld,
+      pb_load<P, RD>(a, static_cast<uint64_t>(p0) * a.stride + g0, &l_mix[wv][p0][0][0], n, lane, ld,
                  ((rejm >> p0) & 1u) != 0, ((ixm >> p0) & 1u) != 0, ((rcm >> p0) & 1u) != 0, cur);
     }
     if constexpr (PF2 && S > 2) {  // and the second
       const uint32_t p1 = after(p0);
       const bool ld = (((trk & (msgm | (self != p1 ? (1u << p1) : 0u))) >> p1) & 1u) != 0;
-      pb_load<P>(a, static_cast<uint64_t>(p1) * a.stride + g0, &l_mix[wv][p1][0][0], n, lane, ld,
+      pb_load<P, RD>(a, static_cast<uint64_t>(p1) * a.stride + g0, &l_mix[wv][p1][0][0], n, lane, ld,
                  ((rejm >> p1) & 1u) != 0, ((ixm >> p1) & 1u) != 0, ((rcm >> p1) & 1u) != 0, nx1);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
@@ -942,7 +947,7 @@ k_progress_step(PArgs a) {
       PB nxt{};  // (the last slot has no next: zeros)
       if constexpr (PF2) {
         if (s2 < static_cast<uint32_t>(S)) {
-          pb_load<P>(sa, static_cast<uint64_t>(s2) * sa.stride + g0, &l_mix[wv][s2][0][0], n, lane,
+          pb_load<P, RD>(sa, static_cast<uint64_t>(s2) * sa.stride + g0, &l_mix[wv][s2][0][0], n, lane,
                      ((tchm >> s2) & 1u) != 0, ((rejm >> s2) & 1u) != 0, ((ixm >> s2) & 1u) != 0,
                      ((rcm >> s2) & 1u) != 0, nxt);
         }
@@ -950,7 +955,7 @@ k_progress_step(PArgs a) {
         cur.mt = l_mix[wv][s][0][lane];
         cur.ix = ((ixm >> s) & 1u) ? l_mix[wv][s][1][lane] : 0;
       } else if (s1 < static_cast<uint32_t>(S)) {
-        pb_load<P>(sa, static_cast<uint64_t>(s1) * sa.stride + g0, &l_mix[wv][s1][0][0], n, lane,
+        pb_load<P, RD>(sa, static_cast<uint64_t>(s1) * sa.stride + g0, &l_mix[wv][s1][0][0], n, lane,
                    ((tchm >> s1) & 1u) != 0, ((rejm >> s1) & 1u) != 0, ((ixm >> s1) & 1u) != 0,
                    ((rcm >> s1) & 1u) != 0, nxt);
       }
@@ -1163,7 +1168,8 @@ k_progress_step(PArgs a) {
       const bool wp = tw && p.pending != pd0;
       const bool ww = tw && nw != cur.w;
       // (storing a changed row for every touched lane, whole sectors, made
-      // no difference here: profiles/r03/cq_fullrow_ab.txt)
+      // no difference here: profiles/r03/cq_fullrow_ab.txt; in the pipelined
+      // loop too, profiles/r05/pstep_full_ab.txt)
       const bool fm = wm, fn = wn, fw = ww;
       // the ring representation bits are not Progress state (not counted)
       const bool wc = touched && ((nw ^ cur.w) & ~QE_PW_RING_MASK) != 0;
