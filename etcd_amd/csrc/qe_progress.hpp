@@ -579,9 +579,7 @@ struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's tur
 // heartbeat response (`rcl`).  The byte accounting is done
 // by the caller, on the lanes the round actually touches.
 // The rolled loop skips each group of loads no lane needs with a wave-level
-// branch; the pipelined one issues them all (fixed wait counts), and a
-// fully dropped load costs nothing measurable there
-// (profiles/r05/pstep_rc_ab.txt).
+// branch; the pipelined one issues them all (fixed wait counts).
 // The arguments the slot loop reads (a PArgs subset with the same names).
 struct SlotArgs {
   uint64_t stride;
@@ -636,9 +634,8 @@ __device__ __forceinline__ void pb_load(const A &a, uint64_t row, const uint64_t
     b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
     b.lt = bld64(mk_rsrc(a.mlogterm + row, n * 8), rej ? lane * 8 : kOOB);
-    // (the heartbeat contexts: only in the variant that tracks ReadIndex;
-    // the always-issued, fully dropped load it replaces cost nothing
-    // measurable, profiles/r05/pstep_rc_ab.txt)
+    // (the heartbeat contexts: only in the variant that tracks ReadIndex --
+    // elsewhere the value is unused and the load was dead code already)
     if constexpr (RD) b.rc = bld32(opt_rsrc(a.read_ctx, row, n), rcl ? lane * 4 : kOOB);
     else b.rc = 0;
     return;
