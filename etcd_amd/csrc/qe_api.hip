@@ -664,8 +664,8 @@ int qe_collect(uint64_t num_groups, uint64_t group_offset, const uint64_t *perm,
   uint64_t *offsets = static_cast<uint64_t *>(scratch);
   uint32_t *counts = reinterpret_cast<uint32_t *>(offsets + nb);
   const bool vec = (reinterpret_cast<uintptr_t>(flags) % 16) == 0;
-  hipLaunchKernelGGL(k_collect_count, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, st, flags,
-                     num_groups, vec, counts);
+  hipLaunchKernelGGL(k_collect_count, dim3(static_cast<unsigned>((nb + kCountWaves - 1) / kCountWaves)),
+                     dim3(kBlock), 0, st, flags, num_groups, vec, nb, counts);
   hipLaunchKernelGGL(k_collect_scan, dim3(1), dim3(1024), 0, st, counts, nb, offsets, out_count);
   hipLaunchKernelGGL(k_collect_scatter, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, st, flags,
                      num_groups, vec, group_offset, perm, values, offsets, out_groups, out_values);

@@ -19,6 +19,11 @@
 // load waited on before its store) 0.285; writing each thread's 16-group
 // run itself (strided stores) 1.14 ms; reading the scatter's flags a byte
 // per round instead of staging them through LDS 0.31.
+// Round 5 (profiles/r05/collect_ab.txt, rocprofv3 per kernel): the count
+// pass as one wave per chunk with four loads per lane in flight 18.1 ->
+// 16.0 us; the scan with each thread's counts held in registers (17.4 us)
+// or staged through 128 KB of LDS (13.0 us) was slower than this one
+// (10.3 us): a single block's scan is latency, not access width.
 #pragma once
 #include "qe_stream.hpp"
 
@@ -46,35 +51,39 @@ __device__ __forceinline__ uint32_t collect_bits(const uint8_t *flags, uint64_t 
   return m;
 }
 
-// Block-wide exclusive prefix of v (kBlock threads); *total = block sum.
-__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t *total) {
-  __shared__ uint32_t wsum[kBlock / 64];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= static_cast<uint32_t>(d)) inc += o;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  uint32_t before = 0, all = 0;
-#pragma unroll
-  for (int k = 0; k < kBlock / 64; k++) {
-    before += static_cast<uint32_t>(k) < w ? wsum[k] : 0u;
-    all += wsum[k];
-  }
-  *total = all;
-  return before + inc - v;
+// Count: one wave per chunk (four chunks per block, no block barrier); lane
+// l holds groups [16 l, 16 l + 16) of each of the chunk's four 1024-group
+// quarters, so a lane's four 16-B loads are independent and in flight
+// together.  Nonzero bytes are counted four to a word: ((w & 0x7F..) +
+// 0x7F..) | w has the high bit of every nonzero byte set.
+constexpr uint32_t kCountWaves = kBlock / 64;  // chunks per count block
+
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w) {
+  return __builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_collect_count(const uint8_t *flags, uint64_t G, bool vec,
-                                                          uint32_t *counts) {
-  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kCollectChunk + threadIdx.x * kCollectPer;
-  const uint32_t c = __builtin_popcount(collect_bits(flags, G, g, vec));
-  uint32_t total;
-  block_exclusive(c, &total);
-  if (threadIdx.x == 0) counts[blockIdx.x] = total;
+                                                          uint64_t nb, uint32_t *counts) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kCountWaves + (threadIdx.x >> 6);
+  if (b >= nb) return;  // (wave-uniform; no barrier below)
+  const uint64_t base = b * kCollectChunk;
+  uint32_t c = 0;
+  if (vec && base + kCollectChunk <= G) {  // a full chunk, 16-B aligned
+    uint4 v[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+      v[q] = *reinterpret_cast<const uint4 *>(flags + base + (q * 64 + lane) * kCollectPer);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) c += nz_bytes(v[q].x) + nz_bytes(v[q].y) + nz_bytes(v[q].z) + nz_bytes(v[q].w);
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+      c += __builtin_popcount(collect_bits(flags, G, base + (q * 64 + lane) * kCollectPer, vec));
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if (lane == 0) counts[b] = c;
 }
 
 // One block: offsets[b] = sum of counts[0..b), *out_count = the total.

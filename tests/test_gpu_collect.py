@@ -96,6 +96,15 @@ def test_collect_full_size(eng):
     check(eng, flags, values)
 
 
+def test_collect_above_register_scan(eng):
+    """More than 16K chunks (64M groups): the scan's register path no longer
+    holds a thread's counts, the looped path takes over."""
+    G = (1 << 26) + 3 * 4096 + 5
+    rng = np.random.default_rng(11)
+    flags = (rng.random(G) < 0.01).astype(np.uint8)
+    check(eng, flags, None, goff=5)
+
+
 def test_collect_replication_commit_delta(eng):
     """The commit delta of a replication round: the groups whose `adv` flag
     is set, with their new committed index, equal numpy's selection of the
