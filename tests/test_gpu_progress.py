@@ -287,9 +287,9 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
             assert_same(ps, pb)
 
 
-@pytest.mark.parametrize("F", [3, 8])
-@pytest.mark.parametrize("S,masks", [(3, ()), (5, ()), (5, ("inc",)), (6, ("inc", "out")),
-                                     (7, ("inc",)), (9, ())])
+@pytest.mark.parametrize("F", [3, 5, 8])
+@pytest.mark.parametrize("S,masks", [(2, ()), (3, ()), (4, ("inc",)), (5, ()), (5, ("inc",)),
+                                     (6, ("inc", "out")), (7, ("inc",)), (8, ()), (9, ())])
 def test_progress_quiet_slot_tiles(eng, S, masks, F):
     """Tiles (64 groups) in which one slot is quiet in every group -- no
     message, and the leader's own slot or an untracked one -- as the
