@@ -662,7 +662,8 @@ def confchange_files():
 # replay (tests/trace_replay.py) restates each leader's side.
 # ---------------------------------------------------------------------------
 TRACE_FILES = ("probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt", "campaign.txt",
-               "campaign_learner_must_vote.txt")
+               "campaign_learner_must_vote.txt", "confchange_v1_add_single.txt",
+               "confchange_v2_add_single_auto.txt", "confchange_v2_add_double_implicit.txt")
 _MSG_RE = re.compile(r"^([0-9a-f]+)->([0-9a-f]+) (Msg\w+) Term:(\d+) Log:(\d+)/(\d+)(.*)$")
 
 

@@ -544,6 +544,10 @@ class OracleRoundBackend:
     def transferee(self):
         return int(self.pb.lead_transferee[0])
 
+    def set_outgoing(self, mask):
+        """Voters[1] of the loaded JointConfig (0: a simple config again)."""
+        self.pb.out[0] = mask
+
     def send(self, want, sei):
         w = np.array([want], self.orc.mask_dtype(self.sc["S"]))
         sent, snap = self.orc.progress_send(self.pb, w, sei)

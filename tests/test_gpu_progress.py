@@ -530,6 +530,10 @@ class GpuBackend:
         uncommittedSize and applied, as the oracle backend does)."""
         return gpu_propose(self, n, payload, append_only, cc)
 
+    def set_outgoing(self, mask):
+        """Voters[1] of the loaded JointConfig (0: a simple config again)."""
+        self.ps.out.fill_(mask)
+
     def peer(self, s):
         h = self.ps.host()
         st = self.ps.stride

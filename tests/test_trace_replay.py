@@ -1,6 +1,7 @@
 """The reference's interaction traces (raft/testdata/probe_and_replicate.txt,
 snapshot_succeed_via_app_resp.txt, campaign.txt,
-campaign_learner_must_vote.txt) replayed from the leader's side through the
+campaign_learner_must_vote.txt, confchange_v1_add_single.txt,
+confchange_v2_add_single_auto.txt, confchange_v2_add_double_implicit.txt) replayed from the leader's side through the
 oracle (tests/trace_replay.py); tests/test_gpu_trace_replay.py runs the same
 replay through the HIP engine."""
 import numpy as np
@@ -41,7 +42,9 @@ def test_trace_replay_on_oracle(orc, trace):
 def test_trace_fixture_counts():
     t = traces()
     assert set(t) == {"probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt",
-                      "campaign.txt", "campaign_learner_must_vote.txt"}
+                      "campaign.txt", "campaign_learner_must_vote.txt",
+                      "confchange_v1_add_single.txt", "confchange_v2_add_single_auto.txt",
+                      "confchange_v2_add_double_implicit.txt"}
     pr = t["probe_and_replicate.txt"]["commands"]
     rejects = [m for c in pr for b in c["blocks"] if b["kind"] == "recv" and b["node"] == 1
                for m in b["msgs"] if m["type"] == "MsgAppResp" and m["reject"]]
@@ -81,14 +84,34 @@ def _first(cmds, pred):
     raise LookupError("no such message in the fixture")
 
 
-@pytest.mark.parametrize("what", ["reply_index", "reject_hint", "status_line"])
+@pytest.mark.parametrize("what", ["reply_index", "reject_hint", "status_line", "snap_index",
+                                  "paused_line"])
 def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
     """Negative controls: the replay fails when one printed value differs
     from what the engine computes -- the index of the MsgApp answering a
     rejection, the hint a rejection carries (the engine then answers from a
-    different probe), a Progress line of a `status` block."""
-    from tests.trace_replay import probe_and_replicate, snapshot_succeed_via_app_resp
-    if what == "reply_index":
+    different probe), a Progress line of a `status` block, the snapshot
+    index of the MsgSnap to a newly added voter, the Progress a "paused
+    sending" DEBUG line prints."""
+    from tests.trace_replay import (confchange_v1_add_single, probe_and_replicate,
+                                    snapshot_succeed_via_app_resp)
+    if what == "snap_index":
+        def edit(cmds):
+            m = _first(cmds, lambda b, m: b["kind"] == "ready" and b["node"] == 1
+                       and m["type"] == "MsgSnap")
+            m["snap_index"] = 3
+        name, trace = "confchange_v1_add_single.txt", confchange_v1_add_single
+    elif what == "paused_line":
+        def edit(cmds):
+            for c in cmds:
+                for b in c["blocks"]:
+                    for i, x in enumerate(b.get("debug", [])):
+                        if "paused sending replication messages to 2" in x:
+                            b["debug"][i] = x.replace("pendingSnap=4", "pendingSnap=3")
+                            return
+            raise LookupError("paused line not found")
+        name, trace = "confchange_v1_add_single.txt", confchange_v1_add_single
+    elif what == "reply_index":
         def edit(cmds):
             m = _first(cmds, lambda b, m: b["kind"] == "ready" and b["node"] == 1
                        and m["type"] == "MsgApp" and m["to"] == 2 and m["index"] == 19)

@@ -11,6 +11,13 @@ engine's entry points on one group:
   campaign.txt                       an election and the first commit
   campaign_learner_must_vote.txt     an election won with a voter the
                                      candidate's config has, then its catch-up
+  confchange_v1_add_single.txt,      a voter added to a one-node cluster: the
+  confchange_v2_add_single_auto.txt  new Progress (initProgress), the probe it
+                                     gets when the config switches, its
+                                     rejection, the MsgSnap, and the catch-up
+  confchange_v2_add_double_implicit  the same through a joint config with
+  .txt                               AutoLeave: the leave entry appended at
+                                     apply time commits only with both halves
 
 The fixture tests/golden/interaction_traces.json holds what the reference
 printed (tests/golden/make_golden.py extracts it: no reference code runs).
@@ -118,7 +125,8 @@ class Leader:
         return node_id - 1
 
     # -- state set-up ------------------------------------------------------
-    def load(self, li, committed, runs, first_index, peers, snap_index=None, term_start=None):
+    def load(self, li, committed, runs, first_index, peers, snap_index=None, term_start=None,
+             inc=None, out=None):
         lg = {"runs": runs, "committed": committed, "first_index": first_index,
               "last_index": li,
               "term_start": term_start if term_start is not None else runs[-1][0]}
@@ -126,7 +134,10 @@ class Leader:
             lg["snap_index"] = snap_index
         sc = {"name": "", "S": self.S, "self": self.self, "max_ents": 0, "log": lg,
               "peers": peers}
-        self.be.load(sc, initial_arrays(sc))
+        if inc is None and out is None:
+            self.be.load(sc, initial_arrays(sc))
+        else:  # a configuration given as voter masks (JointConfig: out too)
+            self.be.load(sc, initial_arrays(sc), inc=inc, out=out)
 
     def become_leader(self, li, committed, runs, first_index):
         """becomeLeader (raft.go:724-759) after a won election: reset()
@@ -149,16 +160,18 @@ class Leader:
         assert out["result"] == 1
         self.bcast()
 
-    def bcast(self):
-        """bcastAppend: sendAppend to every peer but the leader."""
+    def bcast(self, sei=1):
+        """bcastAppend: sendAppend to every peer but the leader (sei = 0:
+        maybeSendAppend(id, false) to every peer, switchToConfig's probe of
+        a new config, raft.go:1688-1692)."""
         nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
         want = sum(1 << s for s in range(self.S) if s != self.self)
-        out = self.be.send(want, 1)
+        out = self.be.send(want, sei)
         for s in range(self.S):
             if (out["sent"] >> s) & 1:
                 snap = bool((out["snap"] >> s) & 1)
                 idx = self.be.peer(s)["pending"] if snap else nxt[s] - 1
-                self.pending.setdefault(s, []).append((idx, snap))
+                self.pending.setdefault(s, []).append((idx, snap, self.be.last_index()))
 
     # -- replay --------------------------------------------------------------
     def recv(self, block):
@@ -194,16 +207,26 @@ class Leader:
                 n = int(out["msg_count"][s])
                 if n:
                     snap = bool((out["snap"] >> s) & 1)
+                    li = self.be.last_index()
                     self.pending.setdefault(s, []).extend(
-                        [(int(out["msg_index"][s]), snap)] + [(None, False)] * (n - 1))
+                        [(int(out["msg_index"][s]), snap, li)] + [(None, False, li)] * (n - 1))
+        # the Progress a DEBUG line prints after the round's last change to
+        # a peer: MaybeDecrTo's "decreased progress" (raft.go:1231), unless
+        # the sendAppend after it turned the peer to StateSnapshot ("paused
+        # sending replication messages", raft.go:466-470, printed after
+        # BecomeSnapshot)
+        last = {}
         for line in block.get("debug", []):
-            d = re.search(r"decreased progress of (\d+) to \[(.*)\]", line)
+            d = (re.search(r"decreased progress of (\d+) to \[(.*)\]", line) or
+                 re.search(r"paused sending replication messages to (\d+) \[(.*)\]", line))
             if d:
-                want = parse_progress(d.group(2))
-                got = self.be.peer(self.slot(int(d.group(1))))
-                for k in ("state", "match", "next"):
-                    assert got[k] == want[k], (line, got)
-                self.checked["progress"] += 1
+                last[int(d.group(1))] = (line, d.group(2))
+        for node, (line, text) in last.items():
+            want = parse_progress(text)
+            got = self.be.peer(self.slot(node))
+            for k in ("state", "match", "next", "pending"):
+                assert got[k] == want[k], (line, got)
+            self.checked["progress"] += 1
 
     def heartbeat(self):
         commit, _, sent = self.be.heartbeat()
@@ -229,12 +252,13 @@ class Leader:
             assert len(got) == len(ms), (where, s, got, ms)
             first = ms[0]
             want_ix = first["snap_index"] if first["type"] == "MsgSnap" else first["index"]
-            assert got[0] == (want_ix, first["type"] == "MsgSnap"), (where, s, got[0], first)
-            li = self.be.last_index()
-            for m in ms:  # MaxSizePerMsg noLimit: a MsgApp carries every entry after its Log index
+            assert got[0][:2] == (want_ix, first["type"] == "MsgSnap"), (where, s, got[0], first)
+            for m, g in zip(ms, got):
+                # MaxSizePerMsg noLimit: a MsgApp carries every entry after its
+                # Log index up to the lastIndex when it was sent
                 if m["type"] == "MsgApp":
-                    assert [e[1] for e in m["entries"]] == list(range(m["index"] + 1, li + 1)), \
-                        (where, s, m, li)
+                    assert [e[1] for e in m["entries"]] == list(range(m["index"] + 1, g[2] + 1)), \
+                        (where, s, m, g)
             p = self.be.peer(s)
             if first["type"] == "MsgSnap":
                 assert p["state"] == 2 and p["pending"] == first["snap_index"], (where, p)
@@ -261,9 +285,11 @@ class Leader:
             assert got == text, (where, k, got, text)
             self.checked["status"] += 1
 
-    def replay(self, cmds, start_line, stop_line=None, on_election=None):
+    def replay(self, cmds, start_line, stop_line=None, on_election=None, after_ready=None):
         """Walk the commands of a trace from start_line: the leader's recv /
-        Ready / status blocks and its tick-heartbeat commands."""
+        Ready / status blocks and its tick-heartbeat commands.
+        after_ready(block): the host's work after a Ready was handled (e.g.
+        applying a committed conf change)."""
         for c in cmds:
             if c["line"] < start_line or (stop_line is not None and c["line"] >= stop_line):
                 continue
@@ -289,6 +315,8 @@ class Leader:
                     if any(m["type"] == "MsgVote" for m in b["msgs"]):
                         continue  # the candidate's vote requests
                     self.ready(b, where)
+                    if after_ready:
+                        after_ready(b)
         assert not any(self.pending.values()), ("sends never reported", self.pending)
         return self.checked
 
@@ -399,5 +427,85 @@ def campaign_learner_must_vote(leader_factory, elector):
     return checked
 
 
+def _confchange_add_single(name):
+    def run(leader_factory, elector):
+        """raft/testdata/{name} from `stabilize`: node 1, bootstrapped alone
+        with the snapshot at 2 (term 1; newRaft's INFO line), won term 1 by
+        itself, appended its empty entry 3 and the conf change 4 and
+        committed both alone (the first Ready's HardState Commit:4).  The
+        state is restated as it is after that Ready applies 4: node 2 added
+        by initProgress (raft/confchange/confchange.go:259-274: Match 0,
+        Next = lastIndex 4, RecentActive); the leader's own Progress at
+        match 4.  switchToConfig then runs (raft.go:1682-1692): maybeCommit
+        is false (4 is on node 1 only, and {{1, 2}} needs both), so every peer
+        gets maybeSendAppend(id, false) -- issued right after the Ready that
+        prints the switch.  The snapshot a compacted log sends is the
+        applied index 4 (the trace's MsgSnap)."""
+        cmds = traces()[name]["commands"]
+        st = command(cmds, "stabilize")
+        L = leader_factory(1, 2)
+        peers = [{"match": 4, "next": 5, "pending": 0, "state": 1, "probe_sent": False,
+                  "recent_active": True, "ring": []},
+                 {"match": 0, "next": 4, "pending": 0, "state": 0, "probe_sent": False,
+                  "recent_active": True, "ring": []}]
+        L.load(4, 4, [[2, 1]], 3, peers, snap_index=4)
+        switched = []
+
+        def after(block):
+            if any("switched to configuration voters=(1 2)" in x for x in block["debug"]):
+                L.bcast(sei=0)
+                switched.append(block)
+
+        checked = L.replay(cmds, st["line"], after_ready=after)
+        assert len(switched) == 1
+        return checked
+    run.__name__ = name[:-4]
+    run.__doc__ = run.__doc__.format(name=name)
+    return run
+
+
+def confchange_v2_add_double_implicit(leader_factory, elector):
+    """raft/testdata/confchange_v2_add_double_implicit.txt from `stabilize 1
+    2`: as the add_single traces, but the V2 change enters a joint config
+    with AutoLeave (voters (1 2)&&(1)): applying 4 switches to it, the new
+    voter gets its probe (switchToConfig, raft.go:1682-1692), and advance()
+    then appends the empty EntryConfChangeV2 that leaves it (raft.go:
+    apply-time auto-leave: appendEntry alone, no bcast -- qe_propose with
+    QE_PROP_APPEND_ONLY) at 5.  Index 5 commits only when both halves hold
+    it: on node 2's ack of 5 (the commit rule of the joint config), whose
+    bcast carries Commit:5; applying 5 leaves the joint config (Voters[1]
+    empty: the same quorum as the simple config) and probes again, which
+    sends nothing."""
+    cmds = traces()["confchange_v2_add_double_implicit.txt"]["commands"]
+    st = command(cmds, "stabilize 1 2")
+    L = leader_factory(1, 2)
+    peers = [{"match": 4, "next": 5, "pending": 0, "state": 1, "probe_sent": False,
+              "recent_active": True, "ring": []},
+             {"match": 0, "next": 4, "pending": 0, "state": 0, "probe_sent": False,
+              "recent_active": True, "ring": []}]
+    L.load(4, 4, [[2, 1]], 3, peers, snap_index=4, inc=0b11, out=0b01)
+    seen = []
+
+    def after(block):
+        for x in block["debug"]:
+            if "switched to configuration voters=(1 2)&&(1) autoleave" in x:
+                L.bcast(sei=0)
+                out = L.be.propose(1, append_only=True)  # the auto-leave entry
+                assert out["result"] == 1 and L.be.last_index() == 5, out
+                seen.append("enter")
+            elif x.endswith("switched to configuration voters=(1 2)"):
+                L.be.set_outgoing(0)
+                L.bcast(sei=0)
+                seen.append("leave")
+
+    checked = L.replay(cmds, st["line"], after_ready=after)
+    assert seen == ["enter", "leave"] and L.be.committed() == 5
+    return checked
+
+
+confchange_v1_add_single = _confchange_add_single("confchange_v1_add_single.txt")
+confchange_v2_add_single_auto = _confchange_add_single("confchange_v2_add_single_auto.txt")
+
 TRACES = [probe_and_replicate, snapshot_succeed_via_app_resp, campaign,
-          campaign_learner_must_vote]
+          campaign_learner_must_vote, confchange_v1_add_single, confchange_v2_add_single_auto,
+          confchange_v2_add_double_implicit]
