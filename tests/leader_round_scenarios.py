@@ -548,6 +548,12 @@ class OracleRoundBackend:
         """Voters[1] of the loaded JointConfig (0: a simple config again)."""
         self.pb.out[0] = mask
 
+    def set_config(self, tracked, inc):
+        """A new configuration's tracked slots and Voters[0] (applied conf
+        change; the Progress of a slot that stays keeps its state)."""
+        self.pb.tracked[0] = tracked
+        self.pb.inc[0] = inc
+
     def send(self, want, sei):
         w = np.array([want], self.orc.mask_dtype(self.sc["S"]))
         sent, snap = self.orc.progress_send(self.pb, w, sei)

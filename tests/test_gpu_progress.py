@@ -534,6 +534,12 @@ class GpuBackend:
         """Voters[1] of the loaded JointConfig (0: a simple config again)."""
         self.ps.out.fill_(mask)
 
+    def set_config(self, tracked, inc):
+        """A new configuration's tracked slots and Voters[0] (applied conf
+        change; the Progress of a slot that stays keeps its state)."""
+        self.ps.tracked.fill_(tracked)
+        self.ps.inc.fill_(inc)
+
     def peer(self, s):
         h = self.ps.host()
         st = self.ps.stride

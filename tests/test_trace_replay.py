@@ -44,7 +44,7 @@ def test_trace_fixture_counts():
     assert set(t) == {"probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt",
                       "campaign.txt", "campaign_learner_must_vote.txt",
                       "confchange_v1_add_single.txt", "confchange_v2_add_single_auto.txt",
-                      "confchange_v2_add_double_implicit.txt"}
+                      "confchange_v2_add_double_implicit.txt", "confchange_v1_remove_leader.txt"}
     pr = t["probe_and_replicate.txt"]["commands"]
     rejects = [m for c in pr for b in c["blocks"] if b["kind"] == "recv" and b["node"] == 1
                for m in b["msgs"] if m["type"] == "MsgAppResp" and m["reject"]]
@@ -85,17 +85,23 @@ def _first(cmds, pred):
 
 
 @pytest.mark.parametrize("what", ["reply_index", "reject_hint", "status_line", "snap_index",
-                                  "paused_line"])
+                                  "paused_line", "dropped_proposal"])
 def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
     """Negative controls: the replay fails when one printed value differs
     from what the engine computes -- the index of the MsgApp answering a
     rejection, the hint a rejection carries (the engine then answers from a
     different probe), a Progress line of a `status` block, the snapshot
     index of the MsgSnap to a newly added voter, the Progress a "paused
-    sending" DEBUG line prints."""
-    from tests.trace_replay import (confchange_v1_add_single, probe_and_replicate,
-                                    snapshot_succeed_via_app_resp)
-    if what == "snap_index":
+    sending" DEBUG line prints, a removed leader's proposal printed as
+    accepted."""
+    from tests.trace_replay import (confchange_v1_add_single, confchange_v1_remove_leader,
+                                    probe_and_replicate, snapshot_succeed_via_app_resp)
+    if what == "dropped_proposal":
+        def edit(cmds):
+            c = next(c for c in cmds if c.get("dropped"))
+            c["dropped"] = False
+        name, trace = "confchange_v1_remove_leader.txt", confchange_v1_remove_leader
+    elif what == "snap_index":
         def edit(cmds):
             m = _first(cmds, lambda b, m: b["kind"] == "ready" and b["node"] == 1
                        and m["type"] == "MsgSnap")

@@ -18,6 +18,10 @@ engine's entry points on one group:
   confchange_v2_add_double_implicit  the same through a joint config with
   .txt                               AutoLeave: the leave entry appended at
                                      apply time commits only with both halves
+  confchange_v1_remove_leader.txt    a leader that removes itself: proposals
+                                     through qe_propose, the commit quorum
+                                     without it, its dropped proposal, its
+                                     heartbeats
 
 The fixture tests/golden/interaction_traces.json holds what the reference
 printed (tests/golden/make_golden.py extracts it: no reference code runs).
@@ -126,7 +130,7 @@ class Leader:
 
     # -- state set-up ------------------------------------------------------
     def load(self, li, committed, runs, first_index, peers, snap_index=None, term_start=None,
-             inc=None, out=None):
+             inc=None, out=None, tracked=None):
         lg = {"runs": runs, "committed": committed, "first_index": first_index,
               "last_index": li,
               "term_start": term_start if term_start is not None else runs[-1][0]}
@@ -134,10 +138,10 @@ class Leader:
             lg["snap_index"] = snap_index
         sc = {"name": "", "S": self.S, "self": self.self, "max_ents": 0, "log": lg,
               "peers": peers}
-        if inc is None and out is None:
+        if inc is None and out is None and tracked is None:
             self.be.load(sc, initial_arrays(sc))
-        else:  # a configuration given as voter masks (JointConfig: out too)
-            self.be.load(sc, initial_arrays(sc), inc=inc, out=out)
+        else:  # a configuration given as slot masks (JointConfig: out too)
+            self.be.load(sc, initial_arrays(sc), inc=inc, out=out, tracked=tracked)
 
     def become_leader(self, li, committed, runs, first_index):
         """becomeLeader (raft.go:724-759) after a won election: reset()
@@ -228,6 +232,25 @@ class Leader:
                 assert got[k] == want[k], (line, got)
             self.checked["progress"] += 1
 
+    def propose(self, c, where):
+        """`propose L data` / `propose-conf-change L ...`: one MsgProp
+        through qe_propose (stepLeader's arm, raft.go:1019-1076, and the
+        bcastAppend after appendEntry) -- a conf-change entry for the
+        latter; the trace prints "raft proposal dropped" or "ok"."""
+        cc = [(0, False, 0)] if c["cmd"].startswith("propose-conf-change") else None
+        nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
+        out = self.be.propose(1, cc=cc)
+        if c.get("dropped"):
+            assert out["result"] in (2, 3, 4), (where, out)  # QE_PROP_DROPPED_*
+            return
+        assert out["result"] == 1, (where, out)  # QE_PROP_OK
+        for s in range(self.S):
+            if (out["sent"] >> s) & 1:
+                snap = bool((out["snap"] >> s) & 1)
+                idx = self.be.peer(s)["pending"] if snap else nxt[s] - 1
+                self.pending.setdefault(s, []).append((idx, snap, self.be.last_index()))
+        self.checked["proposals"] = self.checked.get("proposals", 0) + 1
+
     def heartbeat(self):
         commit, _, sent = self.be.heartbeat()
         for s in range(self.S):
@@ -285,17 +308,22 @@ class Leader:
             assert got == text, (where, k, got, text)
             self.checked["status"] += 1
 
-    def replay(self, cmds, start_line, stop_line=None, on_election=None, after_ready=None):
+    def replay(self, cmds, start_line, stop_line=None, on_election=None, after_ready=None,
+               proposals=False):
         """Walk the commands of a trace from start_line: the leader's recv /
         Ready / status blocks and its tick-heartbeat commands.
         after_ready(block): the host's work after a Ready was handled (e.g.
-        applying a committed conf change)."""
+        applying a committed conf change); proposals: run the leader's
+        `propose` commands through qe_propose."""
         for c in cmds:
             if c["line"] < start_line or (stop_line is not None and c["line"] >= stop_line):
                 continue
             where = f"line {c['line']} `{c['cmd']}`"
             if c["cmd"] == f"tick-heartbeat {self.node}":
                 self.heartbeat()
+            if proposals and c["cmd"].startswith(("propose ", "propose-conf-change ")) and \
+                    c["cmd"].split()[1] == str(self.node):
+                self.propose(c, where)
             for b in c["blocks"]:
                 if b["kind"] == "status":
                     if c["cmd"] == f"status {self.node}":
@@ -503,9 +531,41 @@ def confchange_v2_add_double_implicit(leader_factory, elector):
     return checked
 
 
+def confchange_v1_remove_leader(leader_factory, elector):
+    """raft/testdata/confchange_v1_remove_leader.txt from `log-level debug`:
+    3 voters bootstrapped with the snapshot at 2 (term 1), node 1 elected at
+    term 1 and everything stabilized (quietly): its empty entry 3 committed
+    and acked, every follower in StateReplicate at match 3 with nothing in
+    flight; pendingConfIndex 2 (becomeLeader takes lastIndex before the
+    empty entry, raft.go:745-757), applied 3.  Node 1 then proposes its own
+    removal (a conf-change entry at 4) and entries 5 and 6; applying 4
+    removes its Progress (tracked and Voters lose slot 0) and
+    switchToConfig returns early for a removed leader (raft.go:1663-1674).
+    From then on the commit quorum is {2, 3} alone (6 waits for node 3),
+    its proposals are dropped (no Progress of its own, raft.go:1023-1028),
+    and it still heartbeats both followers."""
+    cmds = traces()["confchange_v1_remove_leader.txt"]["commands"]
+    st = command(cmds, "log-level debug")
+    L = leader_factory(1, 3)
+    rep = {"match": 3, "next": 4, "pending": 0, "state": 1, "probe_sent": False,
+           "recent_active": True, "ring": []}
+    L.load(3, 3, [[2, 1]], 3, [dict(rep) for _ in range(3)], tracked=0b111, inc=0b111)
+    L.be.pci, L.be.applied = 2, 3
+    seen = []
+
+    def after(block):
+        if any(x.endswith("switched to configuration voters=(2 3)") for x in block["debug"]):
+            L.be.set_config(tracked=0b110, inc=0b110)
+            seen.append(block)
+
+    checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
+    assert len(seen) == 1 and L.be.committed() == 6 and checked.get("proposals") == 3
+    return checked
+
+
 confchange_v1_add_single = _confchange_add_single("confchange_v1_add_single.txt")
 confchange_v2_add_single_auto = _confchange_add_single("confchange_v2_add_single_auto.txt")
 
 TRACES = [probe_and_replicate, snapshot_succeed_via_app_resp, campaign,
           campaign_learner_must_vote, confchange_v1_add_single, confchange_v2_add_single_auto,
-          confchange_v2_add_double_implicit]
+          confchange_v2_add_double_implicit, confchange_v1_remove_leader]
