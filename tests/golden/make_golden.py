@@ -664,7 +664,8 @@ def confchange_files():
 TRACE_FILES = ("probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt", "campaign.txt",
                "campaign_learner_must_vote.txt", "confchange_v1_add_single.txt",
                "confchange_v2_add_single_auto.txt", "confchange_v2_add_double_implicit.txt",
-               "confchange_v1_remove_leader.txt")
+               "confchange_v1_remove_leader.txt", "confchange_v2_add_single_explicit.txt",
+               "confchange_v2_add_double_auto.txt")
 _MSG_RE = re.compile(r"^([0-9a-f]+)->([0-9a-f]+) (Msg\w+) Term:(\d+) Log:(\d+)/(\d+)(.*)$")
 
 
@@ -756,8 +757,10 @@ def interaction_traces():
                     k += 1
                 c = {"line": j + 2, "cmd": cmd[0], "input": cmd[1:],
                      "blocks": parse_trace_output(body)}
-                if cmd[0].startswith("propose"):  # "ok" or "raft proposal dropped"
+                if cmd[0].startswith("propose"):  # "ok", "raft proposal dropped" or the
+                    # INFO line of a conf change stepLeader turns into an empty entry
                     c["dropped"] = any("raft proposal dropped" in x for x in body)
+                    c["ignored_cc"] = any("ignoring conf change" in x for x in body)
                 if cmd[0].startswith("raft-log"):  # the node's log: term/index per entry
                     c["log"] = [[int(a), int(b)] for a, b in
                                 (re.match(r"^(\d+)/(\d+) Entry", x).groups() for x in body

@@ -548,6 +548,11 @@ class OracleRoundBackend:
         """Voters[1] of the loaded JointConfig (0: a simple config again)."""
         self.pb.out[0] = mask
 
+    def set_snapshot(self, index):
+        """The index of the snapshot a MsgSnap sends (the applied index
+        where the interaction traces take it)."""
+        self.pb.snap_index[0] = index
+
     def set_config(self, tracked, inc):
         """A new configuration's tracked slots and Voters[0] (applied conf
         change; the Progress of a slot that stays keeps its state)."""

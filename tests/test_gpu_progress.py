@@ -534,6 +534,11 @@ class GpuBackend:
         """Voters[1] of the loaded JointConfig (0: a simple config again)."""
         self.ps.out.fill_(mask)
 
+    def set_snapshot(self, index):
+        """The index of the snapshot a MsgSnap sends (the applied index
+        where the interaction traces take it)."""
+        self.ps.snap_index.fill_(index)
+
     def set_config(self, tracked, inc):
         """A new configuration's tracked slots and Voters[0] (applied conf
         change; the Progress of a slot that stays keeps its state)."""

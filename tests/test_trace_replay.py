@@ -44,7 +44,8 @@ def test_trace_fixture_counts():
     assert set(t) == {"probe_and_replicate.txt", "snapshot_succeed_via_app_resp.txt",
                       "campaign.txt", "campaign_learner_must_vote.txt",
                       "confchange_v1_add_single.txt", "confchange_v2_add_single_auto.txt",
-                      "confchange_v2_add_double_implicit.txt", "confchange_v1_remove_leader.txt"}
+                      "confchange_v2_add_double_implicit.txt", "confchange_v1_remove_leader.txt",
+                      "confchange_v2_add_single_explicit.txt", "confchange_v2_add_double_auto.txt"}
     pr = t["probe_and_replicate.txt"]["commands"]
     rejects = [m for c in pr for b in c["blocks"] if b["kind"] == "recv" and b["node"] == 1
                for m in b["msgs"] if m["type"] == "MsgAppResp" and m["reject"]]
@@ -85,7 +86,7 @@ def _first(cmds, pred):
 
 
 @pytest.mark.parametrize("what", ["reply_index", "reject_hint", "status_line", "snap_index",
-                                  "paused_line", "dropped_proposal"])
+                                  "paused_line", "dropped_proposal", "ignored_cc"])
 def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
     """Negative controls: the replay fails when one printed value differs
     from what the engine computes -- the index of the MsgApp answering a
@@ -93,10 +94,16 @@ def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
     different probe), a Progress line of a `status` block, the snapshot
     index of the MsgSnap to a newly added voter, the Progress a "paused
     sending" DEBUG line prints, a removed leader's proposal printed as
-    accepted."""
+    accepted, a refused conf change printed as accepted."""
     from tests.trace_replay import (confchange_v1_add_single, confchange_v1_remove_leader,
-                                    probe_and_replicate, snapshot_succeed_via_app_resp)
-    if what == "dropped_proposal":
+                                    confchange_v2_add_single_explicit, probe_and_replicate,
+                                    snapshot_succeed_via_app_resp)
+    if what == "ignored_cc":
+        def edit(cmds):
+            c = next(c for c in cmds if c.get("ignored_cc"))
+            c["ignored_cc"] = False
+        name, trace = "confchange_v2_add_single_explicit.txt", confchange_v2_add_single_explicit
+    elif what == "dropped_proposal":
         def edit(cmds):
             c = next(c for c in cmds if c.get("dropped"))
             c["dropped"] = False

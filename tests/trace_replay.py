@@ -18,6 +18,10 @@ engine's entry points on one group:
   confchange_v2_add_double_implicit  the same through a joint config with
   .txt                               AutoLeave: the leave entry appended at
                                      apply time commits only with both halves
+  confchange_v2_add_single_explicit  the joint config left by a proposal:
+  .txt                               stepLeader's conf-change refusals
+  confchange_v2_add_double_auto.txt  two voters added and removed through
+                                     joint configs with AutoLeave
   confchange_v1_remove_leader.txt    a leader that removes itself: proposals
                                      through qe_propose, the commit quorum
                                      without it, its dropped proposal, its
@@ -237,13 +241,17 @@ class Leader:
         through qe_propose (stepLeader's arm, raft.go:1019-1076, and the
         bcastAppend after appendEntry) -- a conf-change entry for the
         latter; the trace prints "raft proposal dropped" or "ok"."""
-        cc = [(0, False, 0)] if c["cmd"].startswith("propose-conf-change") else None
+        # a conf change with no changes listed is the empty ConfChangeV2
+        # that leaves a joint config
+        cc = ([(0, not c["input"], 0)] if c["cmd"].startswith("propose-conf-change") else None)
         nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
         out = self.be.propose(1, cc=cc)
         if c.get("dropped"):
             assert out["result"] in (2, 3, 4), (where, out)  # QE_PROP_DROPPED_*
             return
         assert out["result"] == 1, (where, out)  # QE_PROP_OK
+        # refused conf changes become empty normal entries (raft.go:1050-1069)
+        assert out["cc_refused"] == int(bool(c.get("ignored_cc"))), (where, out)
         for s in range(self.S):
             if (out["sent"] >> s) & 1:
                 snap = bool((out["snap"] >> s) & 1)
@@ -563,9 +571,109 @@ def confchange_v1_remove_leader(leader_factory, elector):
     return checked
 
 
+def confchange_v2_add_single_explicit(leader_factory, elector):
+    """raft/testdata/confchange_v2_add_single_explicit.txt from `stabilize 1
+    2`: the joint config (1 2)&&(1) entered explicitly (no AutoLeave), set up
+    as in the implicit trace (pendingConfIndex 4, applied 4).  Then three
+    conf-change proposals through qe_propose's MsgProp arm: "v3 v4 v5" while
+    joint (refused: must leave first -> an empty normal entry at 5), the
+    empty one that leaves (accepted at 6; pendingConfIndex 6), and, once
+    that is applied, an empty one outside a joint config (refused: an empty
+    entry at 7) -- the trace prints the refusals as INFO lines."""
+    cmds = traces()["confchange_v2_add_single_explicit.txt"]["commands"]
+    st = command(cmds, "stabilize 1 2")
+    L = leader_factory(1, 2)
+    peers = [{"match": 4, "next": 5, "pending": 0, "state": 1, "probe_sent": False,
+              "recent_active": True, "ring": []},
+             {"match": 0, "next": 4, "pending": 0, "state": 0, "probe_sent": False,
+              "recent_active": True, "ring": []}]
+    L.load(4, 4, [[2, 1]], 3, peers, snap_index=4, inc=0b11, out=0b01)
+    L.be.pci, L.be.applied = 4, 4
+    seen = []
+
+    def after(block):
+        for x in block["debug"]:
+            if x.endswith("switched to configuration voters=(1 2)&&(1)"):
+                L.bcast(sei=0)
+                seen.append("enter")
+            elif x.endswith("switched to configuration voters=(1 2)"):
+                L.be.set_outgoing(0)
+                L.be.applied = 6
+                L.bcast(sei=0)
+                seen.append("leave")
+
+    checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
+    assert seen == ["enter", "leave"] and L.be.committed() == 7 and checked.get("proposals") == 3
+    return checked
+
+
+def confchange_v2_add_double_auto(leader_factory, elector):
+    """raft/testdata/confchange_v2_add_double_auto.txt from `process-ready
+    1`: voters 2 and 3 added through the joint config (1 2 3)&&(1) with
+    AutoLeave, then both removed again through (1)&&(1 2 3).  Restated at
+    the first Ready's application of 4 (as the add_single traces, two new
+    peers; pendingConfIndex 4, applied 4); the host work after each Ready
+    that switches configs is the reference's: switchToConfig's probe of
+    every peer (raft.go:1682-1692), advance()'s auto-leave appendEntry with
+    pendingConfIndex at it (raft.go:549-569), the new voter masks, and the
+    snapshot index, which the interaction env takes at the applied index.
+    The removals' proposal and two entries go through qe_propose; the joint
+    quorum (1)&&(1 2 3) commits 7 and 8 one ack at a time; after the last
+    switch the responses of the removed peers are not stepped (RawNode.Step:
+    no Progress for a response's sender, rawnode.go:108-119) -- here, slots
+    no longer tracked."""
+    cmds = traces()["confchange_v2_add_double_auto.txt"]["commands"]
+    st = command(cmds, "process-ready 1")
+    L = leader_factory(1, 3)
+    new = {"match": 0, "next": 4, "pending": 0, "state": 0, "probe_sent": False,
+           "recent_active": True, "ring": []}
+    peers = [{"match": 4, "next": 5, "pending": 0, "state": 1, "probe_sent": False,
+              "recent_active": True, "ring": []}, dict(new), dict(new)]
+    L.load(4, 4, [[2, 1]], 3, peers, snap_index=4, tracked=0b111, inc=0b111, out=0b001)
+    L.be.pci, L.be.applied = 4, 4
+    seen = []
+
+    def auto_leave():
+        out = L.be.propose(1, append_only=True)
+        assert out["result"] == 1, out
+        L.be.pci = L.be.last_index()
+
+    def after(block):
+        for x in block["debug"]:
+            if x.endswith("switched to configuration voters=(1 2 3)&&(1) autoleave"):
+                L.bcast(sei=0)
+                auto_leave()  # at 5
+                seen.append(x)
+            elif x.endswith("switched to configuration voters=(1 2 3)"):
+                L.be.set_outgoing(0)
+                L.be.applied = 5
+                L.be.set_snapshot(5)
+                L.bcast(sei=0)
+                seen.append(x)
+            elif x.endswith("switched to configuration voters=(1)&&(1 2 3) autoleave"):
+                L.be.set_config(tracked=0b111, inc=0b001)
+                L.be.set_outgoing(0b111)
+                L.be.applied = 6
+                L.be.set_snapshot(6)
+                L.bcast(sei=0)
+                auto_leave()  # at 9
+                seen.append(x)
+            elif x.endswith("switched to configuration voters=(1)"):
+                L.be.set_config(tracked=0b001, inc=0b001)
+                L.be.set_outgoing(0)
+                L.be.applied = 9
+                L.bcast(sei=0)
+                seen.append(x)
+
+    checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
+    assert len(seen) == 4 and L.be.committed() == 9 and checked.get("proposals") == 3
+    return checked
+
+
 confchange_v1_add_single = _confchange_add_single("confchange_v1_add_single.txt")
 confchange_v2_add_single_auto = _confchange_add_single("confchange_v2_add_single_auto.txt")
 
 TRACES = [probe_and_replicate, snapshot_succeed_via_app_resp, campaign,
           campaign_learner_must_vote, confchange_v1_add_single, confchange_v2_add_single_auto,
-          confchange_v2_add_double_implicit, confchange_v1_remove_leader]
+          confchange_v2_add_double_implicit, confchange_v2_add_single_explicit,
+          confchange_v2_add_double_auto, confchange_v1_remove_leader]
