@@ -86,6 +86,12 @@ WORKLOADS = {
                 "MaybeUpdate, maybeCommit) and bcastAppend to the 4 followers (StateReplicate, "
                 "Inflights F=8 with room, noLimit MaxSizePerMsg): one MsgApp and one ring entry "
                 "each", 1 << 24, 5, "propose"),
+    "switch_config": ("16M groups x switchToConfig after an applied conf change through "
+                      "qe_switch_config (leader in slot 0, followers StateReplicate with room, "
+                      "old voters {0,1,2,3} + learner 4): half the groups remove voter 3 (the "
+                      "smaller quorum commits more: bcastAppend to 1, 2, 4), half promote the "
+                      "learner (maybeCommit under 5 voters, else the probe of every peer); a "
+                      "transfer to 3 pending in 1/8 of the groups", 1 << 24, 5, "switch"),
     "check_quorum": ("16M groups x 5 peers: MsgCheckQuorum on the leader over the resident "
                      "Progress words (QuorumActive over RecentActive, step-down mask, "
                      "RecentActive reset; each follower active with p = 0.7)", 1 << 24, 5, "cq"),
@@ -671,6 +677,58 @@ def setup(name, G, S, kind, d, stats):
 
         return step, bpg, G, "group-proposals", {"ps": ps, "pr": pr, "prepare": prepare,
                                                  "verify": verify}
+
+    if kind == "switch":
+        # raft.switchToConfig (raft/raft.go:1651-1700) on the progress_send
+        # state: maybeCommit under the new quorum, bcastAppend or the probe of
+        # every peer, abortLeaderTransfer
+        F = 8
+        ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, masks=("inc",),
+                                  extras=("self_slot", "tracked", "lead_transferee"), max_ents=0)
+        psend_state(ps)
+        st = ps.stride
+        li = ps.last_index[:G]
+        ps.self_slot.fill_(0)
+        ps.match[:G].copy_(li)  # the leader's own Progress: Match = lastIndex
+        ps.next[:G].copy_(li + 1)
+        ps.term_start.copy_(li - 127)  # the leader's term holds the followers' acks
+        h = counter_rows(G, 1, 0x5C0F, goff, d.dev)[:G]
+        remove = (h & 1) == 1
+        ps.inc.copy_(torch.where(remove, 0b00111, 0b11111).to(torch.uint8))
+        ps.tracked.copy_(torch.where(remove, 0b10111, 0b11111).to(torch.uint8))
+        ps.lead_transferee.copy_(torch.where(((h >> 1) & 7) == 0, 3, 0xFF).to(torch.uint8))
+        m = ps.match.view(S, st)[:4, :G]
+        ps.committed.copy_(m.sort(dim=0, descending=True).values[2])  # the old quorum's
+        sw = engine.Switch(ps)
+        mutable = ("next", "peer", "committed", "lead_transferee")
+        pristine = {k: getattr(ps, k).clone() for k in mutable}
+
+        def prepare():
+            for k in mutable:
+                getattr(ps, k).copy_(pristine[k])
+
+        # algorithmic bytes: the instrumented variant counts every field the
+        # reference logic reads or writes once (the oracle's
+        # count is equal, tests/test_gpu_switch.py)
+        prepare()
+        bpg = engine.switch_bytes_requested(ps, sw) / G
+        prepare()
+        import ctypes as C
+        p_, q_ = ps.struct(), sw.struct()
+        lib = engine._lib.lib()
+        stream = engine._stream(d.dev)
+        sp = engine._ptr(stats)
+
+        def step():
+            engine.check("qe_switch_config", lib.qe_switch_config(C.byref(p_), C.byref(q_), sp,
+                                                                   stream))
+
+        def verify():
+            out = sw.result & engine._lib.QE_SW_OUTCOME
+            return bool(((out == engine._lib.QE_SW_BCAST) | (out == engine._lib.QE_SW_PROBE)).all())
+
+        return step, bpg, G, "group-switches", {"ps": ps, "sw": sw, "prepare": prepare,
+                                                "verify": verify}
 
     if kind == "heartbeat":
         # stepLeader MsgBeat -> bcastHeartbeat -> sendHeartbeat (raft/raft.go:

@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 6
+QE_ABI_VERSION = 7
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -126,6 +126,14 @@ class QeProposals(C.Structure):  # ABI 6
                 ("cc_refused", vp), ("sent", vp), ("snap", vp), ("bytes_requested", vp)]
 
 
+class QeSwitch(C.Structure):  # ABI 7
+    _fields_ = [("switched", vp), ("result", vp), ("sent", vp), ("snap", vp),
+                ("bytes_requested", vp)]
+
+
+QE_SW_NONE, QE_SW_REMOVED, QE_SW_NO_VOTERS, QE_SW_BCAST, QE_SW_PROBE = 0, 1, 2, 3, 4
+QE_SW_OUTCOME, QE_SW_TRANSFER_ABORTED = 0x0F, 0x10
+
 QE_PROP_NONE, QE_PROP_OK, QE_PROP_DROPPED_NOT_MEMBER, QE_PROP_DROPPED_TRANSFER, \
     QE_PROP_DROPPED_SIZE = 0, 1, 2, 3, 4
 QE_PROP_MAX_CC = 8
@@ -208,6 +216,7 @@ PROTOTYPES = {
     "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp, vp]),
     "qe_propose": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeProposals), vp, vp]),
     "qe_heartbeat": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp, vp]),
+    "qe_switch_config": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeSwitch), vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),

@@ -498,6 +498,23 @@ int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, 
                            p->out_mask != nullptr, static_cast<hipStream_t>(stream));
 }
 
+int qe_switch_config(const qe_progress *p, const qe_switch *sw, uint64_t *stats, void *stream) {
+  PArgs a;
+  int rc = progress_args(p, a);
+  if (rc) return rc;
+  if (!sw) return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (!sw->result) return QE_EINVAL;
+  a.sw_switched = sw->switched;
+  a.sw_result = sw->result;
+  a.sent = sw->sent;
+  a.snap = sw->snap;
+  a.acct = sw->bytes_requested;
+  a.stats = stats;
+  return dispatch_progress(p->num_slots, a, sw->bytes_requested ? 9 : 8, p->inc_mask != nullptr,
+                           p->out_mask != nullptr, static_cast<hipStream_t>(stream));
+}
+
 int qe_heartbeat(const qe_progress *p, uint64_t *commit, uint32_t *ctx, void *sent, void *stream) {
   if (!p) return QE_EINVAL;
   if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)

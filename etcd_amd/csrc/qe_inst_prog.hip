@@ -112,6 +112,15 @@ static int launch_propose(const PArgs &a, bool masked, bool joint, hipStream_t s
   return hip_status(hipGetLastError());
 }
 
+template <bool ACCT>
+static int launch_switch_config(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  if (joint) hipLaunchKernelGGL((k_switch_config<S, MT, true, true, ACCT>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_switch_config<S, MT, true, false, ACCT>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_switch_config<S, MT, false, false, ACCT>), grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 static int launch_heartbeat(const PArgs &a, hipStream_t st) {
   const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
   hipLaunchKernelGGL((k_heartbeat<S, MT>), grid, dim3(kBlock), 0, st, a);
@@ -121,7 +130,8 @@ static int launch_heartbeat(const PArgs &a, hipStream_t st) {
 // kind 0: qe_progress_step, 1: qe_progress_send, 2: qe_progress_step with
 // byte accounting (instrumented variant, measurement only), 3:
 // qe_check_quorum, 4: qe_read_index, 5: qe_propose, 6: qe_propose with byte
-// accounting, 7: qe_heartbeat
+// accounting, 7: qe_heartbeat, 8: qe_switch_config, 9: qe_switch_config with
+// byte accounting
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
   if (kind == 1) return launch_progress_send(a, st);
@@ -130,6 +140,8 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
   if (kind == 5) return launch_propose<false>(a, masked, joint, st);
   if (kind == 6) return launch_propose<true>(a, masked, joint, st);
   if (kind == 7) return launch_heartbeat(a, st);
+  if (kind == 8) return launch_switch_config<false>(a, masked, joint, st);
+  if (kind == 9) return launch_switch_config<true>(a, masked, joint, st);
   // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
   // or two older terms before the current one); 8 keep the block's LDS at
   // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);

@@ -756,6 +756,9 @@ struct PArgs {
   // heartbeat (qe_heartbeat, ABI 6)
   uint64_t *hb_commit;
   uint32_t *hb_ctx;
+  // switchToConfig (qe_switch_config, ABI 7)
+  const uint8_t *sw_switched;
+  uint8_t *sw_result;
 };
 
 struct PR {
@@ -844,7 +847,7 @@ __device__ __forceinline__ uint64_t mci_of(const uint64_t (&vals)[S], uint32_t i
 }
 
 enum { P_GROUPS, P_SUM, P_ADV, P_VIOL, P_READ, P_CSUM, P_N };
-enum { Q_GROUPS, Q_SUM, Q_ADV, Q_CSUM, Q_N };  // k_propose
+enum { Q_GROUPS, Q_SUM, Q_ADV, Q_CSUM, Q_N };  // k_propose, k_switch_config
 
 // k_progress_step: qe_progress.hpp
 

@@ -1678,6 +1678,184 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
   acct_flush<ACCT>(ac, a.acct);
 }
 
+// qe_switch_config (ABI 7): raft.switchToConfig (raft/raft.go:1651-1700) on
+// every group whose configuration was just switched.  One lane per group, a
+// wave per 64-group tile, two round trips per tile: A (the switched flag,
+// the leader's slot, the tracked / Voters masks, the transferee) of the
+// wave's next tile is issued during this tile, before its stores; B (the
+// log model, every voter's Match, every tracked slot's Next and word -- the
+// probe's targets, a superset of the bcast's) at the top of the tile for the
+// groups that get past switchToConfig's early returns.  maybeCommit and its
+// term gate in registers, then one maybeSendAppend per target (memory-form
+// ring appends, as qe_progress_send).
+constexpr uint64_t kSwitchSalt = 0x2545F4914F6CDD1Dull;
+
+template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT>
+__global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr uint32_t MB = sizeof(MT);
+  uint64_t cnt[Q_N] = {0, 0, 0, 0};
+  Acct<ACCT> ac;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  struct SA {
+    uint32_t sw, self, trk, mi, mo, ltr;
+    uint64_t c0;  // committed of every group (the statistics cover it)
+  };
+  auto load_a = [&](uint64_t t, SA &x) {
+    const uint32_t n = t < ntiles ? tile_n(a.G, t) : 0u;  // past the end: nothing
+    const uint64_t g0 = t * 64;
+    x.sw = a.sw_switched ? bld8(mk_rsrc(a.sw_switched + g0, n), lane) : (lane < n ? 1u : 0u);
+    const uint32_t o1 = x.sw ? lane : kOOB;
+    x.self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), o1) : 0xFFu;
+    x.trk = a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * MB),
+                                       x.sw ? lane : kOOB) & kFull)
+                      : kFull;
+    x.mi = MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * MB),
+                                   x.sw ? lane : kOOB) & kFull)
+                  : kFull;
+    x.mo = JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * MB),
+                                  x.sw ? lane : kOOB) & kFull)
+                 : 0u;
+    x.ltr = a.transferee ? bld8(mk_rsrc(a.transferee + g0, n), o1) : 0xFFu;
+    x.c0 = bld64(mk_rsrc(a.committed + g0, n * 8), lane * 8);
+  };
+  SA ha;
+  load_a(wave, ha);
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = t * 64;
+    const uint32_t n = tile_n(a.G, t);
+    const bool live = lane < n;
+    const uint32_t o8 = lane * 8, o4 = lane * 4;
+    const SA h = ha;
+    const bool sw = live && h.sw != 0;
+    ac.add(live, (a.sw_switched ? 1 : 0) + 8);
+    ac.add(sw, (a.self_slot ? 1 : 0) + (a.tracked ? MB : 0) + (MASKED ? MB : 0) + (JOINT ? MB : 0) +
+                   (a.transferee ? 1 : 0));
+    // the early returns (:1663-1680): no Progress of its own, or a learner
+    // (tracked, in neither half); no incoming voters
+    const bool member = h.self < static_cast<uint32_t>(S) && ((h.trk >> h.self) & 1u) != 0;
+    const bool learner = member && (((h.mi | h.mo) >> h.self) & 1u) == 0;
+    uint32_t res = !sw ? QE_SW_NONE
+                       : ((!member || learner) ? QE_SW_REMOVED : (h.mi == 0 ? QE_SW_NO_VOTERS : QE_SW_PROBE));
+    const bool go = res == QE_SW_PROBE;
+    // round trip B of this tile
+    const uint32_t k8 = go ? o8 : kOOB;
+    const rsrc_t r_c = mk_rsrc(a.committed + g0, n * 8);
+    const uint64_t c0 = h.c0;
+    const uint64_t ts = bld64(mk_rsrc(a.term_start + g0, n * 8), k8);
+    const uint64_t li = bld64(mk_rsrc(a.last_index + g0, n * 8), k8);
+    const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), k8);
+    const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
+    const uint32_t vm = h.mi | h.mo;
+    uint64_t mt[S], nx[S];
+    uint32_t pw[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      const uint32_t tgt = go ? h.trk : 0u;
+      mt[s] = bld64(mk_rsrc(a.match + row, n * 8), bit_off(go ? vm : 0u, s, o8));
+      nx[s] = bld64(mk_rsrc(a.next + row, n * 8), bit_off(tgt, s, o8));
+      pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), bit_off(tgt, s, o4));
+    }
+    // round trip A of the wave's next tile, before this tile's stores
+    load_a(t + nwaves, ha);
+    uint64_t c = c0;
+    uint32_t sentm = 0, snapm = 0, ltr = h.ltr;
+    if (__builtin_amdgcn_ballot_w64(go)) {
+      ac.add(go, 24 + (a.snap_index ? 8 : 0) + 8 * popc(vm));  // term start, lastIndex,
+                                                                // firstIndex, snapshot, Match
+      // maybeCommit (raft.go:585-588, log.go:325-331): the new config's
+      // CommittedIndex and the term gate
+      uint64_t vals[S];
+#pragma unroll
+      for (int s = 0; s < S; s++) vals[s] = mt[s];
+      const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, h.mi, h.mo);
+      const bool adv = go && mci > c0 && mci >= ts && mci <= li;
+      c = adv ? mci : c0;
+      res = adv ? QE_SW_BCAST : res;
+      // bcastAppend (sendIfEmpty, not the leader) or the probe of every
+      // tracked peer (maybeSendAppend(id, false), the leader included)
+      const uint32_t selfb = member ? (1u << h.self) : 0u;
+      const uint32_t tg = go ? (adv ? (h.trk & ~selfb) : h.trk) : 0u;
+      PSend x;
+      x.F = a.F;
+      x.me = a.max_ents;
+      x.fi = fi;
+      x.li = li;
+      x.snap = sn;
+      x.lb = lane * a.FP * 4;
+      x.row = false;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+        const bool on = ((tg >> s) & 1u) != 0;
+        PR p;
+        p.match = mt[s];
+        p.next = nx[s];
+        pr_unpack(p, pw[s]);
+        p.pending = 0;
+        p.reset = 0;
+        {
+          const uint64_t rb = row * a.FP;
+          x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
+          x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+        }
+        x.count_msgs = 0;
+        x.first_index = 0;
+        x.snapped = false;
+        PRun run{0, 0, 0};
+        if (__builtin_amdgcn_ballot_w64(on)) send_burst<ACCT>(p, adv, on ? 1u : 0u, x, run, ac);
+        const uint32_t nw = pr_pack(p);
+        const bool wn = on && p.next != nx[s], ww = on && nw != pw[s], wp = on && x.snapped;
+        if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
+        if (__builtin_amdgcn_ballot_w64(ww)) bst32(nw, mk_rsrc(a.pw + row, n * 4), ww ? o4 : kOOB);
+        if (__builtin_amdgcn_ballot_w64(wp)) bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
+        ac.add(on, 12);
+        ac.add(wn, 8);
+        ac.add(on && ((nw ^ pw[s]) & ~QE_PW_RING_MASK) != 0, 4);
+        ac.add(wp, 8);
+        sentm |= (on && x.count_msgs) ? (1u << s) : 0u;
+        snapm |= (on && x.snapped) ? (1u << s) : 0u;
+      }
+      bst64(c, r_c, c != c0 ? o8 : kOOB);
+      ac.add(c != c0, 8);
+      // abortLeaderTransfer when the transferee is no voter of the new
+      // config (:1694-1697)
+      const bool abort = go && ltr < static_cast<uint32_t>(S) && ((vm >> ltr) & 1u) == 0;
+      if (abort) {
+        ltr = 0xFFu;
+        res |= QE_SW_TRANSFER_ABORTED;
+      }
+      if (a.transferee && __builtin_amdgcn_ballot_w64(abort))
+        bst8(0xFFu, mk_rsrc(a.transferee + g0, n), abort ? lane : kOOB);
+      ac.add(abort, 1);
+    }
+    bst8(res, mk_rsrc(a.sw_result + g0, n), lane);
+    if (a.sent) bst_mask<MT>(sentm, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+    if (a.snap) bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+    ac.add(live, 1 + (a.sent ? MB : 0) + (a.snap ? MB : 0));
+    if (live) {
+      const uint64_t gh = (a.goff + g0 + lane) * kPhi;
+      cnt[Q_GROUPS] += 1;
+      cnt[Q_SUM] += c;
+      cnt[Q_ADV] += c != c0;
+      cnt[Q_CSUM] += mix64(gh ^ kSwitchSalt ^ (static_cast<uint64_t>(res) << 56) ^ c) +
+                     mix64(gh ^ kSentSalt ^ (static_cast<uint64_t>(sentm) << 40) ^
+                           (static_cast<uint64_t>(snapm) << 20));
+    }
+  }
+  if (a.stats) {
+    const int idx[Q_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
+                          QE_STAT_CHECKSUM};
+    block_stats_add<Q_N, kBlock>(cnt, idx, a.stats);
+  }
+  acct_flush<ACCT>(ac, a.acct);
+}
+
 // qe_heartbeat (ABI 6): MsgBeat -> bcastHeartbeat (raft/raft.go:524-541):
 // per group the context of the newest pending ReadIndex request, per peer
 // (every tracked slot but the leader's) Commit = min(Match, committed)

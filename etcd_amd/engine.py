@@ -668,6 +668,48 @@ def propose_bytes_requested(ps, props):
     return int(acct.item())
 
 
+class Switch:
+    """One qe_switch_config call's per-group flags and outputs (qe_switch,
+    ABI 7): switched [G] (None = every group), result [G] (QE_SW_*, bit
+    QE_SW_TRANSFER_ABORTED), sent / snap masks [G]."""
+
+    def __init__(self, ps, switched=None):
+        G, dev = ps.G, ps.device
+        self.switched = switched
+        self.result = torch.zeros(G, dtype=torch.uint8, device=dev)
+        md = mask_torch_dtype(ps.S)
+        self.sent = torch.zeros(G, dtype=md, device=dev)
+        self.snap = torch.zeros(G, dtype=md, device=dev)
+        self.bytes_requested = None
+
+    def struct(self):
+        return _lib.QeSwitch(_ptr(self.switched), _ptr(self.result), _ptr(self.sent),
+                             _ptr(self.snap), _ptr(self.bytes_requested))
+
+
+def switch_config(ps, sw, stats=None):
+    """qe_switch_config: raft.switchToConfig (raft/raft.go:1651-1700) on every
+    group with sw.switched[g], the new configuration being ps's inc / out /
+    tracked masks: maybeCommit under it, then bcastAppend or the probe of
+    every peer, and abortLeaderTransfer for a transferee no longer a voter."""
+    p, q = ps.struct(), sw.struct()
+    check("qe_switch_config", _lib.lib().qe_switch_config(C.byref(p), C.byref(q), _ptr(stats),
+                                                           _stream(ps.device)))
+    return sw
+
+
+def switch_bytes_requested(ps, sw):
+    """The algorithmic bytes of one qe_switch_config launch (instrumented
+    variant, field granularity); mutates the state like switch_config."""
+    acct = torch.zeros(1, dtype=torch.int64, device=ps.device)
+    sw.bytes_requested = acct
+    try:
+        switch_config(ps, sw)
+    finally:
+        sw.bytes_requested = None
+    return int(acct.item())
+
+
 class ConfState:
     """Device-resident tracker.Config + ProgressMap key set of G groups in
     slot form (qe_conf): slot_ids ID-major [S][G], slot masks for Voters[0],

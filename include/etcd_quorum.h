@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 6  /* 6: see INTEGRATION.md "ABI 6" (changes listed there) */
+#define QE_ABI_VERSION 7  /* 7: see INTEGRATION.md "ABI 7" (changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -640,6 +640,56 @@ typedef struct qe_proposals {
  * reduceUncommittedSize on apply (:544) stays with the host, which owns the
  * applied entries.  stats: groups, commit sum, commit advanced, checksum. */
 int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, void *stream);
+
+/* ---- switchToConfig: the leader's side of an applied conf change (ABI 7) - */
+
+/* qe_switch.result & QE_SW_OUTCOME */
+#define QE_SW_NONE 0       /* switched[g] == 0: not part of this call           */
+#define QE_SW_REMOVED 1    /* the leader has no Progress any more, or is a
+                              learner: switchToConfig returns at once
+                              (raft.go:1663-1674; the leader stays leader)    */
+#define QE_SW_NO_VOTERS 2  /* Voters[0] is empty: returns (:1678-1680)         */
+#define QE_SW_BCAST 3      /* maybeCommit advanced the commit under the new
+                              config: bcastAppend (:1682-1685)                  */
+#define QE_SW_PROBE 4      /* it did not: maybeSendAppend(id, false) to every
+                              tracked peer (:1686-1692)                         */
+#define QE_SW_OUTCOME 0x0Fu
+#define QE_SW_TRANSFER_ABORTED 0x10u /* result bit: leadTransferee was not a voter
+                                        of the new config, abortLeaderTransfer
+                                        (:1694-1697)                            */
+
+typedef struct qe_switch {
+  const uint8_t *switched;       /* [G] 1: the group's configuration was just
+                                    switched (its conf change applied); NULL =
+                                    every group                               */
+  uint8_t *result;               /* [G] out QE_SW_* (| QE_SW_TRANSFER_ABORTED) */
+  void *sent;                    /* [G] out mask (may be NULL): peers sent a
+                                    MsgApp / MsgSnap                          */
+  void *snap;                    /* [G] out mask (may be NULL): a MsgSnap      */
+  uint64_t *bytes_requested;     /* measurement aid, normally NULL: adds the
+                                    algorithmic bytes (DESIGN.md §3 rules)    */
+} qe_switch;
+
+/* raft.switchToConfig (raft/raft.go:1651-1700) after the new configuration
+ * is in place -- inc_mask / out_mask / tracked of p are the new Voters[0],
+ * Voters[1] and ProgressMap keys (e.g. the qe_conf masks qe_confchange just
+ * wrote) -- for every group with switched[g]:
+ *   the leader (self_slot) has no Progress, or is a learner (tracked but in
+ *     neither half: Learners, confchange.go checkInvariants) -> QE_SW_REMOVED;
+ *   Voters[0] empty -> QE_SW_NO_VOTERS;
+ *   maybeCommit under the new JointConfig (the term gate of qe_progress_step)
+ *     advanced -> bcastAppend: sendAppend (sendIfEmpty) to every tracked slot
+ *     but the leader's; else maybeSendAppend(id, false) to every tracked slot
+ *     (prs.Visit: the leader's own included -- a no-op while its Next is
+ *     lastIndex + 1, as appendEntry keeps it);
+ *   then a lead_transferee that is not in Voters[0] | Voters[1] is cleared
+ *     (abortLeaderTransfer) and QE_SW_TRANSFER_ABORTED set.
+ * As in the reference, this maybeCommit does not release postponed ReadIndex
+ * requests (only stepLeader's MsgAppResp arm calls
+ * releasePendingReadIndexMessages, :1259-1262).  Writes committed, the
+ * peers' Next / word / PendingSnapshot / Inflights and lead_transferee.
+ * stats: groups, commit sum, commit advanced, checksum. */
+int qe_switch_config(const qe_progress *p, const qe_switch *sw, uint64_t *stats, void *stream);
 
 /* ABI 4, HOST pointers: Inflights rings between plain uint64 buffers
  * (Inflights.buffer of each peer, raft/tracker/inflights.go:25-37, peer-major

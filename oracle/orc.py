@@ -66,6 +66,8 @@ def _declare(L):
         "orc_propose_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcProps), vp]),
         "orc_checksum_prop": (u64, [u64, u32, u64, u64, u32]),
         "orc_heartbeat_batch": (None, [C.POINTER(OrcProg), vp, vp, vp]),
+        "orc_switch_config_batch": (None, [C.POINTER(OrcProg), vp, vp, vp, vp, vp, vp]),
+        "orc_checksum_switch": (u64, [u64, u32, u64, u32, u32]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
         "orc_pr_maybe_decr_to": (i32, [u32, vp, vp, u64, u64]),
@@ -405,3 +407,27 @@ def heartbeat(pb):
     s = pb.struct()
     lib().orc_heartbeat_batch(C.byref(s), P(commit), P(ctx), P(sent))
     return commit, ctx, sent
+
+
+class SwitchOut:
+    def __init__(self, pb):
+        md = mask_dtype(pb.S)
+        self.result = np.zeros(pb.G, np.uint8)
+        self.sent = np.zeros(pb.G, md)
+        self.snap = np.zeros(pb.G, md)
+        self.stats = np.zeros(NSTAT, np.uint64)
+        self.bytes = np.zeros(1, np.uint64)
+
+
+def switch_config(pb, switched=None, goff=0):
+    """raft.switchToConfig (raft/raft.go:1651-1700) on every group with
+    switched[g] (None = every group), the new configuration being pb's inc /
+    out / tracked (oracle).  pb is updated in place.  Returns SwitchOut
+    (result: 0 none, 1 removed / demoted leader, 2 no voters, 3 bcastAppend,
+    4 probe, | 0x10 transfer aborted; o.bytes[0] = the algorithmic bytes)."""
+    o = SwitchOut(pb)
+    sw = None if switched is None else np.ascontiguousarray(switched, np.uint8)
+    s = pb.struct(goff)
+    lib().orc_switch_config_batch(C.byref(s), P(sw), P(o.result), P(o.sent), P(o.snap),
+                                  P(o.stats), P(o.bytes))
+    return o

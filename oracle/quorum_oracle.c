@@ -1745,6 +1745,103 @@ void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
   if (q->bytes) *q->bytes += bytes;
 }
 
+/* raft.switchToConfig (raft/raft.go:1651-1700) on every group with
+ * switched[g] (NULL = every group), after the new configuration -- inc /
+ * out / tracked of `a` -- is in place.  result: 0 not switched, 1 the leader
+ * has no Progress or is a learner (r.isLearner, :1660; a learner is a
+ * tracked peer in neither half) -> return (:1663-1674), 2 len(cs.Voters) ==
+ * 0 -> return (:1678-1680), 3 maybeCommit -> bcastAppend (:1682-1685), 4
+ * else maybeSendAppend(id, false) for every Progress (prs.Visit, the
+ * leader's own included, :1686-1692); | 0x10 when leadTransferee is not in
+ * Voters.IDs() and abortLeaderTransfer runs (:1694-1697).  Byte accounting
+ * as orc_propose_batch's rules. */
+uint64_t orc_checksum_switch(uint64_t gid, uint32_t result, uint64_t committed, uint32_t sent,
+                             uint32_t snap) {
+  uint64_t h = gid * PHI;
+  return orc_mix64(h ^ 0x2545F4914F6CDD1Dull ^ ((uint64_t)result << 56) ^ committed) +
+         orc_mix64(h ^ 0xD1B54A32D192ED03ull ^ ((uint64_t)sent << 40) ^ ((uint64_t)snap << 20));
+}
+
+void orc_switch_config_batch(const orc_prog *a, const uint8_t *switched, uint8_t *result,
+                             void *sent, void *snap, uint64_t *stats, uint64_t *bytes) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  uint64_t st[NSTAT];
+  memset(st, 0, sizeof(st));
+  uint64_t total = 0;
+  for (uint64_t g = 0; g < a->G; g++) {
+    uint64_t B = (switched ? 1 : 0) + 8;                     /* switched, committed */
+    uint64_t cm = a->committed[g], c0 = cm;
+    uint32_t res = 0, sentm = 0, snapm = 0;
+    if (!switched || switched[g]) {
+      uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+      uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+      uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+      uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+      uint32_t lt = a->lead_transferee ? a->lead_transferee[g] : 0xFFu;
+      B += (a->self_slot ? 1 : 0) + (a->tracked ? mb : 0) + (a->inc ? mb : 0) + (a->out ? mb : 0) +
+           (a->lead_transferee ? 1 : 0);
+      int ok = self < S && ((trk >> self) & 1u);             /* pr, ok := Progress[r.id] */
+      int is_learner = ok && !(((mi | mo) >> self) & 1u);    /* pr.IsLearner */
+      if (!ok || is_learner) {
+        res = 1;
+      } else if (mi == 0) {
+        res = 2;
+      } else {
+        orc_gctx c;
+        c.a = a;
+        c.m = NULL;
+        c.g = g;
+        c.fi = a->first_index[g];
+        c.li = a->last_index[g];
+        c.snap = a->snap_index ? a->snap_index[g] : c.fi - 1;
+        c.me = a->max_ents;
+        c.sent = c.snapm = 0;
+        B += 24 + (a->snap_index ? 8 : 0) + 8 * (uint64_t)popc(mi | mo); /* log model, Match */
+        uint64_t vals[16];
+        for (uint32_t t = 0; t < S; t++) vals[t] = a->match[t * a->stride + g];
+        uint64_t mci = orc_joint_committed(S, mi, mo, vals);
+        int adv = orc_maybe_commit(mci, &cm, a->term_start[g], c.li);
+        res = adv ? 3 : 4;
+        for (uint32_t t = 0; t < S; t++) {
+          if (!((trk >> t) & 1u)) continue;
+          if (adv && t == self) continue;                    /* bcastAppend skips r.id */
+          orc_pr p;
+          pr_load2(&p, a, t, g);
+          uint64_t nx0 = p.next;
+          uint32_t pw0 = pr_word(&p);
+          if (bytes) p.acct = &B;
+          send_append(&c, &p, t, adv);                       /* sendAppend / maybeSendAppend(id, false) */
+          p.acct = NULL;
+          B += 12 + (p.next != nx0 ? 8 : 0) + (pr_word(&p) != pw0 ? 4 : 0) + (p.reset ? 8 : 0);
+          pr_store2(&p, a, t, g);
+        }
+        a->committed[g] = cm;
+        B += cm != c0 ? 8 : 0;
+        sentm = c.sent;
+        snapm = c.snapm;
+        if (lt < S && !(((mi | mo) >> lt) & 1u)) {           /* leadTransferee not a voter */
+          a->lead_transferee[g] = 0xFF;                      /* abortLeaderTransfer */
+          res |= 0x10;
+          B += 1;
+        }
+      }
+    }
+    result[g] = (uint8_t)res;
+    if (sent) st_mask(sent, mb, g, sentm);
+    if (snap) st_mask(snap, mb, g, snapm);
+    B += 1 + (sent ? mb : 0) + (snap ? mb : 0);
+    total += B;
+    st[ST_GROUPS] += 1;
+    st[ST_COMMIT_ADVANCED] += cm != c0;
+    st[ST_COMMIT_SUM] += cm;
+    st[ST_CHECKSUM] += orc_checksum_switch(a->goff + g, res, cm, sentm, snapm);
+  }
+  if (stats)
+    for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+  if (bytes) *bytes += total;
+}
+
 /* MsgBeat on each group's leader (stepLeader, raft/raft.go:991-993):
  * bcastHeartbeat (:524-541) -> sendHeartbeat (:494-510) to every Progress
  * but the leader's, Commit = min(Match, committed), Context =

@@ -481,6 +481,104 @@ def add_node_check_quorum(be):
     assert qa == 0, (qa, ra)  # steps down
 
 
+SW_REMOVED, SW_BCAST, SW_PROBE, SW_ABORTED = 1, 3, 4, 0x10  # QE_SW_*
+
+
+def commit_after_remove_node(be):
+    """TestCommitAfterRemoveNode (raft/raft_test.go:3370-3431): peers {1, 2},
+    node 1 made leader by becomeCandidate + becomeLeader (term 1; reset()
+    leaves node 2 at Match 0, Next 1, StateProbe; the leader's empty entry
+    at 1, no bcast).  A proposal of ConfChange{RemoveNode 2} appends 2 (its
+    bcastAppend probes node 2), a normal entry "hello" appends 3 (node 2 is
+    paused: nothing sent); nothing is committed.  Node 2's MsgAppResp for 2
+    commits 1 and 2 (the empty entry and the conf change).  Applying the
+    conf change (Voters {1}, node 2's Progress removed) and switchToConfig:
+    maybeCommit under the new quorum commits 3 -- "This reduces quorum
+    requirements so the pending command can now commit" -- and bcastAppend
+    has nobody to send to."""
+    S = 2
+    sc = {"name": "", "S": S, "self": 0, "max_ents": 0,
+          "log": {"runs": [[0, 0], [1, 1]], "committed": 0, "term_start": 1, "first_index": 1,
+                  "last_index": 1},
+          "peers": [_peer(1, 2, REPLICATE), _peer(0, 1, 0)]}
+    be.load(sc, initial_arrays(sc), inc=0b11, tracked=0b11)
+    be.pci, be.applied = 0, 0  # becomeLeader: pendingConfIndex = lastIndex before the empty entry
+    out = be.propose(1, cc=[(0, False, 16)])  # EntryConfChange (RemoveNode 2) at 2
+    assert out["result"] == 1 and out["cc_refused"] == 0 and bits(out["sent"]) == [1], out
+    assert be.committed() == 0
+    cc_index = be.last_index()
+    assert cc_index == 2
+    out = be.propose(1, payload=5)  # "hello" at 3; node 2 is paused (ProbeSent)
+    assert out["result"] == 1 and out["sent"] == 0, out
+    z = np.zeros(S, np.uint64)
+    be.step(np.array([0, 1], np.uint8), np.array([0, cc_index], np.uint64), z, z)
+    assert be.committed() == 2  # ents: the empty entry and the conf change
+    be.set_config(tracked=0b01, inc=0b01)  # applyConfChange: Voters {1}
+    out = be.switch_config()
+    assert out["result"] == SW_BCAST and out["sent"] == 0, out
+    assert be.committed() == 3  # "hello" commits under the new quorum
+
+
+def leader_transfer_remove_node(be):
+    """TestLeaderTransferRemoveNode (raft/raft_test.go:3681-3698): node 3 is
+    caught up, so the transfer sends MsgTimeoutNow (ignored by the network)
+    and leadTransferee = 3; then applyConfChange(RemoveNode 3):
+    switchToConfig finds no commit to make (the probe of every peer sends
+    nothing: all caught up) and aborts the transfer, since 3 is no voter
+    (raft.go:1694-1697) -- checkLeaderTransferState(lead, StateLeader, 1)."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc), inc=0b111, tracked=0b111)
+    out = _transfer(be, S, 2)
+    assert bits(out["timeout_now"]) == [2] and be.transferee() == 2
+    be.set_config(tracked=0b011, inc=0b011)
+    out = be.switch_config()
+    assert out["result"] == SW_PROBE | SW_ABORTED and out["sent"] == 0, out
+    assert be.transferee() == 0xFF and be.committed() == 1
+
+
+def leader_transfer_demote_node(be):
+    """TestLeaderTransferDemoteNode (raft/raft_test.go:3700-3730): the
+    transfer to 3 pending, ConfChangeV2{RemoveNode 3, AddLearnerNode 3}
+    enters the joint config (1 2)&&(1 2 3) with 3 in LearnersNext: 3 is
+    still in Voters.IDs(), so the transfer stays; the empty ConfChangeV2
+    leaves it -- 3 becomes a learner (tracked, in neither half) -- and the
+    transfer is aborted."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc), inc=0b111, tracked=0b111, out=0)
+    _transfer(be, S, 2)
+    assert be.transferee() == 2
+    be.set_config(tracked=0b111, inc=0b011)  # EnterJoint: Voters[0] {1, 2}
+    be.set_outgoing(0b111)                   # Voters[1] {1, 2, 3}
+    out = be.switch_config()
+    assert out["result"] == SW_PROBE and be.transferee() == 2, out
+    be.set_outgoing(0)                       # LeaveJoint: 3 a learner
+    out = be.switch_config()
+    assert out["result"] == SW_PROBE | SW_ABORTED and be.transferee() == 0xFF, out
+
+
+def switch_removed_or_demoted_leader(be):
+    """switchToConfig returns at once for a leader that was removed
+    (raft.go:1663-1674, the branch confchange_v1_remove_leader.txt takes) or
+    demoted to a learner (the same branch, "we handle them the same way"):
+    no commit, no sends, a pending transfer kept.  Derived: the reference
+    has no test of the demotion ("It is untested at the time of writing")."""
+    S = 3
+    sc = _leader_after_hup(S)
+    sc["peers"][1]["match"] = 2  # node 2 ahead of the commit
+    sc["log"]["last_index"] = 2
+    be.load(sc, initial_arrays(sc), inc=0b111, tracked=0b111)
+    _transfer(be, S, 1)
+    be.set_config(tracked=0b110, inc=0b110)  # node 1 removed
+    out = be.switch_config()
+    assert out["result"] == SW_REMOVED and out["sent"] == 0 and be.committed() == 1, out
+    assert be.transferee() == 1
+    be.set_config(tracked=0b111, inc=0b110)  # node 1 a learner
+    out = be.switch_config()
+    assert out["result"] == SW_REMOVED and out["sent"] == 0 and be.committed() == 1, out
+
+
 SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lease,
              raft_frees_read_only_mem, read_only_for_new_leader,
              postponed_read_commit_advances_twice, two_reads_in_flight,
@@ -490,7 +588,9 @@ SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lea
              leader_transfer_to_slow_follower, leader_transfer_to_self,
              leader_transfer_to_non_existing_node, leader_transfer_second_to_another_node,
              leader_transfer_second_to_same_node, leader_transfer_back,
-             leader_transfer_learner_ignored]
+             leader_transfer_learner_ignored, commit_after_remove_node,
+             leader_transfer_remove_node, leader_transfer_demote_node,
+             switch_removed_or_demoted_leader]
 
 
 class OracleRoundBackend:
@@ -558,6 +658,11 @@ class OracleRoundBackend:
         change; the Progress of a slot that stays keeps its state)."""
         self.pb.tracked[0] = tracked
         self.pb.inc[0] = inc
+
+    def switch_config(self):
+        """switchToConfig on the loaded group (orc_switch_config_batch)."""
+        o = self.orc.switch_config(self.pb)
+        return {"result": int(o.result[0]), "sent": int(o.sent[0]), "snap": int(o.snap[0])}
 
     def send(self, want, sei):
         w = np.array([want], self.orc.mask_dtype(self.sc["S"]))

@@ -30,7 +30,7 @@ def test_header_declares_expected_surface():
               "qe_comm_unique_id", "qe_comm_destroy", "qe_comm_id_bytes", "qe_check_quorum",
               "qe_pack_order", "qe_progress_step", "qe_progress_send", "qe_confchange",
               "qe_read_index", "qe_propose", "qe_comm_init_timeout", "qe_comm_abort",
-              "qe_heartbeat"]:
+              "qe_heartbeat", "qe_switch_config"]:
         assert f in fns
 
 
@@ -72,6 +72,7 @@ int main(void) {
   F(qe_conf_changes, new_progress)
   Z(qe_proposals) F(qe_proposals, max_cc) F(qe_proposals, cc_stride) F(qe_proposals, cc_size)
   F(qe_proposals, max_uncommitted) F(qe_proposals, cc_refused) F(qe_proposals, bytes_requested)
+  Z(qe_switch) F(qe_switch, result) F(qe_switch, snap) F(qe_switch, bytes_requested)
   return 0;
 }
 """
@@ -82,7 +83,8 @@ CTYPES = {"qe_groups": _lib.QeGroups, "qe_outputs": _lib.QeOutputs,
           "qe_election_params": _lib.QeElectionParams, "qe_gen_params": _lib.QeGenParams,
           "qe_confstate_csr": _lib.QeConfStateCSR, "qe_progress": _lib.QeProgress,
           "qe_peer_msgs": _lib.QePeerMsgs, "qe_conf": _lib.QeConf,
-          "qe_conf_changes": _lib.QeConfChanges, "qe_proposals": _lib.QeProposals}
+          "qe_conf_changes": _lib.QeConfChanges, "qe_proposals": _lib.QeProposals,
+          "qe_switch": _lib.QeSwitch}
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -101,7 +103,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 6
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 7
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0

@@ -506,6 +506,11 @@ class GpuBackend:
     def transferee(self):
         return int(self.ps.lead_transferee[0])
 
+    def switch_config(self):
+        """qe_switch_config on the one group."""
+        sw = self.eng.switch_config(self.ps, self.eng.Switch(self.ps))
+        return {"result": int(sw.result[0]), "sent": int(sw.sent[0]), "snap": int(sw.snap[0])}
+
     def send(self, want, sei):
         dt = torch.uint8 if self.sc["S"] <= 8 else torch.int16
         w = torch.tensor([want], dtype=dt, device=DEV)

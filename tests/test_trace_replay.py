@@ -149,3 +149,14 @@ def test_trace_replay_detects_a_changed_value(orc, monkeypatch, what):
     _mutated(monkeypatch, name, edit)  # (LookupError, not a pass, if the value moved)
     with pytest.raises(AssertionError):
         trace(lambda node, S: Leader(OracleRoundBackend(orc), node, S), oracle_elector(orc))
+
+
+@pytest.mark.parametrize("trace", TRACES, ids=lambda f: f.__name__)
+def test_trace_replay_in_tiles_on_oracle(trace):
+    """The tile replay of tests/test_gpu_trace_tiles.py with the oracle alone:
+    the trace's group at lane 37 of a 192-group batch of random groups with
+    F = 8 (the GPU test compares the engine with this, group by group)."""
+    from tests.test_gpu_trace_tiles import TileBackend
+    checked = trace(lambda node, S: Leader(TileBackend(None, 37, seed=5), node, S),
+                    oracle_elector(__import__("oracle.orc", fromlist=["orc"])))
+    assert checked["rounds"] > 0 and checked["sends"] > 0

@@ -61,6 +61,7 @@ from tests.progress_scenarios import initial_arrays
 
 STATE = {"StateProbe": 0, "StateReplicate": 1, "StateSnapshot": 2}
 STATE_NAME = {v: k for k, v in STATE.items()}
+SW_REMOVED, SW_BCAST, SW_PROBE = 1, 3, 4  # QE_SW_* outcomes of qe_switch_config
 # MaxInflightMsgs of the interaction env is math.MaxInt32 and MaxSizePerMsg
 # math.MaxUint64 (raft/rafttest/interaction_env.go:96-97): no trace holds more
 # than a few MsgApps in flight, so the slot model's 255 never binds
@@ -169,9 +170,8 @@ class Leader:
         self.bcast()
 
     def bcast(self, sei=1):
-        """bcastAppend: sendAppend to every peer but the leader (sei = 0:
-        maybeSendAppend(id, false) to every peer, switchToConfig's probe of
-        a new config, raft.go:1688-1692)."""
+        """bcastAppend: sendAppend to every peer but the leader (stepCandidate
+        after a won election, raft.go:1405-1407)."""
         nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
         want = sum(1 << s for s in range(self.S) if s != self.self)
         out = self.be.send(want, sei)
@@ -180,6 +180,24 @@ class Leader:
                 snap = bool((out["snap"] >> s) & 1)
                 idx = self.be.peer(s)["pending"] if snap else nxt[s] - 1
                 self.pending.setdefault(s, []).append((idx, snap, self.be.last_index()))
+
+    def switch(self, want):
+        """switchToConfig (raft.go:1651-1700) after the host applied a conf
+        change, through the engine's qe_switch_config: the removed-leader
+        return, maybeCommit under the new config and bcastAppend, or the
+        probe of every peer (maybeSendAppend(id, false)), the transfer
+        abort.  `want`: the QE_SW_* outcome the trace implies (the Ready
+        after it checks the sends and the commit)."""
+        nxt = {s: self.be.peer(s)["next"] for s in range(self.S)}
+        out = self.be.switch_config()
+        assert out["result"] == want, ("switchToConfig", out, want)
+        for s in range(self.S):
+            if (out["sent"] >> s) & 1:
+                snap = bool((out["snap"] >> s) & 1)
+                idx = self.be.peer(s)["pending"] if snap else nxt[s] - 1
+                self.pending.setdefault(s, []).append((idx, snap, self.be.last_index()))
+        self.checked["switches"] = self.checked.get("switches", 0) + 1
+        return out
 
     # -- replay --------------------------------------------------------------
     def recv(self, block):
@@ -472,11 +490,11 @@ def _confchange_add_single(name):
         state is restated as it is after that Ready applies 4: node 2 added
         by initProgress (raft/confchange/confchange.go:259-274: Match 0,
         Next = lastIndex 4, RecentActive); the leader's own Progress at
-        match 4.  switchToConfig then runs (raft.go:1682-1692): maybeCommit
-        is false (4 is on node 1 only, and {{1, 2}} needs both), so every peer
-        gets maybeSendAppend(id, false) -- issued right after the Ready that
-        prints the switch.  The snapshot a compacted log sends is the
-        applied index 4 (the trace's MsgSnap)."""
+        match 4.  switchToConfig then runs through qe_switch_config right
+        after the Ready that prints the switch: maybeCommit under {{1, 2}}
+        finds nothing to commit, so every peer gets maybeSendAppend(id,
+        false) (raft.go:1682-1692).  The snapshot a compacted log sends is
+        the applied index 4 (the trace's MsgSnap)."""
         cmds = traces()[name]["commands"]
         st = command(cmds, "stabilize")
         L = leader_factory(1, 2)
@@ -489,7 +507,7 @@ def _confchange_add_single(name):
 
         def after(block):
             if any("switched to configuration voters=(1 2)" in x for x in block["debug"]):
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 switched.append(block)
 
         checked = L.replay(cmds, st["line"], after_ready=after)
@@ -525,13 +543,13 @@ def confchange_v2_add_double_implicit(leader_factory, elector):
     def after(block):
         for x in block["debug"]:
             if "switched to configuration voters=(1 2)&&(1) autoleave" in x:
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 out = L.be.propose(1, append_only=True)  # the auto-leave entry
                 assert out["result"] == 1 and L.be.last_index() == 5, out
                 seen.append("enter")
             elif x.endswith("switched to configuration voters=(1 2)"):
                 L.be.set_outgoing(0)
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 seen.append("leave")
 
     checked = L.replay(cmds, st["line"], after_ready=after)
@@ -564,6 +582,7 @@ def confchange_v1_remove_leader(leader_factory, elector):
     def after(block):
         if any(x.endswith("switched to configuration voters=(2 3)") for x in block["debug"]):
             L.be.set_config(tracked=0b110, inc=0b110)
+            L.switch(SW_REMOVED)  # the removed leader returns at once (raft.go:1663-1674)
             seen.append(block)
 
     checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
@@ -594,12 +613,12 @@ def confchange_v2_add_single_explicit(leader_factory, elector):
     def after(block):
         for x in block["debug"]:
             if x.endswith("switched to configuration voters=(1 2)&&(1)"):
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 seen.append("enter")
             elif x.endswith("switched to configuration voters=(1 2)"):
                 L.be.set_outgoing(0)
                 L.be.applied = 6
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 seen.append("leave")
 
     checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
@@ -641,28 +660,28 @@ def confchange_v2_add_double_auto(leader_factory, elector):
     def after(block):
         for x in block["debug"]:
             if x.endswith("switched to configuration voters=(1 2 3)&&(1) autoleave"):
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 auto_leave()  # at 5
                 seen.append(x)
             elif x.endswith("switched to configuration voters=(1 2 3)"):
                 L.be.set_outgoing(0)
                 L.be.applied = 5
                 L.be.set_snapshot(5)
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 seen.append(x)
             elif x.endswith("switched to configuration voters=(1)&&(1 2 3) autoleave"):
                 L.be.set_config(tracked=0b111, inc=0b001)
                 L.be.set_outgoing(0b111)
                 L.be.applied = 6
                 L.be.set_snapshot(6)
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 auto_leave()  # at 9
                 seen.append(x)
             elif x.endswith("switched to configuration voters=(1)"):
                 L.be.set_config(tracked=0b001, inc=0b001)
                 L.be.set_outgoing(0)
                 L.be.applied = 9
-                L.bcast(sei=0)
+                L.switch(SW_PROBE)
                 seen.append(x)
 
     checked = L.replay(cmds, st["line"], after_ready=after, proposals=True)
