@@ -1,0 +1,25 @@
+#!/bin/bash
+# r06: the new GPU tests first (qe_switch_config, the tile-embedded trace
+# replays), then the whole GPU suite, then the switch_config workload's bench
+# line and its per-workload rocprofv3 passes.  Logs under gpurun_out/$TAG/.
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
+T=${TAG:-r06a}; O=gpurun_out/$T; mkdir -p "$O"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_switch.py tests/test_gpu_trace_tiles.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/new_tests.log" 2>&1 || { echo "new tests failed"; tail -40 "$O/new_tests.log"; exit 2; }
+tail -1 "$O/new_tests.log"
+if [ "${FULL:-1}" = 1 ]; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
+    --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$O/gpu_tests.log"; exit 3; }
+  tail -1 "$O/gpu_tests.log"
+fi
+for W in ${WLS:-switch_config}; do
+  timeout -k 10 300 python -u bench.py --workload $W --no-aux --no-cpu-baseline --steps 20 --warmup 5 > "$O/bench_$W.log" 2>&1 || { echo "bench $W failed"; tail -20 "$O/bench_$W.log"; exit 4; }
+  tail -1 "$O/bench_$W.log" | python3 -c "
+import json,sys
+d=json.loads(sys.stdin.read())
+print('$W', d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['roofline']['bytes_per_unit'])"
+done
+if [ "${PROF:-1}" = 1 ]; then
+  WLS="${WLS:-switch_config}" bash scripts/gpu_profile_workloads.sh || exit 5
+fi
+echo session done

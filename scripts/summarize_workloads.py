@@ -61,6 +61,7 @@ DOMINANT = {
     "progress_send": ("void qe::k_progress_send<5,", 2),
     "propose": ("void qe::k_propose<5, unsigned char, false, false, false>", 2),
     "heartbeat": ("void qe::k_heartbeat<5, unsigned char>", 2),
+    "switch_config": ("void qe::k_switch_config<5, unsigned char, true, false, false>", 2),
     "progress_step_n7": ("void qe::k_progress_step<7, unsigned char, false, false, 4, false,", 2),
     "progress_step_joint": ("void qe::k_progress_step<6, unsigned char, true, true, 4, false,", 2),
 }
