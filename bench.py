@@ -148,6 +148,7 @@ def maybe_spawn(args):
 
 
 COMM_INIT_TIMEOUT_MS = 120_000  # qe_comm_init_timeout: peers that never join
+STATS_WAIT_S = 60.0  # bound on one engine all-reduce's completion (its own stream)
 
 
 class Dist:
@@ -164,7 +165,15 @@ class Dist:
     over the torch group, so all of them use qe_allreduce_stats or all of
     them use torch's all_reduce -- never a mix, which would leave the ranks
     in different collectives (a hang).  A fallback is reported in the JSON
-    line and fails the run unless --allow-stats-fallback is given."""
+    line and fails the run unless --allow-stats-fallback is given.
+
+    Every agreement runs on a host-side gloo group (`hgroup`), never on the
+    device: a torch collective on the launch stream could queue behind an
+    engine all-reduce that waits for a peer which never enqueued it.  The
+    engine all-reduce itself runs on a stream of its own and its completion
+    is awaited with a deadline; a failure anywhere aborts the engine
+    communicator on every rank before any fallback runs (on the host
+    group), so no rank can block behind the aborted collective."""
 
     def __init__(self, backend=None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,15 +188,18 @@ class Dist:
         else:  # CPU tests of the rank logic (gloo)
             self.dev = torch.device("cpu")
         self.comm = None
+        self.hgroup = None          # host-side (gloo) group for every agreement
         self.stats_path = None      # what the stats all-reduce went through
         self.stats_fallback = None  # why the engine's collective is not used (all ranks)
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)
+                self.hgroup = dist.new_group(backend="gloo")
                 self._select_stats_path()
             else:
                 dist.init_process_group(self.backend)
+                self.hgroup = dist.group.WORLD
 
     def _coll(self, t):
         return t if self.backend == "nccl" else t.cpu()
@@ -207,18 +219,19 @@ class Dist:
         return float(t.item())
 
     def all_ok(self, ok):
-        """True iff `ok` holds on every rank (MIN over the torch group), so
-        every rank takes the same branch after it."""
+        """True iff `ok` holds on every rank (MIN over the host-side gloo
+        group: nothing is queued on the device), so every rank takes the
+        same branch after it."""
         if self.world == 1:
             return bool(ok)
-        t = self._coll(torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.dev))
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.hgroup)
         return int(t.item()) == 1
 
     def _errors(self, err):
-        """Every rank's error text (all_gather_object), for the JSON line."""
+        """Every rank's error text (all_gather_object on the host group)."""
         errs = [None] * self.world
-        dist.all_gather_object(errs, err)
+        dist.all_gather_object(errs, err, group=self.hgroup)
         return "; ".join(f"rank {r}: {e}" for r, e in enumerate(errs) if e)
 
     def _try_engine_comm(self):
@@ -235,7 +248,7 @@ class Dist:
                 payload = [bytes(idb), ""]
             except Exception as e:  # noqa: BLE001 -- every rank learns it below
                 payload = [None, f"qe_comm_unique_id: {e}"]
-        dist.broadcast_object_list(payload, src=0)
+        dist.broadcast_object_list(payload, src=0, group=self.hgroup)
         if payload[0] is None:
             return None, payload[1] if self.rank == 0 else ""
         idb = (C.c_uint8 * len(payload[0])).from_buffer_copy(payload[0])
@@ -258,13 +271,46 @@ class Dist:
         self.stats_fallback = self._errors(err) or "engine communicator unavailable"
         self.stats_path = f"torch.distributed all_reduce (FALLBACK: {self.stats_fallback})"
 
-    def _torch_sum(self, folded):
-        if self.backend == "nccl":
+    def _torch_sum(self, folded, host=False):
+        """torch's all-reduce of the counters: RCCL on the device, or (host
+        = True, the fallback after an engine failure) gloo on a host copy."""
+        if self.backend == "nccl" and not host:
             dist.all_reduce(folded, op=dist.ReduceOp.SUM)
             return folded
-        t = self._coll(folded)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t = folded.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.hgroup)
         return t.to(self.dev)
+
+    def _engine_sum(self, folded):
+        """qe_allreduce_stats on a stream of its own (after the launch
+        stream's work on `folded`) -> error text ("" = enqueued)."""
+        import ctypes as C
+        gpu = self.dev.type == "cuda"  # (CPU: the rank-logic tests' fake library)
+        if gpu:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(self.dev)
+            self._side.wait_stream(torch.cuda.current_stream(self.dev))
+        self._done = None
+        try:
+            engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
+                engine._ptr(folded), folded.numel(), self.comm,
+                C.c_void_p(self._side.cuda_stream) if gpu else None))
+        except Exception as e:  # noqa: BLE001
+            return f"qe_allreduce_stats: {e}"
+        if gpu:
+            self._done = torch.cuda.Event()
+            self._done.record(self._side)
+        return ""
+
+    def _engine_wait(self):
+        """Wait for the engine all-reduce with a deadline (polling its event,
+        never blocking on it) -> error text."""
+        t0 = time.monotonic()
+        while self._done is not None and not self._done.query():
+            if time.monotonic() - t0 > STATS_WAIT_S:
+                return f"qe_allreduce_stats did not complete in {STATS_WAIT_S:.0f} s"
+            time.sleep(0.001)
+        return ""
 
     def sum_stats(self, folded):
         """All-reduce (sum) of the uint64 statistics vector: RCCL over xGMI
@@ -281,19 +327,22 @@ class Dist:
                 self.stats_path = f"torch.distributed {self.backend} (rehearsal)"
             return self._torch_sum(folded)
         keep = folded.clone()
-        err = ""
-        try:
-            engine.check("qe_allreduce_stats", engine._lib.lib().qe_allreduce_stats(
-                engine._ptr(folded), folded.numel(), self.comm, engine._stream(self.dev)))
-        except Exception as e:  # noqa: BLE001
-            err = f"qe_allreduce_stats: {e}"
+        err = self._engine_sum(folded)
+        # agreement 1 (host): every rank enqueued it; agreement 2: every rank
+        # saw it complete in time.  Either failing aborts the communicator on
+        # every rank (a rank whose collective waits for a peer that never
+        # enqueued it is released), and the counters go over the host group.
         if self.all_ok(not err):
-            return folded
+            err = self._engine_wait()
+            if self.all_ok(not err):
+                if self._done is not None:
+                    torch.cuda.current_stream(self.dev).wait_stream(self._side)
+                return folded
         engine._lib.lib().qe_comm_abort(self.comm)
         self.comm = None
         self.stats_fallback = self._errors(err) or "qe_allreduce_stats failed on a rank"
-        self.stats_path = f"torch.distributed all_reduce (FALLBACK: {self.stats_fallback})"
-        return self._torch_sum(keep)
+        self.stats_path = f"torch.distributed gloo all_reduce (FALLBACK: {self.stats_fallback})"
+        return self._torch_sum(keep, host=True)
 
     def close(self):
         if self.comm is not None:

@@ -136,6 +136,7 @@ QE_SW_OUTCOME, QE_SW_TRANSFER_ABORTED = 0x0F, 0x10
 
 QE_PROP_NONE, QE_PROP_OK, QE_PROP_DROPPED_NOT_MEMBER, QE_PROP_DROPPED_TRANSFER, \
     QE_PROP_DROPPED_SIZE = 0, 1, 2, 3, 4
+QE_PROP_BAD_CC = 5  # ABI 7: more conf-change entries than max_cc
 QE_PROP_MAX_CC = 8
 QE_PROP_APPEND_ONLY = 1
 

@@ -468,6 +468,7 @@ int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, 
   if (prop->max_cc > QE_PROP_MAX_CC) return QE_ERANGE;
   if (p->num_groups == 0) return QE_OK;
   if (!prop->num_entries || !prop->result) return QE_EINVAL;
+  if (!p->self_slot) return QE_EINVAL;  // MsgProp is handled by the leader: its slot is needed
   if (prop->max_cc && (!prop->cc_count || !prop->cc_pos || !prop->cc_leave || !prop->cc_size ||
                        !prop->applied || !prop->pending_conf_index ||
                        prop->cc_stride < p->num_groups))

@@ -30,6 +30,25 @@ static int comm_status(ncclResult_t r) {
   return QE_ECOMM;
 }
 
+// Bound on waiting for a non-blocking communicator's pending operation (an
+// enqueue, a finalize) to leave ncclInProgress.  The wait sleeps between
+// polls, so a stuck peer costs a thread sleeping, not a spinning core.
+constexpr long long kCommWaitMs = 30000;
+
+// Polls ncclCommGetAsyncError until `r` is no longer ncclInProgress or
+// kCommWaitMs passed (then ncclInProgress is returned: the caller aborts).
+static ncclResult_t comm_wait(ncclComm_t c, ncclResult_t r) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
+    if (ms >= kCommWaitMs) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return ncclInternalError;
+  }
+  return r;
+}
+
 extern "C" {
 
 size_t qe_comm_id_bytes(void) { return sizeof(ncclUniqueId); }
@@ -96,7 +115,20 @@ int qe_comm_abort(void *comm) {
 
 int qe_comm_destroy(void *comm) {
   if (!comm) return QE_EINVAL;
-  return comm_status(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
+  const ncclComm_t c = static_cast<ncclComm_t>(comm);
+  // flush the communicator's operations first: on a non-blocking one
+  // (qe_comm_init_timeout) the finalize returns ncclInProgress and is
+  // polled, bounded; one that does not complete is aborted instead
+  const ncclResult_t r = comm_wait(c, ncclCommFinalize(c));
+  if (r != ncclSuccess) {
+    ncclCommAbort(c);
+    if (r == ncclInProgress) {
+      qe::set_error("qe_comm_destroy: the communicator did not finalize in time (aborted)");
+      return QE_ECOMM;
+    }
+    return comm_status(r);
+  }
+  return comm_status(ncclCommDestroy(c));
 }
 
 int qe_allreduce_stats(uint64_t *stats, uint32_t n, void *comm, void *stream) {
@@ -105,9 +137,14 @@ int qe_allreduce_stats(uint64_t *stats, uint32_t n, void *comm, void *stream) {
   ncclResult_t r = ncclAllReduce(stats, stats, n, ncclUint64, ncclSum, c,
                                  static_cast<hipStream_t>(stream));
   // a non-blocking communicator (qe_comm_init_timeout) may return before the
-  // collective is enqueued: wait for the enqueue (not for the sum itself)
-  while (r == ncclInProgress)
-    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) break;
+  // collective is enqueued: wait for the enqueue (not for the sum itself),
+  // bounded -- an enqueue still pending after kCommWaitMs is an error the
+  // caller answers with qe_comm_abort
+  r = comm_wait(c, r);
+  if (r == ncclInProgress) {
+    qe::set_error("qe_allreduce_stats: the collective was not enqueued in time");
+    return QE_ECOMM;
+  }
   return comm_status(r);
 }
 

@@ -1524,8 +1524,12 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
       // conf-change entries (:1034-1072): refused ones become empty
       // EntryNormal entries (no payload), an accepted one sets
       // pendingConfIndex to its index
-      uint32_t ncc = go ? ncc_ld : 0u;
-      ncc = ncc < a.max_cc ? ncc : a.max_cc;
+      // a proposal listing more conf-change entries than max_cc is refused
+      // whole (QE_PROP_BAD_CC: nothing appended, no state changes), never
+      // clamped silently
+      const bool bad_cc = go && ncc_ld > a.max_cc;
+      res = bad_cc ? QE_PROP_BAD_CC : res;
+      const uint32_t ncc = (go && !bad_cc) ? ncc_ld : 0u;
       bool out_counted = false;
       if (__builtin_amdgcn_ballot_w64(ncc > 0)) {
         const bool cl = ncc > 0;
@@ -1560,10 +1564,10 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
       }
       // appendEntry -> increaseUncommittedSize (:1761-1779)
       const rsrc_t r_unc = opt_rsrc(a.unc, g0, n);
-      ac.add(go && a.unc, 8);
-      const bool drop = go && us > 0 && sz > 0 && us + sz > maxu;
+      ac.add(go && !bad_cc && a.unc, 8);
+      const bool drop = go && !bad_cc && us > 0 && sz > 0 && us + sz > maxu;
       res = drop ? QE_PROP_DROPPED_SIZE : res;
-      const bool ok = go && !drop;
+      const bool ok = go && !bad_cc && !drop;
       bst64(us + sz, r_unc, (ok && sz) ? o8 : kOOB);
       ac.add(ok && a.unc && sz, 8);
       const uint64_t li2 = li + ne;  // raftLog.append

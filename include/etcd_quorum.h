@@ -576,6 +576,9 @@ int qe_progress_send(const qe_progress *p, const void *want, uint32_t send_if_em
                                          in progress (raft.go:1029-1032)       */
 #define QE_PROP_DROPPED_SIZE 4        /* ErrProposalDropped: the uncommitted
                                          size limit (raft.go:627-633, 1761-1779) */
+#define QE_PROP_BAD_CC 5              /* ABI 7: cc_count[g] > max_cc -- refused
+                                         whole, nothing changes (an input error
+                                         reported per group, never clamped)    */
 #define QE_PROP_MAX_CC 8              /* conf-change entries per proposal      */
 /* qe_proposals.flags: appendEntry alone, as the reference calls it outside
  * MsgProp (the auto-leave entry of advance, raft.go:555-569; tests'
@@ -593,7 +596,8 @@ typedef struct qe_proposals {
                                     <= QE_PROP_MAX_CC (0: no conf changes)  */
   uint32_t flags;                /* QE_PROP_APPEND_ONLY or 0                  */
   uint64_t cc_stride;            /* >= num_groups                            */
-  const uint8_t *cc_count;       /* [G] conf-change entries of the proposal  */
+  const uint8_t *cc_count;       /* [G] conf-change entries of the proposal
+                                    (> max_cc: QE_PROP_BAD_CC)              */
   const uint32_t *cc_pos;        /* [max_cc][cc_stride] position in m.Entries,
                                     ascending, < num_entries                */
   const uint8_t *cc_leave;       /* [max_cc][cc_stride] 1: a ConfChangeV2
@@ -618,7 +622,8 @@ typedef struct qe_proposals {
 } qe_proposals;
 
 /* stepLeader's MsgProp arm (raft/raft.go:1019-1076) for every group with
- * num_entries > 0, on the leader-side state p:
+ * num_entries > 0, on the leader-side state p (p->self_slot is required:
+ * MsgProp needs the leader's own id, QE_EINVAL without it):
  *   the leader has no Progress of its own (self_slot untracked) -> dropped;
  *   a leadership transfer is in progress (lead_transferee < S) -> dropped;
  *   each conf-change entry in order: refused (replaced by an empty
@@ -932,6 +937,8 @@ int qe_comm_init(void **comm, uint32_t nranks, uint32_t rank, const void *id,
  * every rank takes (bench.py Dist._select_stats_path). */
 int qe_comm_init_timeout(void **comm, uint32_t nranks, uint32_t rank, const void *id,
                          int device, uint32_t timeout_ms);
+/* ncclCommFinalize (polled, at most 30 s, on a non-blocking communicator;
+ * aborted when it does not complete: QE_ECOMM) then ncclCommDestroy. */
 int qe_comm_destroy(void *comm);
 /* ncclCommAbort (ABI 6): frees the communicator without waiting for its
  * outstanding collectives -- the way out when a peer failed mid-run. */
@@ -940,7 +947,12 @@ int qe_comm_abort(void *comm);
 /* stats[0..n) (DEVICE, n <= QE_STATS_WORDS; normally the QE_STATS_COUNTERS
  * words qe_stats_reduce produced) = elementwise sum over all ranks of comm,
  * in place, asynchronously on `stream`: ncclAllReduce(ncclUint64, ncclSum).
- * uint64 addition wraps like the counters themselves. */
+ * uint64 addition wraps like the counters themselves.  On a non-blocking
+ * communicator the enqueue is awaited (sleeping polls, at most 30 s; then
+ * QE_ECOMM).  The collective completes only when every rank enqueued it: a
+ * host should run it on a stream of its own, agree with its peers over its
+ * own transport that every rank enqueued it, and bound its wait for the
+ * completion (qe_comm_abort on failure) -- bench.py Dist.sum_stats. */
 int qe_allreduce_stats(uint64_t *stats, uint32_t n, void *comm, void *stream);
 
 /* ---- synthetic inputs (counter-based, bit-identical to oracle/) -------- */

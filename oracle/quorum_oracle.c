@@ -1593,7 +1593,9 @@ void orc_progress_send_batch(const orc_prog *a, const void *want, uint32_t send_
  * ConfChangeV2 without Changes = wantsLeaveJoint, PayloadSize).
  * result: 0 no proposal, 1 appended + bcastAppend, 2 dropped (no Progress
  * of its own, :1023-1028), 3 dropped (leadership transfer, :1029-1032),
- * 4 dropped (increaseUncommittedSize, :627-633 / :1761-1779). */
+ * 4 dropped (increaseUncommittedSize, :627-633 / :1761-1779), 5 more
+ * conf-change entries than max_cc (QE_PROP_BAD_CC, ABI 7: refused whole, no
+ * state changes -- an input error, reported per group). */
 typedef struct orc_props {
   const uint32_t *num_entries;
   const uint64_t *payload;
@@ -1649,8 +1651,9 @@ void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
         uint32_t mcc = app_only ? 0 : q->max_cc;
         B += (q->payload ? 8 : 0) + (mcc ? 1 : 0);
         uint32_t ncc = mcc ? q->cc_count[g] : 0;
-        if (ncc > mcc) ncc = mcc;
-        if (ncc) {
+        if (ncc > mcc) {                                     /* QE_PROP_BAD_CC: refused whole */
+          res = 5;
+        } else if (ncc) {
           uint64_t pci = q->pending_conf_index[g], pci0 = pci, applied = q->applied[g];
           int joint = mo != 0;                               /* len(Voters[1]) > 0 */
           B += (a->out ? mb : 0) + 16;                       /* out mask, applied, pendingConfIndex */
@@ -1671,9 +1674,11 @@ void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
           B += pci != pci0 ? 8 : 0;
         }
         /* appendEntry -> increaseUncommittedSize (:1761-1779) */
-        uint64_t us = q->uncommitted_size ? q->uncommitted_size[g] : 0;
-        B += q->uncommitted_size ? 8 : 0;
-        if (us > 0 && s > 0 && us + s > maxu) {
+        uint64_t us = (res != 5 && q->uncommitted_size) ? q->uncommitted_size[g] : 0;
+        B += (res != 5 && q->uncommitted_size) ? 8 : 0;
+        if (res == 5) {
+          /* nothing appended */
+        } else if (us > 0 && s > 0 && us + s > maxu) {
           res = 4;
         } else {
           res = 1;

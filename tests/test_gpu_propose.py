@@ -37,6 +37,8 @@ def random_proposals(rng, pb, max_cc):
     payload = np.where(rng.random(G) < 0.3, 0, rng.integers(1, 40, G)).astype(np.uint64)
     cnt = (rng.integers(0, max_cc + 1, G) * (rng.random(G) < 0.5)).astype(np.uint8)
     cnt = np.minimum(cnt, ne).astype(np.uint8)
+    if max_cc:  # more conf-change entries than max_cc: QE_PROP_BAD_CC, refused whole
+        cnt[rng.random(G) < 0.05] = max_cc + 1
     m = max(1, max_cc)
     pos = np.zeros((m, G), np.uint32)
     for g in range(G):
@@ -123,6 +125,8 @@ def test_propose_matches_oracle(eng, S, F, masks, extras, max_cc, max_ents, flag
         assert (res == 1).any() and (res == 0).any()
         if flags == 0 and "self_slot" in extras and S > 1:
             assert (res == 2).any() and o.sent.any()
+        if flags == 0 and max_cc:
+            assert (res == 5).any()  # QE_PROP_BAD_CC
 
 
 def test_propose_argument_errors(eng):
@@ -146,6 +150,9 @@ def test_propose_argument_errors(eng):
     q.result = None
     assert L.qe_propose(C.byref(p), C.byref(q), None, None) == eng._lib.QE_EINVAL
     q = pr.struct()
+    p.self_slot = None  # MsgProp needs the leader's slot
+    assert L.qe_propose(C.byref(p), C.byref(q), None, None) == eng._lib.QE_EINVAL
+    p = ps.struct()
     assert L.qe_propose(C.byref(p), C.byref(q), None, None) == eng._lib.QE_OK
 
 

@@ -6,7 +6,8 @@ through the engine's qe_allreduce_stats or through torch's all_reduce
 move every rank to the same fallback -- one rank in torch's all_reduce while
 another waits in RCCL is a hang -- and the sums must still be right.  The
 engine's C calls are replaced by fakes here (no GPU, no RCCL); the gloo
-group carries the agreement exactly as the nccl group does on the GPU box.
+group carries the agreement exactly as on the GPU box, where bench.Dist
+runs every agreement on a host-side gloo group beside the nccl one.
 """
 import os
 import socket
@@ -50,7 +51,7 @@ def _fake_engine(lib):
                                  _ptr=lambda t: 0, _stream=lambda d: None)
 
 
-def _worker(rank, world, port, fail_init_on, fail_allreduce_on, q):
+def _worker(rank, world, port, fail_init_on, fail_allreduce_on, q, hang_on=()):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import bench
@@ -64,6 +65,8 @@ def _worker(rank, world, port, fail_init_on, fail_allreduce_on, q):
         return object(), ""
 
     d._try_engine_comm = try_comm
+    if rank in hang_on:  # the collective never completes on this rank
+        d._engine_wait = lambda: "qe_allreduce_stats did not complete in 60 s (injected)"
     d._select_stats_path()
     folded = torch.arange(16, dtype=torch.int64) + 100 * (rank + 1)
     out = d.sum_stats(folded.clone())
@@ -72,11 +75,12 @@ def _worker(rank, world, port, fail_init_on, fail_allreduce_on, q):
     d.close()
 
 
-def _run(fail_init_on, fail_allreduce_on):
+def _run(fail_init_on, fail_allreduce_on, hang_on=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fail_init_on, fail_allreduce_on, q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fail_init_on, fail_allreduce_on, q,
+                                               tuple(hang_on)))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -121,6 +125,19 @@ def test_failed_allreduce_on_one_rank_aborts_and_sums_through_torch():
         out, path, fallback, aborted, has_comm = got[r]
         assert out == WANT  # the saved copy, summed through torch
         assert "rank 1: qe_allreduce_stats" in fallback
+        assert aborted == 1 and not has_comm
+
+
+def test_allreduce_not_completing_on_one_rank_aborts_everywhere():
+    """Enqueued on every rank but not complete in time on one (a peer lost
+    mid-collective): the second agreement, on the host group, moves every
+    rank to the abort and the host-side sum -- nothing waits on the device."""
+    got = _run(fail_init_on=set(), fail_allreduce_on=set(), hang_on={0})
+    for r in (0, 1):
+        out, path, fallback, aborted, has_comm = got[r]
+        assert out == WANT
+        assert "rank 0: qe_allreduce_stats did not complete" in fallback
+        assert path.startswith("torch.distributed gloo all_reduce (FALLBACK")
         assert aborted == 1 and not has_comm
 
 
