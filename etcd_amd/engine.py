@@ -404,7 +404,24 @@ class ProgressState:
             dst[: a.size].copy_(torch.from_numpy(a.copy()).to(self.device))
         if ibuf is not None:
             self.load_rings(ibuf)
+        if "pending" in arrays or "peer" in arrays:
+            self.check_pending_precondition()
         return self
+
+    def check_pending_precondition(self):
+        """The ABI's precondition (include/etcd_quorum.h qe_progress.
+        pending_snapshot): PendingSnapshot is 0 for every peer not in
+        StateSnapshot -- ResetState clears it on each state change
+        (raft/tracker/progress.go:84-89), and the kernels write it only where
+        its value changes.  Raises ValueError on a host-loaded state that
+        violates it (results would be unspecified)."""
+        pend = self.pending.view(self.S, self.stride)[:, : self.G].cpu().numpy()
+        state = self.peer.view(self.S, self.stride)[:, : self.G].cpu().numpy() & 3
+        bad = (pend != 0) & (state != _lib.QE_PR_SNAPSHOT)
+        if bad.any():
+            s, g = (int(x[0]) for x in np.nonzero(bad))
+            raise ValueError(f"PendingSnapshot != 0 outside StateSnapshot (slot {s}, group {g}): "
+                             "the qe_progress precondition")
 
     def load_rings(self, ibuf):
         """Plain uint64 rings, entry-major [S][F][stride] -> ilo / ihi and the

@@ -19,6 +19,11 @@ import json,sys
 d=json.loads(sys.stdin.read())
 print('$W', d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['roofline']['bytes_per_unit'])"
 done
+if [ -n "${AB_WL:-}" ]; then  # in-process A/B of one qe_tune knob (scripts/tune_bench.py)
+  TUNE_WL=$AB_WL TUNE_TPW=-1 TUNE_NT=3 TUNE_KNOB=$AB_KNOB timeout -k 10 400 python -u scripts/tune_bench.py \
+    > "$O/ab_${AB_WL}.txt" 2>&1 || { echo "A/B failed"; tail -20 "$O/ab_${AB_WL}.txt"; exit 6; }
+  cat "$O/ab_${AB_WL}.txt"
+fi
 if [ "${PROF:-1}" = 1 ]; then
   WLS="${WLS:-switch_config}" bash scripts/gpu_profile_workloads.sh || exit 5
 fi

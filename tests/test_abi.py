@@ -299,3 +299,23 @@ def test_set_ring_slot_matches_ring_pack(F):
     got_hi = ps.ihi.numpy().view(np.uint32).reshape(S * st, FP)[:, :F]
     assert np.array_equal(got_lo, lo.reshape(S * st, FP)[:, :F])
     assert np.array_equal(got_hi, hi.reshape(S * st, FP)[:, :F])
+
+
+def test_load_host_rejects_pending_outside_snapshot():
+    """ProgressState.load_host checks the qe_progress precondition the
+    kernels rely on (PendingSnapshot is 0 outside StateSnapshot, written only
+    where it changes): a violating host state is refused (CPU tensors)."""
+    import numpy as np
+
+    from etcd_amd import engine
+    G, S = 70, 3
+    ps = engine.ProgressState(G, S, 4, 1, device="cpu")
+    flags = np.full(S * ps.stride, 1, np.uint8)  # StateReplicate
+    pend = np.zeros(S * ps.stride, np.uint64)
+    ps.load_host(flags=flags, pending=pend)  # fine
+    flags[5] = 2  # StateSnapshot: any PendingSnapshot
+    pend[5] = 9
+    ps.load_host(flags=flags, pending=pend)
+    pend[ps.stride + 3] = 4  # slot 1, group 3 in StateReplicate
+    with pytest.raises(ValueError, match="slot 1, group 3"):
+        ps.load_host(flags=flags, pending=pend)

@@ -81,3 +81,26 @@ def test_bounded_init_times_out_when_peers_never_join(eng):
     rc = L.qe_comm_init_timeout(C.byref(comm), 2, 0, idb, 0, 3000)
     assert rc == eng._lib.QE_ECOMM
     assert not comm.value
+
+
+def test_bounded_init_then_destroy_world_size_one(eng):
+    """A non-blocking communicator (qe_comm_init_timeout) freed through
+    qe_comm_destroy: the finalize is polled (ncclInProgress) and bounded, then
+    the communicator is destroyed -- after an all-reduce on it, and with the
+    engine all-reduce on a stream of its own as bench.py runs it."""
+    L = eng._lib.lib()
+    idb = (C.c_uint8 * L.qe_comm_id_bytes())()
+    eng.check("qe_comm_unique_id", L.qe_comm_unique_id(idb))
+    comm = C.c_void_p()
+    eng.check("qe_comm_init_timeout", L.qe_comm_init_timeout(C.byref(comm), 1, 0, idb, 0, 60_000))
+    side = torch.cuda.Stream(DEV)
+    x = torch.tensor([11, -2] + [0] * 14, dtype=torch.int64, device=DEV)
+    y = x.clone()
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    eng.check("qe_allreduce_stats", L.qe_allreduce_stats(eng._ptr(y), 16, comm,
+                                                          C.c_void_p(side.cuda_stream)))
+    ev = torch.cuda.Event()
+    ev.record(side)
+    ev.synchronize()
+    assert torch.equal(x, y)
+    eng.check("qe_comm_destroy", L.qe_comm_destroy(comm))
