@@ -349,6 +349,78 @@ def leader_transfer_to_slow_follower(be):
     assert bits(out["timeout_now"]) == [2]
 
 
+def leader_transfer_after_snapshot(be):
+    """TestLeaderTransferAfterSnapshot (raft/raft_test.go:3543-3587), the
+    leader's side.  Node 1 leads term 1 of {1, 2, 3}; node 3 was isolated
+    while entry 2 was proposed (its MsgApp lost: StateReplicate, Match 1,
+    Next 3, one entry in flight); entry 2 committed with node 2; the leader's
+    log compacted to the snapshot at 2 (firstIndex 3).  The transfer to 3
+    finds it behind: sendAppend sends an empty MsgApp at Index 2; node 3
+    rejects it (hint 1, LogTerm 1: findConflictByTerm over the compacted
+    prefix gives 1); MaybeDecrTo(2, 1) moves Next to Match + 1 = 2 and
+    BecomeProbe; the retry finds 2 compacted and sends the snapshot at 2
+    (BecomeSnapshot) -- the leader is still the leader, the transfer
+    pending.  Node 3's MsgAppResp after applying the snapshot (Index 2)
+    ends StateSnapshot (Match >= PendingSnapshot: BecomeProbe +
+    BecomeReplicate) and, its Match now lastIndex, the leader sends
+    MsgTimeoutNow (raft.go:1275-1281)."""
+    S = 3
+    sc = {"name": "", "S": S, "self": 0, "max_ents": 0,
+          "log": {"runs": [[2, 1]], "committed": 2, "term_start": 1, "first_index": 3,
+                  "last_index": 2, "snap_index": 2},
+          "peers": [_peer(2, 3, REPLICATE), _peer(2, 3, REPLICATE, True),
+                    dict(_peer(1, 3, REPLICATE), ring=[2])]}
+    be.load(sc, initial_arrays(sc), inc=0b111, tracked=0b111)
+    out = _transfer(be, S, 2)
+    assert be.transferee() == 2 and out["timeout_now"] == 0
+    assert bits(out["sent"]) == [2] and int(out["msg_index"][2]) == 2 and out["snap"] == 0
+    z = np.zeros(S, np.uint64)
+    out = be.step(np.array([0, 0, 2], np.uint8), np.array([0, 0, 2], np.uint64),
+                  np.array([0, 0, 1], np.uint64), np.array([0, 0, 1], np.uint64))
+    assert bits(out["snap"]) == [2] and out["timeout_now"] == 0, out
+    p = be.peer(2)
+    assert (p["state"], p["pending"], p["match"]) == (2, 2, 1), p  # StateSnapshot(2)
+    out = be.step(np.array([0, 0, 1], np.uint8), np.array([0, 0, 2], np.uint64), z, z)
+    assert bits(out["timeout_now"]) == [2], out
+    p = be.peer(2)
+    assert (p["state"], p["match"], p["next"]) == (REPLICATE, 2, 3), p
+    assert be.transferee() == 2
+
+
+def leader_transfer_with_check_quorum(be):
+    """TestLeaderTransferWithCheckQuorum (raft/raft_test.go:3488-3521), the
+    side of the leader the transfers go to.  Node 2 has won term 2 after the
+    first transfer (becomeLeader: reset() -- every Progress at Match 0, Next
+    lastIndex + 1 = 2, the leader's own at Match 1 -- then its empty entry 2
+    and the bcastAppend probes); nodes 1 and 3 accept 2.  The MsgProp of the
+    test appends 3, which both followers accept: node 1 is up to date, so its
+    MsgTransferLeader makes node 2 send MsgTimeoutNow at once -- CheckQuorum
+    (the leader lease) does not hold the transfer back on the leader's side,
+    and a MsgCheckQuorum in between keeps node 2 the leader (both followers
+    active).  Node 1 is slot 0, node 2 slot 1."""
+    S = 3
+    sc = {"name": "", "S": S, "self": 1, "max_ents": 0,
+          "log": {"runs": [[0, 0], [1, 1], [2, 2]], "committed": 1, "term_start": 2,
+                  "first_index": 1, "last_index": 1},
+          "peers": [_peer(0, 2, 0), _peer(1, 2, REPLICATE), _peer(0, 2, 0)]}
+    be.load(sc, initial_arrays(sc), inc=0b111, tracked=0b111)
+    out = be.propose(1, append_only=True)  # becomeLeader's empty entry at 2
+    assert out["result"] == 1 and be.last_index() == 2
+    out = be.send(0b101, 1)  # stepCandidate's bcastAppend: probes
+    assert bits(out["sent"]) == [0, 2]
+    z = np.zeros(S, np.uint64)
+    be.step(np.array([1, 0, 1], np.uint8), np.array([2, 0, 2], np.uint64), z, z)
+    assert be.committed() == 2  # the term's first entry commits
+    out = be.propose(1)  # the test's MsgProp: entry 3, bcast to both
+    assert out["result"] == 1 and bits(out["sent"]) == [0, 2]
+    be.step(np.array([1, 0, 1], np.uint8), np.array([3, 0, 3], np.uint64), z, z)
+    assert be.committed() == 3
+    qa, _ = be.check_quorum()  # the lease: both followers were heard from
+    assert qa == 1
+    out = _transfer(be, S, 0)  # MsgTransferLeader from node 1
+    assert bits(out["timeout_now"]) == [0] and out["sent"] == 0 and be.transferee() == 0
+
+
 def leader_transfer_to_self(be):
     """TestLeaderTransferToSelf (raft/raft_test.go:3589-3598): a transfer to
     the leader itself is a no-op (raft.go:1355-1358)."""
@@ -587,6 +659,7 @@ SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lea
              add_node_check_quorum, leader_transfer_to_up_to_date_node,
              leader_transfer_to_slow_follower, leader_transfer_to_self,
              leader_transfer_to_non_existing_node, leader_transfer_second_to_another_node,
+             leader_transfer_after_snapshot, leader_transfer_with_check_quorum,
              leader_transfer_second_to_same_node, leader_transfer_back,
              leader_transfer_learner_ignored, commit_after_remove_node,
              leader_transfer_remove_node, leader_transfer_demote_node,
