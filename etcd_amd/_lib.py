@@ -107,6 +107,7 @@ class QeProgress(C.Structure):
         ("tracked", vp), ("self_slot", vp), ("lead_transferee", vp), ("snap_index", vp),
         ("max_ents", u32), ("reserved2", u32),
         ("read_acks", vp), ("read_head", vp), ("read_count", vp),  # ABI 5
+        ("read_cap", u32), ("reserved3", u32), ("read_ovf", vp), ("read_keys", vp),  # ABI 7
     ]
 
 
@@ -155,6 +156,8 @@ QE_MSG_SNAP_STATUS, QE_MSG_SNAP_STATUS_REJECT, QE_MSG_UNREACHABLE = 4, 5, 6
 QE_MSG_TRANSFER_LEADER = 7  # ABI 5
 QE_READ_QUEUE = 4           # ABI 5: ReadIndex requests pending per group
 QE_RI_NONE, QE_RI_RESPOND, QE_RI_POSTPONED, QE_RI_QUEUED, QE_RI_FULL = 0, 1, 2, 3, 4
+QE_RI_DUPLICATE = 5         # ABI 7: the request's key is pending already
+QE_READ_CAP_MAX = 255       # ABI 7: the longest queue (read_cap)
 QE_MAX_INFLIGHT = 255
 QE_MAX_LOG_RUNS = 16
 
@@ -214,7 +217,7 @@ PROTOTYPES = {
     "qe_progress_step": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QePeerMsgs), vp, vp]),
     "qe_progress_send": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp]),
     "qe_check_quorum": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp]),
-    "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, u32, vp, vp, vp, vp]),
+    "qe_read_index": (C.c_int, [C.POINTER(QeProgress), vp, vp, u32, vp, vp, vp, vp]),
     "qe_propose": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeProposals), vp, vp]),
     "qe_heartbeat": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp, vp]),
     "qe_switch_config": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeSwitch), vp, vp]),

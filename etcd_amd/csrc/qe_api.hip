@@ -371,6 +371,19 @@ int qe_apply_append_resps(uint64_t num_groups, uint32_t num_slots, uint64_t stri
   return hip_status(hipGetLastError());
 }
 
+// The ReadIndex queue's ABI 7 fields: a capacity of 0 is QE_READ_QUEUE (the
+// ABI 5 queue); a longer queue needs the overflow ring.
+static int read_queue_args(const qe_progress *p, PArgs &a) {
+  if (p->reserved3) return QE_EINVAL;
+  if (p->read_cap != 0 && (p->read_cap < QE_READ_QUEUE || p->read_cap > QE_READ_CAP_MAX))
+    return QE_ERANGE;
+  a.read_cap = p->read_cap ? p->read_cap : QE_READ_QUEUE;
+  if (p->read_acks && a.read_cap > QE_READ_QUEUE && !p->read_ovf) return QE_EINVAL;
+  a.read_ovf = p->read_ovf;
+  a.read_keys = p->read_keys;
+  return QE_OK;
+}
+
 static int progress_args(const qe_progress *p, PArgs &a) {
   if (!p) return QE_EINVAL;
   if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
@@ -418,7 +431,7 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.read_acks = p->read_acks;
   a.read_head = p->read_head;
   a.read_count = p->read_count;
-  return QE_OK;
+  return read_queue_args(p, a);
 }
 
 int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stats,
@@ -540,14 +553,17 @@ int qe_heartbeat(const qe_progress *p, uint64_t *commit, uint32_t *ctx, void *se
   a.read_acks = p->read_acks;
   a.read_head = p->read_head;
   a.read_count = p->read_count;
+  const int rq = read_queue_args(p, a);
+  if (rq) return rq;
   a.hb_commit = commit;
   a.hb_ctx = ctx;
   a.sent = sent;
   return dispatch_progress(p->num_slots, a, 7, false, false, static_cast<hipStream_t>(stream));
 }
 
-int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
-                  uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream) {
+int qe_read_index(const qe_progress *p, const uint8_t *request, const uint64_t *key,
+                  uint32_t lease_based, uint8_t *result, uint32_t *ctx, uint64_t *index,
+                  void *stream) {
   if (!p) return QE_EINVAL;
   if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)
     return QE_EINVAL;
@@ -570,6 +586,9 @@ int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_b
   a.read_acks = p->read_acks;
   a.read_head = p->read_head;
   a.read_count = p->read_count;
+  const int rq = read_queue_args(p, a);
+  if (rq) return rq;
+  a.ri_key = p->read_keys ? key : nullptr;  // keys are checked only when the state keeps them
   a.ri_request = request;
   a.ri_result = result;
   a.ri_ctx = ctx;

@@ -19,7 +19,7 @@
     (defined(QE_CQ_CHANGED_ONLY) || defined(QE_STREAM_ALL_ROWS) || defined(QE_NO_RM8) || \
      defined(QE_RM16_WPB) || defined(QE_PSTEP_WAVES) || defined(QE_STREAM_TPW) ||        \
      defined(QE_STREAM_WAVES) || defined(QE_JOINT_MIN_WAVES) || defined(QE_LD_AUX) ||     \
-     defined(QE_ST_AUX) || defined(QE_SEND_AUX))
+     defined(QE_ST_AUX) || defined(QE_SEND_AUX) || defined(QE_NO_READ_OVF))
 #error "A/B knob set in a product build: use scripts/build_variant*.sh (QE_VARIANT_BUILD)"
 #endif
 #include <hip/hip_runtime.h>
@@ -716,10 +716,15 @@ struct PArgs {
   const uint8_t *self_slot;
   uint8_t *transferee;  // rw (ABI 5: MsgTransferLeader)
   uint32_t max_ents;
-  // ReadIndex queue (ABI 5): acks [G][QE_READ_QUEUE] mask-typed, head, count
+  // ReadIndex queue (ABI 5): acks [G][QE_READ_QUEUE] mask-typed, head, count;
+  // ABI 7: capacity (host-normalised: >= QE_READ_QUEUE), the overflow ring
+  // [G][read_cap] mask-typed, the request keys [G][read_cap]
   void *read_acks;
   uint32_t *read_head;
   uint8_t *read_count;
+  uint32_t read_cap;
+  void *read_ovf;
+  uint64_t *read_keys;
   // step messages and outputs
   const uint8_t *mtype;
   const uint64_t *mindex, *mhint, *mlogterm;
@@ -732,6 +737,7 @@ struct PArgs {
   uint64_t *stats;
   // read index (qe_read_index)
   const uint8_t *ri_request;
+  const uint64_t *ri_key;  // ABI 7: request keys (NULL: no duplicate check)
   uint8_t *ri_result;
   uint32_t *ri_ctx;
   uint64_t *ri_index;

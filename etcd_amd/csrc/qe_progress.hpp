@@ -566,6 +566,32 @@ __device__ __forceinline__ uint32_t mem_prefix_le(const uint32_t (&lo)[kRingChun
 //   3.68, S = 7 4.74 -> 4.45 ms (profiles/r05/pstep_pipe_ab*.txt); at S = 7
 //   the loads run two slots ahead (PF2 below).
 // ---------------------------------------------------------------------------
+// The ReadIndex queue beyond its word (ABI 7): entry j >= QE_READ_QUEUE of
+// group g, context c, at read_ovf[g*cap + c % cap] -- lane `lane` of a tile's
+// block [64][cap] (mask-typed); keys likewise in read_keys.  Offsets for the
+// tile's descriptors.
+template <typename MT>
+__device__ __forceinline__ rsrc_t ovf_rsrc(const PArgs &a, uint64_t g0, uint32_t n) {
+  return mk_rsrc(static_cast<const MT *>(a.read_ovf) + g0 * a.read_cap, n * a.read_cap * sizeof(MT));
+}
+__device__ __forceinline__ uint32_t ovf_off(const PArgs &a, uint32_t lane, uint32_t ctx, uint32_t mb) {
+  return (lane * a.read_cap + ctx % a.read_cap) * mb;
+}
+template <typename MT>
+__device__ __forceinline__ uint32_t ovf_ld(rsrc_t r, uint32_t off) {
+  if constexpr (sizeof(MT) == 1) return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  else return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+template <typename MT>
+__device__ __forceinline__ void ovf_st(uint32_t v, rsrc_t r, uint32_t off) {
+  if constexpr (sizeof(MT) == 1) __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v), r, off, 0, 0);
+}
+// A lane's own earlier store to the overflow ring must have landed before it
+// reads the same entry again (rare paths only: the ring is touched by groups
+// with more than QE_READ_QUEUE pending requests).
+__device__ __forceinline__ void ovf_fence() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 struct PB {  // per-peer loads of one slot (the ring is loaded at the slot's turn)
   uint64_t mt, ix, nx, hn, lt;  // mt, ix: from the wave's LDS copy of phase 1's rows
   uint32_t w;                   // the packed per-peer word (QE_PW_*)
@@ -689,6 +715,11 @@ k_progress_step(PArgs a) {
   using QT = typename std::conditional<sizeof(MT) == 1, uint32_t, uint64_t>::type;
   constexpr uint32_t EW = 8 * sizeof(MT);
   constexpr uint32_t kRQ = QE_READ_QUEUE;
+#ifdef QE_NO_READ_OVF  // A/B knob: without the overflow-ring paths (ABI 5 queue only)
+  constexpr bool OVF = false;
+#else
+  constexpr bool OVF = RD;  // queue entries past the word (ABI 7)
+#endif
   // statistics: per-lane counts in 32 bits (a lane sees at most one group
   // per tile), the sums in 64
   uint32_t n_groups = 0, n_adv = 0, n_viol = 0, n_read = 0;
@@ -741,14 +772,15 @@ k_progress_step(PArgs a) {
     const uint64_t c0 = bld64(r_commit, o8);
     const uint64_t snap_ld = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), o8) : 0;
     // ReadIndex queue (ABI 5): entry 0's context number, the pending count
-    // (clamped: a count above QE_READ_QUEUE is invalid input) and every
-    // entry's acks in one word
+    // (clamped: a count above the capacity is invalid input) and the first
+    // QE_READ_QUEUE entries' acks in one word; entries beyond it (ABI 7) in
+    // the overflow ring, read only when a response carries their context
     const bool rd = RD && a.read_acks != nullptr;  // RD: the variant that tracks ReadIndex
     uint32_t qh = 0, qn = 0;
     QT q0 = 0;
     if (rd) {
       qn = bld8(mk_rsrc(a.read_count + g0, n), lane);
-      qn = qn < kRQ ? qn : kRQ;
+      qn = qn < a.read_cap ? qn : a.read_cap;
       qh = bld32(mk_rsrc(a.read_head + g0, n * 4), o8 >> 1);
       if constexpr (sizeof(QT) == 4)
         q0 = bld32(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 4), o8 >> 1);
@@ -1032,6 +1064,11 @@ k_progress_step(PArgs a) {
       bool lp = false;
       pb_ready<P>(nxt);  // (before the sends: in memory form they append in memory)
       if (__builtin_amdgcn_ballot_w64(k1 > 0)) send_burst<ACCT>(p, true, k1, x, r1, ac);
+      // ReadIndex: the entries this slot's heartbeat response releases
+      // (readOnly.advance through the acked one); a response for an entry
+      // in the overflow ring (ABI 7) is resolved after the handlers
+      uint32_t rel = 0;
+      bool ovf_hit = false;
       if (touched) {
         if (tt == QE_MSG_APP_RESP_REJECT) {  // raft.go:1109-1236
           p.recent_active = 1;
@@ -1109,18 +1146,13 @@ k_progress_step(PArgs a) {
           if (rd) {
             const uint32_t cx = sa.read_ctx ? cur.rc : dctx;
             const uint32_t j = cx - qh;
-            if (cx != 0 && j < qn) {
+            if (cx != 0 && j < kRQ && j < qn) {
               q |= static_cast<QT>(1u << s) << (EW * j);
               qtouch = true;
               const uint32_t e = static_cast<uint32_t>(q >> (EW * j)) & kFull;
-              if (joint_vote(mi, mo, e, e) == kVoteWon) {
-                const uint32_t r = j + 1;
-                q = r >= kRQ ? static_cast<QT>(0) : static_cast<QT>(q >> (EW * r));
-                qh += r;
-                qn -= r;
-                nrel += r;
-              }
+              if (joint_vote(mi, mo, e, e) == kVoteWon) rel = j + 1;
             }
+            ovf_hit = OVF && cx != 0 && j >= kRQ && j < qn;  // an entry beyond the word
           }
         } else if (tt == QE_MSG_SNAP_STATUS || tt == QE_MSG_SNAP_STATUS_REJECT) {  // :1310-1331
           if (p.state == QE_PR_SNAPSHOT) {
@@ -1142,6 +1174,45 @@ k_progress_step(PArgs a) {
               ltr = s;
               if (p.match == li) tnow |= 1u << s;  // sendTimeoutNow (:1364-1366)
               else k2 = 1;                         // sendAppend (:1368)
+            }
+          }
+        }
+      }
+      if constexpr (RD) {
+        // an ack for an entry past the word: its acks from the overflow ring
+        // (a rare, wave-uniform path; the fence orders this lane's earlier
+        // ring stores of the round before the load)
+        if (OVF && __builtin_amdgcn_ballot_w64(ovf_hit)) {
+          ovf_fence();
+          const uint32_t ovf_ctx = sa.read_ctx ? cur.rc : dctx;  // (the context of the response)
+          const rsrc_t r_ovf = ovf_rsrc<MT>(a, g0, n);
+          const uint32_t off = ovf_hit ? ovf_off(a, lane, ovf_ctx, sizeof(MT)) : kOOB;
+          const uint32_t e = ovf_ld<MT>(r_ovf, off) | (1u << s);
+          const bool won = ovf_hit && joint_vote(mi, mo, e & kFull, e & kFull) == kVoteWon;
+          ovf_st<MT>(e, r_ovf, (ovf_hit && !won) ? off : kOOB);
+          rel = won ? ovf_ctx - qh + 1u : rel;
+          ac.add(ovf_hit, sizeof(MT));
+          ac.add(ovf_hit && !won, sizeof(MT));
+        }
+        if (__builtin_amdgcn_ballot_w64(rel != 0)) {  // readOnly.advance (read_only.go:81-112)
+          const uint32_t qn_old = qn;
+          if (rel != 0) {
+            q = rel >= kRQ ? static_cast<QT>(0) : static_cast<QT>(q >> (EW * rel));
+            qh += rel;
+            qn -= rel;
+            nrel += rel;
+            qtouch = true;
+          }
+          // the entries that move into the word come from the overflow ring
+          if (OVF && __builtin_amdgcn_ballot_w64(rel != 0 && qn_old > kRQ)) {
+            ovf_fence();
+            const rsrc_t r_ovf = ovf_rsrc<MT>(a, g0, n);
+#pragma unroll 1
+            for (uint32_t pp = 0; pp < kRQ; pp++) {  // (rolled: a rare path, few registers)
+              const bool on = rel != 0 && qn_old > kRQ && pp < qn && pp + rel >= kRQ;
+              const uint32_t e = ovf_ld<MT>(r_ovf, on ? ovf_off(a, lane, qh + pp, sizeof(MT)) : kOOB);
+              if (on) q |= static_cast<QT>(e) << (EW * pp);
+              ac.add(on, sizeof(MT));
             }
           }
         }
@@ -1890,7 +1961,7 @@ __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
       if (a.read_acks) {
         const uint32_t qn = bld8(mk_rsrc(a.read_count + g0, n), lane);
         const uint32_t qh = bld32(mk_rsrc(a.read_head + g0, n * 4), lane * 4);
-        const uint32_t q = qn < QE_READ_QUEUE ? qn : QE_READ_QUEUE;
+        const uint32_t q = qn < a.read_cap ? qn : a.read_cap;
         cx = q ? qh + q - 1u : 0u;  // lastPendingRequestCtx
       }
       bst32(cx, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);
@@ -1947,7 +2018,7 @@ __device__ __forceinline__ void hb_finish(const PArgs &a, uint64_t t, uint32_t l
   const uint32_t n = tile_n(a.G, t);
   const uint32_t o8 = lane * 8;
   if (a.hb_ctx) {
-    const uint32_t q = x.qn < QE_READ_QUEUE ? x.qn : QE_READ_QUEUE;
+    const uint32_t q = x.qn < a.read_cap ? x.qn : a.read_cap;
     bst32(q ? x.qh + q - 1u : 0u, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);  // lastPendingRequestCtx
   }
 #pragma unroll
@@ -2132,17 +2203,22 @@ __global__ __launch_bounds__(kBlock) void k_check_quorum(PArgs a) {
 // qe_read_index: MsgReadIndex on the leader (stepLeader, raft/raft.go:
 // 1078-1096; sendMsgReadIndexResponse :1827-1843).  One lane per group, a
 // wave per 64-group tile; the queue word of a group that queues is rewritten
-// whole (entry `count` = the leader's own ack).
+// whole (entry `count` = the leader's own ack), or (ABI 7) the new entry's
+// overflow slot is written when the word is full.  With keys, the pending
+// requests' keys are compared first (addRequest's duplicate check, a loop
+// over the group's pending entries: rare and short).
 template <int S, typename MT, bool MASKED, bool JOINT>
 __global__ __launch_bounds__(kBlock) void k_read_index(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   using QT = typename std::conditional<sizeof(MT) == 1, uint32_t, uint64_t>::type;
   constexpr uint32_t EW = 8 * sizeof(MT);
+  constexpr uint32_t kRQ = QE_READ_QUEUE;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
   const uint64_t ntiles = (a.G + 63) / 64;
+  const uint32_t cap = a.read_cap;
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
@@ -2178,31 +2254,51 @@ __global__ __launch_bounds__(kBlock) void k_read_index(PArgs a) {
           q = bld32(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 4), qo);
         else
           q = bld64(mk_rsrc(static_cast<const QT *>(a.read_acks) + g0, n * 8), qd ? o8 : kOOB);
+        const uint64_t key = a.ri_key ? bld64(mk_rsrc(a.ri_key + g0, n * 8), qd ? o8 : kOOB) : 0;
+        qn = qn < cap ? qn : cap;  // (a count above the capacity is invalid input)
         // an empty queue starts over at context 1 when its head is 0 (a
         // fresh state, or numbers that wrapped exactly)
         if (qn == 0 && qh == 0) qh = 1;
-        const bool full = qn >= QE_READ_QUEUE || qh + qn == 0u;
-        res = (qd && full) ? QE_RI_FULL : res;
-        const bool add = qd && !full;
+        // addRequest's duplicate check (read_only.go:57-60)
+        bool dup = false;
+        const rsrc_t r_key = a.ri_key ? mk_rsrc(a.read_keys + g0 * cap, n * cap * 8) : mk_rsrc(nullptr, 0);
+        for (uint32_t j = 0; __builtin_amdgcn_ballot_w64(a.ri_key && qd && !dup && j < qn); j++) {
+          const bool on = a.ri_key && qd && !dup && j < qn;
+          const uint64_t kj = bld64(r_key, on ? (lane * cap + (qh + j) % cap) * 8 : kOOB);
+          if (on && kj == key) {
+            dup = true;
+            ctx = qh + j;
+          }
+        }
+        res = (qd && dup) ? QE_RI_DUPLICATE : res;
+        const bool full = qn >= cap || qh + qn == 0u;
+        res = (qd && !dup && full) ? QE_RI_FULL : res;
+        const bool add = qd && !dup && !full;
         const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), add ? lane : kOOB) : 0xFFu;
         const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
-        ctx = qh + qn;
+        if (add) ctx = qh + qn;
+        const bool in_word = qn < kRQ;
         // entries past the count are dead: the word is rewritten canonical
-        const QT live = qn >= QE_READ_QUEUE ? q : static_cast<QT>(q & ((static_cast<QT>(1) << (EW * qn)) - 1u));
-        const QT nq = static_cast<QT>(live | (static_cast<QT>(selfb) << (EW * (qn < QE_READ_QUEUE ? qn : 0u))));
+        const QT live = qn >= kRQ ? q : static_cast<QT>(q & ((static_cast<QT>(1) << (EW * qn)) - 1u));
+        const QT nq = static_cast<QT>(live | (static_cast<QT>(selfb) << (EW * (in_word ? qn : 0u))));
         if (__builtin_amdgcn_ballot_w64(add)) {
+          const bool ww = add && in_word;
           if constexpr (sizeof(QT) == 4)
-            bst32(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 4), add ? o4 : kOOB);
+            bst32(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 4), ww ? o4 : kOOB);
           else
-            bst64(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 8), add ? o8 : kOOB);
+            bst64(nq, mk_rsrc(static_cast<QT *>(a.read_acks) + g0, n * 8), ww ? o8 : kOOB);
+          if (__builtin_amdgcn_ballot_w64(add && !in_word))  // ABI 7: the overflow ring
+            ovf_st<MT>(selfb, ovf_rsrc<MT>(a, g0, n), (add && !in_word) ? ovf_off(a, lane, ctx, sizeof(MT)) : kOOB);
+          if (a.ri_key) bst64(key, r_key, add ? (lane * cap + ctx % cap) * 8 : kOOB);
           bst32(qh, mk_rsrc(a.read_head + g0, n * 4), add ? o4 : kOOB);
           bst8(qn + 1, mk_rsrc(a.read_count + g0, n), add ? lane : kOOB);
         }
       }
     }
     bst8(res, mk_rsrc(a.ri_result + g0, n), lane);
-    if (a.ri_ctx && __builtin_amdgcn_ballot_w64(res == QE_RI_QUEUED))
-      bst32(ctx, mk_rsrc(a.ri_ctx + g0, n * 4), res == QE_RI_QUEUED ? o4 : kOOB);
+    const bool wc = res == QE_RI_QUEUED || res == QE_RI_DUPLICATE;
+    if (a.ri_ctx && __builtin_amdgcn_ballot_w64(wc))
+      bst32(ctx, mk_rsrc(a.ri_ctx + g0, n * 4), wc ? o4 : kOOB);
     const bool wi = res == QE_RI_RESPOND || res == QE_RI_QUEUED;
     if (a.ri_index && __builtin_amdgcn_ballot_w64(wi))
       bst64(c, mk_rsrc(a.ri_index + g0, n * 8), wi ? o8 : kOOB);

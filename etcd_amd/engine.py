@@ -304,10 +304,13 @@ class ProgressState:
     allocates the optional per-group arrays: "tracked" (slot mask),
     "self_slot", "lead_transferee" (u8, 0xFF = none), "snap_index" (u64),
     "reads" (ABI 5: the ReadIndex queue -- read_acks [G][QE_READ_QUEUE]
-    mask-typed, read_head u32 (starting at context 1), read_count u8)."""
+    mask-typed, read_head u32 (starting at context 1), read_count u8; ABI 7:
+    read_cap > QE_READ_QUEUE adds the overflow ring read_ovf [G][read_cap]
+    mask-typed), "read_keys" (ABI 7: [G][cap] u64 request keys, for
+    qe_read_index's duplicate check)."""
 
     def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None,
-                 extras=(), max_ents=0):
+                 extras=(), max_ents=0, read_cap=0):
         if not 1 <= S <= _lib.QE_MAX_SLOTS or not 1 <= F <= _lib.QE_MAX_INFLIGHT:
             raise ValueError("bad num_slots / inflight_cap")
         if not 1 <= R <= _lib.QE_MAX_LOG_RUNS:
@@ -350,6 +353,12 @@ class ProgressState:
                           if "reads" in extras else None)
         self.read_count = (torch.zeros(self.G, dtype=u8, device=dev)
                            if "reads" in extras else None)
+        self.read_cap = int(read_cap)
+        cap = max(rq, self.read_cap)
+        self.read_ovf = (torch.zeros(self.G * cap, dtype=md, device=dev)
+                         if "reads" in extras and cap > rq else None)
+        self.read_keys = (torch.zeros(self.G * cap, dtype=i64, device=dev)
+                          if "read_keys" in extras else None)
 
     def struct(self):
         return _lib.QeProgress(
@@ -360,12 +369,12 @@ class ProgressState:
             _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
             _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
             _ptr(self.snap_index), self.max_ents, 0, _ptr(self.read_acks), _ptr(self.read_head),
-            _ptr(self.read_count))
+            _ptr(self.read_count), self.read_cap, 0, _ptr(self.read_ovf), _ptr(self.read_keys))
 
     ARRAYS = ("match", "next", "pending", "peer", "ilo", "ihi", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
               "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index",
-              "read_acks", "read_head", "read_count")
+              "read_acks", "read_head", "read_count", "read_ovf", "read_keys")
 
     def load_host(self, **arrays):
         """numpy arrays (uint64 as uint64, masks as uint8/uint16, peer words
@@ -579,18 +588,20 @@ def progress_send(ps, want, send_if_empty=False):
     return sent, snap
 
 
-def read_index(ps, request, lease_based=False):
+def read_index(ps, request, lease_based=False, key=None):
     """qe_read_index: MsgReadIndex on the leader of every group with
     request[g] != 0 (raft/raft.go:1078-1096) -> (result uint8[G] QE_RI_*,
-    ctx int32[G] (the context number of a QUEUED request), index int64[G]
-    (the read index of RESPOND / QUEUED))."""
+    ctx int32[G] (the context number of a QUEUED request, or of the pending
+    one a DUPLICATE key names), index int64[G] (the read index of RESPOND /
+    QUEUED)).  key: int64[G] request keys (ABI 7, with ps.read_keys)."""
     G, dev = ps.G, ps.device
     result = torch.zeros(G, dtype=torch.uint8, device=dev)
     ctx = torch.zeros(G, dtype=torch.int32, device=dev)
     index = torch.zeros(G, dtype=torch.int64, device=dev)
     p = ps.struct()
     check("qe_read_index", _lib.lib().qe_read_index(
-        C.byref(p), _ptr(request), int(bool(lease_based)), _ptr(result), _ptr(ctx), _ptr(index),
+        C.byref(p), _ptr(request), _ptr(key), int(bool(lease_based)), _ptr(result), _ptr(ctx),
+        _ptr(index),
         _stream(dev)))
     return result, ctx, index
 

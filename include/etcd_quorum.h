@@ -334,12 +334,17 @@ int qe_election_steps(const qe_election_state *st,
                                          slot (raft.go:1339-1370)            */
 
 /* ABI 5: ReadIndex requests a leader keeps pending under ReadOnlySafe
- * (readOnly.pendingReadIndex + readIndexQueue, raft/read_only.go:39-63), at
- * most QE_READ_QUEUE per group.  Each request has a context number (the
- * engine's stand-in for the request's context bytes, unique within the
- * group): queue entry j has context read_head + j; numbers are 32-bit,
- * assigned consecutively by qe_read_index, never 0 (0 = no context). */
+ * (readOnly.pendingReadIndex + readIndexQueue, raft/read_only.go:39-63).
+ * Each request has a context number (the engine's stand-in for the
+ * request's context bytes, unique within the group): queue entry j has
+ * context read_head + j; numbers are 32-bit, assigned consecutively by
+ * qe_read_index, never 0 (0 = no context).  The first QE_READ_QUEUE entries
+ * live in one word per group (read_acks, the fast form every kernel reads
+ * with the group); ABI 7: a queue of up to read_cap entries keeps entries
+ * QE_READ_QUEUE.. in the overflow ring read_ovf, each at its context number
+ * mod read_cap (an entry never moves while it waits there). */
 #define QE_READ_QUEUE 4
+#define QE_READ_CAP_MAX 255     /* read_count is a byte                      */
 
 /* Leader-side Progress of every peer of G groups (raft/tracker/progress.go:
  * 30-80) plus the leader's log model: term runs r < run_count[g] covering
@@ -403,7 +408,24 @@ typedef struct qe_progress {
                                    read_acks[g*QE_READ_QUEUE + j] (one 4- or
                                    8-byte word per group)                    */
   uint32_t *read_head;          /* [G] rw: context number of queue entry 0   */
-  uint8_t *read_count;          /* [G] rw: pending requests, 0..QE_READ_QUEUE */
+  uint8_t *read_count;          /* [G] rw: pending requests, 0..read_cap     */
+  /* ABI 7: a queue longer than the word (readIndexQueue is unbounded in the
+   * reference, read_only.go:56-63) and the duplicate-request check */
+  uint32_t read_cap;            /* entries a queue holds: 0 (= QE_READ_QUEUE,
+                                   ABI 5) or QE_READ_QUEUE..QE_READ_CAP_MAX  */
+  uint32_t reserved3;           /* must be 0                                 */
+  void *read_ovf;               /* [G][read_cap] rw mask-typed: the acks of
+                                   the entry with context c at queue position
+                                   >= QE_READ_QUEUE, at read_ovf[g*read_cap +
+                                   c % read_cap]; needed when read_cap >
+                                   QE_READ_QUEUE                             */
+  uint64_t *read_keys;          /* [G][read_cap] rw: the caller's key (e.g. a
+                                   hash of the request context bytes) of the
+                                   entry with context c, at read_keys[g*
+                                   read_cap + c % read_cap]; NULL = keys not
+                                   tracked.  Given, it must have been given to
+                                   every qe_read_index that queued the pending
+                                   entries                                   */
 } qe_progress;
 
 /* One round of peer responses: message of slot s for group g at
@@ -501,14 +523,15 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
  *   ReadOnlySafe -> readOnly.addRequest(committed) + the leader's own ack
  *     (self_slot; recvAck(r.id)): QE_RI_QUEUED with context number ctx[g]
  *     and index = committed; the host sends the heartbeats carrying ctx and
- *     answers when qe_progress_step releases the entry.  With QE_READ_QUEUE
- *     requests already pending (or the context numbers exhausted:
- *     read_head + read_count would be 0 mod 2^32) -> QE_RI_FULL, nothing
- *     changes (an engine limit; the host retries later).
- * addRequest ignores a context already pending (read_only.go:57-60): a
- * host that resends a request (etcd's server retries the same request id,
- * server/etcdserver/v3_server.go:808-824) keeps its context number and does
- * not submit it again.
+ *     answers when qe_progress_step releases the entry.  ABI 7: with keys
+ *     (key and p->read_keys non-NULL) a request whose key[g] equals a
+ *     pending request's is ignored, as addRequest ignores a context already
+ *     pending (read_only.go:57-60; etcd's server resends the same request
+ *     id, server/etcdserver/v3_server.go:808-824) -> QE_RI_DUPLICATE with
+ *     that request's context.  With read_cap (QE_READ_QUEUE when 0)
+ *     requests already pending (or the context numbers exhausted: read_head
+ *     + read_count would be 0 mod 2^32) -> QE_RI_FULL, nothing changes (a
+ *     capacity the host chose; up to QE_READ_CAP_MAX).
  * Needs p->read_acks / read_head / read_count unless every result is
  * RESPOND or POSTPONED (lease_based).  ctx and index may be NULL; they are
  * written only where they apply.  Groups without a request: result 0. */
@@ -517,8 +540,13 @@ int qe_progress_step(const qe_progress *p, const qe_peer_msgs *m, uint64_t *stat
 #define QE_RI_POSTPONED 2
 #define QE_RI_QUEUED 3
 #define QE_RI_FULL 4
-int qe_read_index(const qe_progress *p, const uint8_t *request, uint32_t lease_based,
-                  uint8_t *result, uint32_t *ctx, uint64_t *index, void *stream);
+#define QE_RI_DUPLICATE 5  /* ABI 7: key[g] is pending already: addRequest
+                              ignores it (read_only.go:57-60); ctx[g] = the
+                              pending request's context (the heartbeats the
+                              reference sends then carry it), index not set */
+int qe_read_index(const qe_progress *p, const uint8_t *request, const uint64_t *key,
+                  uint32_t lease_based, uint8_t *result, uint32_t *ctx, uint64_t *index,
+                  void *stream);
 
 /* MsgCheckQuorum on every group's leader (stepLeader, raft/raft.go:997-1018):
  * the leader's own Progress (self_slot, when tracked) becomes RecentActive;

@@ -61,7 +61,7 @@ def _declare(L):
         "orc_max_threads": (i32, []),
         "orc_progress_step_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcMsgs), vp, i32]),
         "orc_check_quorum_batch": (None, [C.POINTER(OrcProg), vp, vp]),
-        "orc_read_index_batch": (None, [C.POINTER(OrcProg), vp, u32, vp, vp, vp]),
+        "orc_read_index_batch": (None, [C.POINTER(OrcProg), vp, vp, u32, vp, vp, vp]),
         "orc_progress_send_batch": (None, [C.POINTER(OrcProg), vp, u32, u32, vp, vp]),
         "orc_propose_batch": (None, [C.POINTER(OrcProg), C.POINTER(OrcProps), vp]),
         "orc_checksum_prop": (u64, [u64, u32, u64, u64, u32]),
@@ -176,7 +176,8 @@ class OrcProg(C.Structure):
         ("out", C.c_void_p), ("tracked", C.c_void_p), ("self_slot", C.c_void_p),
         ("lead_transferee", C.c_void_p), ("snap_index", C.c_void_p), ("max_ents", C.c_uint32),
         ("reserved2", C.c_uint32), ("read_acks", C.c_void_p), ("read_head", C.c_void_p),
-        ("read_count", C.c_void_p),
+        ("read_count", C.c_void_p), ("read_cap", C.c_uint32), ("reserved3", C.c_uint32),
+        ("read_ovf", C.c_void_p), ("read_keys", C.c_void_p),
     ]
 
 
@@ -218,7 +219,7 @@ class ProgressBatch:
     rewrites them)."""
 
     OPTIONAL = ("inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index",
-                "read_acks", "read_head", "read_count")
+                "read_acks", "read_head", "read_count", "read_ovf", "read_keys")
     READ_QUEUE = 4
 
     def __init__(self, G, S, F, R, stride=None, max_ents=0):
@@ -240,6 +241,7 @@ class ProgressBatch:
         self.run_count = np.zeros(G, np.uint8)
         for k in self.OPTIONAL:
             setattr(self, k, None)
+        self.read_cap = 0
 
     @property
     def flags(self):
@@ -260,13 +262,19 @@ class ProgressBatch:
         ct = self.icount if icount is None else np.broadcast_to(icount, self.pw.shape)
         self.pw[:] = pack_word(f, st, ct)
 
-    def track_reads(self):
+    def track_reads(self, cap=0, keys=False):
         """Allocate the ReadIndex queue (ABI 5): acks word per group (uint32
         for S <= 8, uint64 above: entry j in bits [8*mb*j, ...)), the
-        context number of entry 0 (starting at 1) and the count."""
+        context number of entry 0 (starting at 1) and the count; ABI 7: a
+        capacity `cap` > 4 adds the overflow ring [G][cap] (mask type),
+        `keys` the request keys [G][max(cap, 4)] (uint64)."""
         self.read_acks = np.zeros(self.G, np.uint32 if self.S <= 8 else np.uint64)
         self.read_head = np.ones(self.G, np.uint32)
         self.read_count = np.zeros(self.G, np.uint8)
+        self.read_cap = int(cap)
+        c = max(4, self.read_cap)
+        self.read_ovf = np.zeros(self.G * c, mask_dtype(self.S)) if c > 4 else None
+        self.read_keys = np.zeros(self.G * c, np.uint64) if keys else None
         return self
 
     def copy(self):
@@ -283,7 +291,7 @@ class ProgressBatch:
                        P(self.run_count), P(self.inc), P(self.out), P(self.tracked),
                        P(self.self_slot), P(self.lead_transferee), P(self.snap_index),
                        self.max_ents, 0, P(self.read_acks), P(self.read_head),
-                       P(self.read_count))
+                       P(self.read_count), self.read_cap, 0, P(self.read_ovf), P(self.read_keys))
 
 
 class StepOut:
@@ -336,14 +344,16 @@ def progress_send(pb, want, send_if_empty, max_ents=None):
     return sent, snap
 
 
-def read_index(pb, request, lease_based=False):
+def read_index(pb, request, lease_based=False, key=None):
     """MsgReadIndex on the leader of every group with request[g] != 0
-    (oracle) -> (result uint8[G], ctx uint32[G], index uint64[G])."""
+    (oracle) -> (result uint8[G], ctx uint32[G], index uint64[G]); key:
+    uint64[G] request keys (ABI 7, with pb.read_keys)."""
     result = np.zeros(pb.G, np.uint8)
     ctx = np.zeros(pb.G, np.uint32)
     index = np.zeros(pb.G, np.uint64)
     s = pb.struct()
-    lib().orc_read_index_batch(C.byref(s), P(np.ascontiguousarray(request, np.uint8)),
+    k = None if key is None else np.ascontiguousarray(key, np.uint64)
+    lib().orc_read_index_batch(C.byref(s), P(np.ascontiguousarray(request, np.uint8)), P(k),
                                int(bool(lease_based)), P(result), P(ctx), P(index))
     return result, ctx, index
 

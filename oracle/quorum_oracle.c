@@ -1007,6 +1007,11 @@ typedef struct orc_prog {
   void *read_acks;
   uint32_t *read_head;
   uint8_t *read_count;
+  /* ABI 7: entries past the word in a ring at context % read_cap (0 = the
+   * word alone), the requests' keys likewise (NULL: not tracked) */
+  uint32_t read_cap, reserved3;
+  void *read_ovf;
+  uint64_t *read_keys;
 } orc_prog;
 
 typedef struct orc_msgs {
@@ -1029,16 +1034,28 @@ typedef struct orc_msgs {
 /* message kinds (qe_peer_msgs.type) */
 enum { M_NONE = 0, M_APP_RESP, M_APP_RESP_REJECT, M_HEARTBEAT_RESP, M_SNAP_STATUS,
        M_SNAP_STATUS_REJECT, M_UNREACHABLE, M_TRANSFER_LEADER };
-#define READ_QUEUE 4 /* QE_READ_QUEUE */
+#define READ_QUEUE 4 /* QE_READ_QUEUE: the entries of the device form's word */
 
 /* readOnly (raft/read_only.go:39-63) of one group as the reference keeps
  * it: the queue of pending requests in arrival order, each with its
- * context (here its context number) and its acks (a set of slots). */
+ * context (here its context number) and its acks (a set of slots); at most
+ * read_cap (<= 255) of them, the device form's capacity. */
 typedef struct orc_ro {
   uint32_t n;                      /* len(readIndexQueue)                  */
-  uint32_t ctx[READ_QUEUE];        /* readIndexQueue                       */
-  uint32_t acks[READ_QUEUE];       /* pendingReadIndex[ctx].acks           */
+  uint32_t ctx[256];               /* readIndexQueue                       */
+  uint32_t acks[256];              /* pendingReadIndex[ctx].acks           */
 } orc_ro;
+
+static inline uint32_t ro_cap(const orc_prog *a) { return a->read_cap ? a->read_cap : READ_QUEUE; }
+static uint32_t ovf_get(const orc_prog *a, uint32_t mb, uint64_t g, uint32_t ctx) {
+  uint64_t i = g * ro_cap(a) + ctx % ro_cap(a);
+  return mb == 1 ? ((const uint8_t *)a->read_ovf)[i] : ((const uint16_t *)a->read_ovf)[i];
+}
+static void ovf_set(const orc_prog *a, uint32_t mb, uint64_t g, uint32_t ctx, uint32_t v) {
+  uint64_t i = g * ro_cap(a) + ctx % ro_cap(a);
+  if (mb == 1) ((uint8_t *)a->read_ovf)[i] = (uint8_t)v;
+  else ((uint16_t *)a->read_ovf)[i] = (uint16_t)v;
+}
 
 static uint64_t ro_word_get(const void *w, uint32_t mb, uint64_t g) {
   return mb == 1 ? ((const uint32_t *)w)[g] : ((const uint64_t *)w)[g];
@@ -1047,13 +1064,21 @@ static void ro_word_set(void *w, uint32_t mb, uint64_t g, uint64_t v) {
   if (mb == 1) ((uint32_t *)w)[g] = (uint32_t)v;
   else ((uint64_t *)w)[g] = v;
 }
-/* the device form -> the queue: entry j has context head + j */
-static void ro_load(orc_ro *r, uint64_t word, uint32_t head, uint32_t count, uint32_t mb) {
-  r->n = count < READ_QUEUE ? count : READ_QUEUE;
+/* the device form -> the queue: entry j has context head + j; entries
+ * j >= READ_QUEUE come from the overflow ring (ABI 7) */
+static void ro_load(orc_ro *r, const orc_prog *a, uint64_t g, uint32_t mb) {
+  uint64_t word = ro_word_get(a->read_acks, mb, g);
+  uint32_t head = a->read_head[g], count = a->read_count[g], cap = ro_cap(a);
+  r->n = count < cap ? count : cap;
   for (uint32_t j = 0; j < r->n; j++) {
     r->ctx[j] = head + j;
-    r->acks[j] = (uint32_t)(word >> (8 * mb * j)) & ((1u << (8 * mb)) - 1u);
+    r->acks[j] = j < READ_QUEUE ? (uint32_t)(word >> (8 * mb * j)) & ((1u << (8 * mb)) - 1u)
+                                : ovf_get(a, mb, g, head + j);
   }
+}
+/* the queue's entries past the word -> the overflow ring */
+static void ro_store_ovf(const orc_ro *r, const orc_prog *a, uint64_t g, uint32_t mb) {
+  for (uint32_t j = READ_QUEUE; j < r->n; j++) ovf_set(a, mb, g, r->ctx[j], r->acks[j]);
 }
 /* the queue -> the device form (entries past the count 0) */
 static uint64_t ro_word(const orc_ro *r, uint32_t mb) {
@@ -1267,10 +1292,11 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
       uint32_t rhead0 = 0, rn0 = 0, released = 0, dctx = 0;
       int rtouch = 0;
       ro.n = 0;
+      uint64_t ovfB = 0; /* overflow-ring bytes (ABI 7) */
       if (rd) {
         rword0 = ro_word_get(a->read_acks, mb, g);
         rhead0 = a->read_head[g];
-        ro_load(&ro, rword0, rhead0, a->read_count[g], mb);
+        ro_load(&ro, a, g, mb);
         rn0 = ro.n;
         /* lastPendingRequestCtx (raft.go:525-532) */
         dctx = ro.n ? ro.ctx[ro.n - 1] : 0;
@@ -1355,10 +1381,21 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
             uint32_t cx = m->read_ctx ? m->read_ctx[off] : dctx;
             int j = ro_find(&ro, cx);
             if (j >= 0) {
+              uint32_t n_old = ro.n;
               ro.acks[j] |= 1u << s;
               rtouch = 1;
-              if (orc_joint_vote(mi, mo, ro.acks[j], ro.acks[j]) == VOTE_WON)
-                released += ro_advance(&ro, cx);
+              int won = orc_joint_vote(mi, mo, ro.acks[j], ro.acks[j]) == VOTE_WON;
+              /* an entry past the word: read from the ring, written back
+               * unless released (device-form accounting, ABI 7) */
+              if (j >= READ_QUEUE) ovfB += won ? mb : 2 * mb;
+              if (won) {
+                uint32_t r = ro_advance(&ro, cx);
+                released += r;
+                /* the entries that move into the word are read from the ring */
+                if (n_old > READ_QUEUE)
+                  for (uint32_t q = 0; q < READ_QUEUE; q++)
+                    if (q < ro.n && q + r >= READ_QUEUE) ovfB += mb;
+              }
             }
           }
         } else if (ty == M_SNAP_STATUS || ty == M_SNAP_STATUS_REJECT) {
@@ -1426,6 +1463,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
         B += released ? 5 : 0;
         B += (tc && m->term_commit_index) ? 8 : 0;
         B += (a->lead_transferee && lt != lt0) ? 1 : 0;
+        B += ovfB;
         lbytes += B;
       }
       for (uint32_t s = 0; s < S; s++) pr_store2(&prs[s], a, s, g);
@@ -1435,6 +1473,7 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
       if (m->timeout_now) st_mask(m->timeout_now, mb, g, tnow);
       if (m->bcast) m->bcast[g] = (uint8_t)bc;
       if (wq) ro_word_set(a->read_acks, mb, g, rword);
+      if (rd && a->read_ovf) ro_store_ovf(&ro, a, g, mb);
       if (rd && released) {
         a->read_head[g] = rhead0 + released;
         a->read_count[g] = (uint8_t)ro.n;
@@ -1510,8 +1549,8 @@ void orc_check_quorum_batch(const orc_prog *a, uint8_t *qa, uint64_t *stats) {
  *   queue of READ_QUEUE requests (or exhausted numbers) -> full (the
  *   engine's limit, nothing changes).
  * result: 1 respond, 2 postponed, 3 queued, 4 full (QE_RI_*). */
-void orc_read_index_batch(const orc_prog *a, const uint8_t *request, uint32_t lease_based,
-                          uint8_t *result, uint32_t *ctx, uint64_t *index) {
+void orc_read_index_batch(const orc_prog *a, const uint8_t *request, const uint64_t *key,
+                          uint32_t lease_based, uint8_t *result, uint32_t *ctx, uint64_t *index) {
   uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
   uint32_t full = (1u << S) - 1u;
   for (uint64_t g = 0; g < a->G; g++) {
@@ -1535,18 +1574,31 @@ void orc_read_index_batch(const orc_prog *a, const uint8_t *request, uint32_t le
       continue;
     }
     orc_ro ro;
-    uint32_t head = a->read_head[g];
-    ro_load(&ro, ro_word_get(a->read_acks, mb, g), head, a->read_count[g], mb);
+    uint32_t head = a->read_head[g], cap = ro_cap(a);
+    ro_load(&ro, a, g, mb);
     if (ro.n == 0 && head == 0) head = 1; /* context numbers start at 1 */
-    if (ro.n >= READ_QUEUE || head + ro.n == 0u) {
+    /* addRequest ignores a request already pending (read_only.go:57-60):
+     * the keys stand for the context bytes (ABI 7) */
+    uint64_t *keys = (key && a->read_keys) ? a->read_keys + g * cap : NULL;
+    int dup = -1;
+    for (uint32_t j = 0; keys && j < ro.n && dup < 0; j++)
+      if (keys[(head + j) % cap] == key[g]) dup = (int)j;
+    if (dup >= 0) {
+      result[g] = 5; /* QE_RI_DUPLICATE */
+      if (ctx) ctx[g] = head + (uint32_t)dup;
+      continue;
+    }
+    if (ro.n >= cap || head + ro.n == 0u) {
       result[g] = 4;
       continue;
     }
     uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
     ro.ctx[ro.n] = head + ro.n;                              /* addRequest */
     ro.acks[ro.n] = self < S ? 1u << self : 0u;              /* recvAck(r.id) */
+    if (keys) keys[(head + ro.n) % cap] = key[g];
     ro.n++;
     ro_word_set(a->read_acks, mb, g, ro_word(&ro, mb));
+    if (a->read_ovf) ro_store_ovf(&ro, a, g, mb);
     a->read_head[g] = head;
     a->read_count[g] = (uint8_t)ro.n;
     result[g] = 3;
@@ -1871,7 +1923,7 @@ void orc_heartbeat_batch(const orc_prog *a, uint64_t *commit, uint32_t *ctx, voi
       uint32_t cx = 0;
       if (a->read_acks) {
         orc_ro ro;
-        ro_load(&ro, ro_word_get(a->read_acks, mb, g), a->read_head[g], a->read_count[g], mb);
+        ro_load(&ro, a, g, mb);
         cx = ro.n ? ro.ctx[ro.n - 1] : 0;
       }
       ctx[g] = cx;

@@ -78,7 +78,7 @@ def _heartbeat_round(be, S, slots, ctx=None):
     return be.step(t, z, z, z, ctx=c)
 
 
-QUEUED, RESPOND, POSTPONED, FULL = 3, 1, 2, 4
+QUEUED, RESPOND, POSTPONED, FULL, DUPLICATE = 3, 1, 2, 4, 5
 
 
 def read_only_option_safe(be):
@@ -268,6 +268,42 @@ def two_reads_in_flight(be):
     # makes e's acks {1, 2} a quorum and advance releases d and e together;
     # slot 2's response then finds d gone
     out = _heartbeat_round(be, S, (1, 2), ctx={1: e, 2: d})
+    assert out["read_released"] == 2 and be.queue()[0] == 0
+
+
+def read_queue_deep_and_duplicates(be):
+    """ABI 7: a queue longer than the word (readIndexQueue is unbounded in
+    the reference, read_only.go:56-63; here a capacity of 8) and
+    addRequest's duplicate drop (:57-60) by request key.  Eight requests
+    queue (four in the word, four in the overflow ring); a ninth is over the
+    capacity; a resent request (its key pending) is a duplicate naming the
+    pending context, nothing queued.  A heartbeat response for the seventh
+    request -- an overflow entry -- makes its acks a quorum: advance
+    releases the seven oldest at once and the eighth moves into the word; a
+    response for a released context records nothing; MsgBeat carries the
+    newest context; the next response releases the last one."""
+    S = 3
+    sc = _leader_after_hup(S)
+    be.load(sc, initial_arrays(sc), read_cap=8)
+    got = [be.read_index(key=100 + k) for k in range(8)]
+    assert [r for r, _, _ in got] == [QUEUED] * 8
+    ctxs = [c for _, c, _ in got]
+    assert ctxs == list(range(ctxs[0], ctxs[0] + 8))
+    assert be.read_index(key=200)[0] == FULL
+    res, ctx, _ = be.read_index(key=103)  # resent: pending already
+    assert (res, ctx) == (DUPLICATE, ctxs[3]) and be.queue()[0] == 8
+    n, head, acks = be.queue()
+    assert (n, head) == (8, ctxs[0]) and acks == [0b001] * 8  # the leader's own acks
+    out = _heartbeat_round(be, S, (1,), ctx=ctxs[6])
+    assert out["read_released"] == 7
+    assert be.queue() == (1, ctxs[7], [0b001])
+    out = _heartbeat_round(be, S, (2,), ctx=ctxs[5])  # released: nothing recorded
+    assert out["read_released"] == 0 and be.queue() == (1, ctxs[7], [0b001])
+    _, hctx, _ = be.heartbeat()
+    assert hctx == ctxs[7]
+    res, ctx, _ = be.read_index(key=103)  # released: a fresh request now
+    assert (res, ctx) == (QUEUED, ctxs[7] + 1)
+    out = _heartbeat_round(be, S, (2,), ctx=ctxs[7] + 1)
     assert out["read_released"] == 2 and be.queue()[0] == 0
 
 
@@ -654,7 +690,7 @@ def switch_removed_or_demoted_leader(be):
 SCENARIOS = [read_only_option_safe, read_only_with_learner, read_only_option_lease,
              raft_frees_read_only_mem, read_only_for_new_leader,
              postponed_read_commit_advances_twice, two_reads_in_flight,
-             read_queue_full, learner_ack_does_not_count,
+             read_queue_full, read_queue_deep_and_duplicates, learner_ack_does_not_count,
              leader_stepdown_when_quorum_active, leader_stepdown_when_quorum_lost,
              add_node_check_quorum, leader_transfer_to_up_to_date_node,
              leader_transfer_to_slow_follower, leader_transfer_to_self,
@@ -673,7 +709,7 @@ class OracleRoundBackend:
     def __init__(self, orc):
         self.orc = orc
 
-    def load(self, sc, a, inc=None, tracked=None, out=None):
+    def load(self, sc, a, inc=None, tracked=None, out=None, read_cap=0):
         S = sc["S"]
         pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
         a = dict(a)
@@ -687,7 +723,7 @@ class OracleRoundBackend:
             pb.tracked = np.array([tracked], md)
         if out is not None:
             pb.out = np.array([out], md)
-        pb.track_reads()
+        pb.track_reads(read_cap, keys=True)
         self.pb, self.sc = pb, sc
         self.pci = self.unc = self.applied = self.max_unc = 0  # MsgProp state (qe_propose)
 
@@ -703,8 +739,9 @@ class OracleRoundBackend:
         commit, ctx, sent = self.orc.heartbeat(self.pb)
         return [int(x) for x in commit[: self.sc["S"]]], int(ctx[0]), int(sent[0])
 
-    def read_index(self, lease_based=False):
-        r, c, i = self.orc.read_index(self.pb, np.ones(1, np.uint8), lease_based)
+    def read_index(self, lease_based=False, key=None):
+        k = None if key is None else np.array([key], np.uint64)
+        r, c, i = self.orc.read_index(self.pb, np.ones(1, np.uint8), lease_based, key=k)
         return int(r[0]), int(c[0]), int(i[0])
 
     def queue(self):
@@ -712,7 +749,9 @@ class OracleRoundBackend:
         n, head = int(pb.read_count[0]), int(pb.read_head[0])
         mb = 1 if self.sc["S"] <= 8 else 2
         w = int(pb.read_acks[0])
-        return n, head, [(w >> (8 * mb * j)) & ((1 << (8 * mb)) - 1) for j in range(n)]
+        cap = max(4, pb.read_cap)
+        return n, head, [((w >> (8 * mb * j)) & ((1 << (8 * mb)) - 1)) if j < 4 else
+                         int(pb.read_ovf[(head + j) % cap]) for j in range(n)]
 
     def transferee(self):
         return int(self.pb.lead_transferee[0])

@@ -63,7 +63,8 @@ int main(void) {
   Z(qe_progress) F(qe_progress, peer) F(qe_progress, infl_lo) F(qe_progress, infl_hi) F(qe_progress, log_runs)
   F(qe_progress, out_mask) F(qe_progress, tracked) F(qe_progress, snap_index)
   F(qe_progress, max_ents) F(qe_progress, read_acks) F(qe_progress, read_head)
-  F(qe_progress, read_count) F(qe_progress, lead_transferee)
+  F(qe_progress, read_count) F(qe_progress, lead_transferee) F(qe_progress, read_cap)
+  F(qe_progress, read_ovf) F(qe_progress, read_keys)
   Z(qe_peer_msgs) F(qe_peer_msgs, bcast) F(qe_peer_msgs, timeout_now) F(qe_peer_msgs, msg_index)
   F(qe_peer_msgs, bytes_requested) F(qe_peer_msgs, read_ctx) F(qe_peer_msgs, read_released)
   F(qe_peer_msgs, term_commit) F(qe_peer_msgs, term_commit_index)
@@ -115,7 +116,8 @@ def test_constants_and_introspection():
                       ("QE_PF_RECENT_ACTIVE", 8), ("QE_PW_START_SHIFT", 8),
                       ("QE_PW_COUNT_SHIFT", 16), ("QE_PF_RING_WIDE", 16),
                       ("QE_MSG_TRANSFER_LEADER", 7), ("QE_READ_QUEUE", 4), ("QE_RI_RESPOND", 1),
-                      ("QE_RI_POSTPONED", 2), ("QE_RI_QUEUED", 3), ("QE_RI_FULL", 4)]:
+                      ("QE_RI_POSTPONED", 2), ("QE_RI_QUEUED", 3), ("QE_RI_FULL", 4),
+                      ("QE_RI_DUPLICATE", 5), ("QE_READ_CAP_MAX", 255)]:
         m = re.search(rf"#define {name} \(?(-?\d+)u?\)?", src)
         assert m and int(m.group(1)) == val, name
 
@@ -150,14 +152,14 @@ def test_argument_errors_without_gpu():
     assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_EINVAL
     pr = _lib.QeProgress(num_groups=0, num_slots=3)  # empty batch is a no-op
     assert L.qe_check_quorum(C.byref(pr), None, None, None) == _lib.QE_OK
-    assert L.qe_read_index(C.byref(pr), None, 0, None, None, None, None) == _lib.QE_OK
-    assert L.qe_read_index(None, None, 0, None, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_read_index(C.byref(pr), None, None, 0, None, None, None, None) == _lib.QE_OK
+    assert L.qe_read_index(None, None, None, 0, None, None, None, None) == _lib.QE_EINVAL
     v = C.c_void_p(64)
     pr = _lib.QeProgress(num_groups=4, num_slots=3, inflight_cap=4, stride=4, committed=v,
                          term_start=v, last_index=v)
     # ReadOnlySafe needs the queue; LeaseBased does not
-    assert L.qe_read_index(C.byref(pr), v, 0, v, None, None, None) == _lib.QE_EINVAL
-    assert L.qe_read_index(C.byref(pr), None, 1, v, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_read_index(C.byref(pr), v, None, 0, v, None, None, None) == _lib.QE_EINVAL
+    assert L.qe_read_index(C.byref(pr), None, None, 1, v, None, None, None) == _lib.QE_EINVAL
     # a queue comes whole or not at all (qe_progress_step)
     pr = _lib.QeProgress(num_groups=4, num_slots=3, inflight_cap=4, stride=4, log_runs=1,
                          match=v, next=v, pending_snapshot=v, peer=v, infl_lo=v, infl_hi=v,

@@ -110,8 +110,10 @@ def random_msgs(rng, pb):
 
 
 def to_device(eng, pb, masks, extras=()):
+    if pb.read_keys is not None:
+        extras = tuple(extras) + ("read_keys",)
     ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride,
-                           extras=extras, max_ents=pb.max_ents)
+                           extras=extras, max_ents=pb.max_ents, read_cap=pb.read_cap)
     md = orc.mask_dtype(pb.S)
     ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, peer=pb.pw,
                  ibuf=pb.ibuf, committed=pb.committed,
@@ -120,7 +122,9 @@ def to_device(eng, pb, masks, extras=()):
                  inc=pb.inc, out=pb.out, tracked=pb.tracked, self_slot=pb.self_slot,
                  lead_transferee=pb.lead_transferee, snap_index=pb.snap_index,
                  read_acks=None if pb.read_acks is None else pb.read_acks.view(md),
-                 read_head=pb.read_head, read_count=pb.read_count)
+                 read_head=pb.read_head, read_count=pb.read_count,
+                 read_ovf=None if pb.read_ovf is None else pb.read_ovf.view(md),
+                 read_keys=pb.read_keys)
     return ps
 
 
@@ -151,6 +155,10 @@ def assert_same(ps, pb):
                                       err_msg="read_acks")
         np.testing.assert_array_equal(h["read_head"], pb.read_head, err_msg="read_head")
         np.testing.assert_array_equal(h["read_count"], pb.read_count, err_msg="read_count")
+        if pb.read_ovf is not None:  # ABI 7: the overflow ring, raw (dead slots untouched)
+            np.testing.assert_array_equal(h["read_ovf"], pb.read_ovf, err_msg="read_ovf")
+        if pb.read_keys is not None:
+            np.testing.assert_array_equal(h["read_keys"], pb.read_keys, err_msg="read_keys")
     np.testing.assert_array_equal(h["peer"] & ~RING_MASK, pb.pw, err_msg="packed peer words")
     live = live_entries(pb.pw, pb.S, pb.F, pb.stride)
     np.testing.assert_array_equal(h["ibuf"][live], pb.ibuf[live], err_msg="live ring entries")
@@ -452,11 +460,12 @@ class GpuBackend:
     def __init__(self, eng):
         self.eng = eng
 
-    def load(self, sc, a, inc=None, tracked=None, out=None):
+    def load(self, sc, a, inc=None, tracked=None, out=None, read_cap=0):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
         masks = (("inc",) if inc is not None else ()) + (("out",) if out is not None else ())
         ps = self.eng.ProgressState(1, sc["S"], cap(sc), len(sc["log"]["runs"]), DEV, stride=1,
-                                    extras=READS, max_ents=sc["max_ents"], masks=masks)
+                                    extras=READS + ("read_keys",), max_ents=sc["max_ents"],
+                                    masks=masks, read_cap=read_cap)
         if tracked is None:
             ps.tracked = None  # every slot holds a Progress (as the oracle backend)
         else:
@@ -491,17 +500,19 @@ class GpuBackend:
         c = commit.cpu().numpy().view(np.uint64)[: self.sc["S"] * st: st]
         return [int(x) for x in c], int(ctx[0]) & 0xFFFFFFFF, int(sent[0])
 
-    def read_index(self, lease_based=False):
+    def read_index(self, lease_based=False, key=None):
         req = torch.ones(1, dtype=torch.uint8, device=DEV)
-        r, c, i = self.eng.read_index(self.ps, req, lease_based)
+        k = None if key is None else torch.tensor([key], dtype=torch.int64, device=DEV)
+        r, c, i = self.eng.read_index(self.ps, req, lease_based, key=k)
         return int(r[0]), int(c[0]) & 0xFFFFFFFF, int(i[0])
 
     def queue(self):
         ps = self.ps
         n, head = int(ps.read_count[0]), int(ps.read_head[0]) & 0xFFFFFFFF
-        mask = (1 << self.sc["S"]) - 1
-        acks = [int(ps.read_acks[j]) & 0xFFFF for j in range(n)]
-        return n, head, [a & 0xFFFF if self.sc["S"] > 8 else a & 0xFF for a in acks]
+        cap = max(4, ps.read_cap)
+        m = 0xFFFF if self.sc["S"] > 8 else 0xFF
+        return n, head, [(int(ps.read_acks[j]) if j < 4 else int(ps.read_ovf[(head + j) % cap])) & m
+                         for j in range(n)]
 
     def transferee(self):
         return int(self.ps.lead_transferee[0])

@@ -37,13 +37,13 @@ def random_proposals(rng, pb, max_cc):
     payload = np.where(rng.random(G) < 0.3, 0, rng.integers(1, 40, G)).astype(np.uint64)
     cnt = (rng.integers(0, max_cc + 1, G) * (rng.random(G) < 0.5)).astype(np.uint8)
     cnt = np.minimum(cnt, ne).astype(np.uint8)
-    if max_cc:  # more conf-change entries than max_cc: QE_PROP_BAD_CC, refused whole
-        cnt[rng.random(G) < 0.05] = max_cc + 1
     m = max(1, max_cc)
     pos = np.zeros((m, G), np.uint32)
     for g in range(G):
         if cnt[g]:
             pos[: cnt[g], g] = np.sort(rng.choice(int(ne[g]), int(cnt[g]), replace=False))
+    if max_cc:  # more conf-change entries than max_cc: QE_PROP_BAD_CC, refused whole
+        cnt[(rng.random(G) < 0.05) & (ne > 0)] = max_cc + 1
     leave = (rng.random((m, G)) < 0.4).astype(np.uint8)
     size = rng.integers(0, 30, (m, G)).astype(np.uint32)
     li = pb.last_index.astype(np.int64)
