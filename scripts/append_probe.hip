@@ -69,6 +69,22 @@ __global__ __launch_bounds__(256) void lm32_rmw(u32 *R, size_t G) {
   r[0] = a;
   r[1] = b;
 }
+// lane-major u16 ring = 16 B per peer (round 6: the 16-bit offsets the
+// Inflights rings would need): one dwordx4 load + one store;
+// two peers share a 32-B sector
+typedef unsigned short u16;
+__global__ __launch_bounds__(256) void lm16_rmw(u16 *R, size_t G) {
+  const size_t g = blockIdx.x * 256ull + threadIdx.x;
+  u32x4 *r = reinterpret_cast<u32x4 *>(R + g * 8);
+  u32x4 a = r[0];
+  const u32 p = pos_of(g), v = (u32)(g + 1) & 0xFFFFu;
+  const u32 sh = (p & 1u) * 16u, keep = ~(0xFFFFu << sh), nv = v << sh;
+  a.x = (p >> 1) == 0 ? (a.x & keep) | nv : a.x;
+  a.y = (p >> 1) == 1 ? (a.y & keep) | nv : a.y;
+  a.z = (p >> 1) == 2 ? (a.z & keep) | nv : a.z;
+  a.w = (p >> 1) == 3 ? (a.w & keep) | nv : a.w;
+  r[0] = a;
+}
 // tile-blocked u32 block (2 KB per 64 peers) loaded and stored whole, 16 B
 // per lane per instruction, the append applied through LDS
 __global__ __launch_bounds__(256) void tb32_rmw(u32 *R, size_t G) {
@@ -147,6 +163,11 @@ int main() {
   rep("lm32 rmw", t, G, 4);
   t = bench([&] { hipLaunchKernelGGL(tb32_rmw, grid, blk, 0, 0, R32, G); });
   rep("tb32 rmw", t, G, 4);
+  u16 *R16 = static_cast<u16 *>(R);
+  t = bench([&] { hipLaunchKernelGGL(lm_scatter<u16>, grid, blk, 0, 0, R16, G); });
+  rep("lm16 scatter", t, G, 2);
+  t = bench([&] { hipLaunchKernelGGL(lm16_rmw, grid, blk, 0, 0, R16, G); });
+  rep("lm16 rmw", t, G, 2);
   (void)hipDeviceSynchronize();
   printf("done\n");
   return 0;

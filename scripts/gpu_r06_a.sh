@@ -4,7 +4,7 @@
 # line and its per-workload rocprofv3 passes.  Logs under gpurun_out/$TAG/.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 T=${TAG:-r06a}; O=gpurun_out/$T; mkdir -p "$O"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_switch.py tests/test_gpu_trace_tiles.py tests/test_gpu_readindex.py tests/test_gpu_comm.py -m gpu -x -q \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_switch.py tests/test_gpu_trace_tiles.py tests/test_gpu_readindex.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py -m gpu -x -q \
   -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/new_tests.log" 2>&1 || { echo "new tests failed"; tail -40 "$O/new_tests.log"; exit 2; }
 tail -1 "$O/new_tests.log"
 if [ "${FULL:-1}" = 1 ]; then
