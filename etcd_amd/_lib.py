@@ -132,6 +132,15 @@ class QeSwitch(C.Structure):  # ABI 7
                 ("bytes_requested", vp)]
 
 
+class QeLeader(C.Structure):  # ABI 7
+    _fields_ = [("elected", vp), ("term", vp), ("flags", u32), ("reserved", u32),
+                ("pending_conf_index", vp), ("uncommitted_size", vp), ("result", vp),
+                ("sent", vp), ("snap", vp)]
+
+
+QE_BL_NONE, QE_BL_LEADER, QE_BL_NOT_MEMBER, QE_BL_RUNS_FULL = 0, 1, 2, 3
+QE_BL_BCAST = 1
+
 QE_SW_NONE, QE_SW_REMOVED, QE_SW_NO_VOTERS, QE_SW_BCAST, QE_SW_PROBE = 0, 1, 2, 3, 4
 QE_SW_OUTCOME, QE_SW_TRANSFER_ABORTED = 0x0F, 0x10
 
@@ -221,6 +230,7 @@ PROTOTYPES = {
     "qe_propose": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeProposals), vp, vp]),
     "qe_heartbeat": (C.c_int, [C.POINTER(QeProgress), vp, vp, vp, vp]),
     "qe_switch_config": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeSwitch), vp, vp]),
+    "qe_become_leader": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeLeader), vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),

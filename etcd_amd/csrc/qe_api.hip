@@ -536,6 +536,27 @@ int qe_switch_config(const qe_progress *p, const qe_switch *sw, uint64_t *stats,
                            p->out_mask != nullptr, static_cast<hipStream_t>(stream));
 }
 
+int qe_become_leader(const qe_progress *p, const qe_leader *l, uint64_t *stats, void *stream) {
+  PArgs a;
+  int rc = progress_args(p, a);
+  if (rc) return rc;
+  if (!l || l->reserved || (l->flags & ~QE_BL_BCAST)) return QE_EINVAL;
+  if (p->num_groups == 0) return QE_OK;
+  if (!l->term || !l->result || !p->self_slot) return QE_EINVAL;
+  if (p->log_runs && !p->run_count) return QE_EINVAL;
+  a.bl_elected = l->elected;
+  a.bl_term = l->term;
+  a.bl_flags = l->flags;
+  a.bl_pci = l->pending_conf_index;
+  a.bl_unc = l->uncommitted_size;
+  a.bl_result = l->result;
+  a.sent = l->sent;
+  a.snap = l->snap;
+  a.stats = stats;
+  return dispatch_progress(p->num_slots, a, 10, p->inc_mask != nullptr, p->out_mask != nullptr,
+                           static_cast<hipStream_t>(stream));
+}
+
 int qe_heartbeat(const qe_progress *p, uint64_t *commit, uint32_t *ctx, void *sent, void *stream) {
   if (!p) return QE_EINVAL;
   if (p->num_slots == 0 || p->num_slots > QE_MAX_SLOTS || p->reserved || p->reserved2)

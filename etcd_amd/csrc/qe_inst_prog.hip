@@ -121,6 +121,14 @@ static int launch_switch_config(const PArgs &a, bool masked, bool joint, hipStre
   return hip_status(hipGetLastError());
 }
 
+static int launch_become_leader(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  if (joint) hipLaunchKernelGGL((k_become_leader<S, MT, true, true>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_become_leader<S, MT, true, false>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_become_leader<S, MT, false, false>), grid, dim3(kBlock), 0, st, a);
+  return hip_status(hipGetLastError());
+}
+
 static int launch_heartbeat(PArgs a, hipStream_t st) {
   if (g_hb_kernel == 0) {  // round 5's one-tile-per-wave form (A/B)
     const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
@@ -147,7 +155,7 @@ static int launch_heartbeat(PArgs a, hipStream_t st) {
 // byte accounting (instrumented variant, measurement only), 3:
 // qe_check_quorum, 4: qe_read_index, 5: qe_propose, 6: qe_propose with byte
 // accounting, 7: qe_heartbeat, 8: qe_switch_config, 9: qe_switch_config with
-// byte accounting
+// byte accounting, 10: qe_become_leader
 int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool joint,
                                      hipStream_t st) {
   if (kind == 1) return launch_progress_send(a, st);
@@ -158,6 +166,7 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
   if (kind == 7) return launch_heartbeat(a, st);
   if (kind == 8) return launch_switch_config<false>(a, masked, joint, st);
   if (kind == 9) return launch_switch_config<true>(a, masked, joint, st);
+  if (kind == 10) return launch_become_leader(a, masked, joint, st);
   // run table (staged in LDS, l_run): 4 runs cover the common leader log (one
   // or two older terms before the current one); 8 keep the block's LDS at
   // 52 KB (3 blocks per CU at S = 5, where 16 runs' 84 KB allow one);

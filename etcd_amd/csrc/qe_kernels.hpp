@@ -766,6 +766,12 @@ struct PArgs {
   // switchToConfig (qe_switch_config, ABI 7)
   const uint8_t *sw_switched;
   uint8_t *sw_result;
+  // becomeLeader (qe_become_leader, ABI 7)
+  const uint8_t *bl_elected;
+  const uint64_t *bl_term;
+  uint32_t bl_flags;
+  uint64_t *bl_pci, *bl_unc;
+  uint8_t *bl_result;
 };
 
 struct PR {

@@ -1931,6 +1931,167 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
   acct_flush<ACCT>(ac, a.acct);
 }
 
+// qe_become_leader (ABI 7): raft.becomeLeader (raft/raft.go:724-759) with the
+// reset it starts with (:590-613), the empty entry's appendEntry and, with
+// QE_BL_BCAST, stepCandidate's bcastAppend.  One lane per group, a wave per
+// tile; reset writes every tracked slot's Progress without reading it (the
+// new values are constants of lastIndex), so a group costs its log model,
+// one write per Progress field and the probes' sends.
+constexpr uint64_t kLeaderSalt = 0x6A09E667BB67AE85ull;
+
+template <int S, typename MT, bool MASKED, bool JOINT>
+__global__ __launch_bounds__(kBlock) void k_become_leader(PArgs a) {
+  constexpr uint32_t kFull = (1u << S) - 1u;
+  constexpr uint32_t MB = sizeof(MT);
+  uint64_t cnt[Q_N] = {0, 0, 0, 0};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t ntiles = (a.G + 63) / 64;
+  const bool bcast = (a.bl_flags & QE_BL_BCAST) != 0;
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t g0 = t * 64;
+    const uint32_t n = tile_n(a.G, t);
+    const bool live = lane < n;
+    const uint32_t o8 = lane * 8, o4 = lane * 4;
+    const bool el = a.bl_elected ? bld8(mk_rsrc(a.bl_elected + g0, n), lane) != 0 : live;
+    const uint32_t o1 = el ? lane : kOOB;
+    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), o1) : 0xFFu;
+    const uint32_t trk =
+        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * MB), lane) & kFull)
+                  : kFull;
+    const uint32_t mi = MASKED ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.inc) + g0, n * MB), lane) & kFull)
+                               : kFull;
+    const uint32_t mo = JOINT ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.out) + g0, n * MB), lane) & kFull)
+                              : 0u;
+    const rsrc_t r_li = mk_rsrc(a.last_index + g0, n * 8), r_c = mk_rsrc(a.committed + g0, n * 8);
+    const uint64_t li = bld64(r_li, el ? o8 : kOOB);
+    const uint64_t c0 = bld64(r_c, o8);
+    const uint32_t rc = (a.R && a.run_count) ? bld8(mk_rsrc(a.run_count + g0, n), o1) : 0u;
+    const bool member = self < static_cast<uint32_t>(S) && ((trk >> self) & 1u) != 0;
+    // (a full run table refuses only when a new run is needed; checked
+    // against the last run's term below, conservatively here)
+    const uint32_t res = !el ? QE_BL_NONE
+                             : (!member ? QE_BL_NOT_MEMBER
+                                        : ((a.R && rc >= a.R) ? QE_BL_RUNS_FULL : QE_BL_LEADER));
+    const bool go = res == QE_BL_LEADER;
+    const uint32_t k8 = go ? o8 : kOOB;
+    const uint64_t term = bld64(mk_rsrc(a.bl_term + g0, n * 8), k8);
+    const uint64_t fi = bld64(mk_rsrc(a.first_index + g0, n * 8), k8);
+    const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
+    uint64_t c = c0;
+    uint32_t sentm = 0, snapm = 0;
+    if (__builtin_amdgcn_ballot_w64(go)) {
+      const uint64_t li2 = li + 1;  // the empty entry (appendEntry)
+      // the log model enters the term: a run of `term` from lastIndex + 1 --
+      // unless the log's last run has that term already (a bootstrap
+      // snapshot of the new leader's own term): the term then starts there
+      uint64_t ts2 = li2;
+      if (a.R) {
+        bool same = false;
+        for (uint32_t r = 0; r < a.R; r++) {  // the last run, a row per lane
+          const bool on = go && rc == r + 1;
+          if (!__builtin_amdgcn_ballot_w64(on)) continue;
+          const uint64_t row = static_cast<uint64_t>(r) * a.stride + g0;
+          const uint64_t f = bld64(mk_rsrc(a.run_first + row, n * 8), on ? o8 : kOOB);
+          const uint64_t tt = bld64(mk_rsrc(a.run_term + row, n * 8), on ? o8 : kOOB);
+          if (on && tt == term) {
+            same = true;
+            ts2 = f;
+          }
+        }
+        for (uint32_t r = 0; r < a.R; r++) {
+          const bool on = go && !same && rc == r;
+          if (!__builtin_amdgcn_ballot_w64(on)) continue;
+          const uint64_t row = static_cast<uint64_t>(r) * a.stride + g0;
+          bst64(li2, mk_rsrc(a.run_first + row, n * 8), on ? o8 : kOOB);
+          bst64(term, mk_rsrc(a.run_term + row, n * 8), on ? o8 : kOOB);
+        }
+        bst8(rc + 1, mk_rsrc(a.run_count + g0, n), (go && !same) ? lane : kOOB);
+      }
+      bst64(ts2, mk_rsrc(a.term_start + g0, n * 8), k8);
+      bst64(li2, r_li, k8);
+      if (a.transferee) bst8(0xFFu, mk_rsrc(a.transferee + g0, n), go ? lane : kOOB);
+      if (a.read_acks) {  // newReadOnly: nothing pending, the old numbers never reused
+        const uint32_t qn = bld8(mk_rsrc(a.read_count + g0, n), go ? lane : kOOB);
+        const uint32_t qh = bld32(mk_rsrc(a.read_head + g0, n * 4), go ? o4 : kOOB);
+        const uint32_t q = qn < a.read_cap ? qn : a.read_cap;
+        bst32(qh + q, mk_rsrc(a.read_head + g0, n * 4), go ? o4 : kOOB);
+        bst8(0u, mk_rsrc(a.read_count + g0, n), go ? lane : kOOB);
+      }
+      if (a.bl_pci) bst64(li, mk_rsrc(a.bl_pci + g0, n * 8), k8);
+      if (a.bl_unc) bst64(0, mk_rsrc(a.bl_unc + g0, n * 8), k8);
+      // maybeCommit with the leader's own Match at the empty entry (the
+      // others are 0 after reset): a one-voter config commits it
+      uint64_t vals[S];
+#pragma unroll
+      for (int s = 0; s < S; s++) vals[s] = self == static_cast<uint32_t>(s) ? li2 : 0;
+      const uint64_t mci = mci_of<S, MASKED, JOINT>(vals, mi, mo);
+      if (go && mci > c0 && mci >= ts2 && mci <= li2) c = mci;
+      bst64(c, r_c, c != c0 ? o8 : kOOB);
+      PSend x;
+      x.F = a.F;
+      x.me = a.max_ents;
+      x.fi = fi;
+      x.li = li2;
+      x.snap = sn;
+      x.lb = lane * a.FP * 4;
+      x.row = false;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+        const bool tr = go && ((trk >> s) & 1u) != 0;
+        const bool is_self = self == static_cast<uint32_t>(s);
+        PR p;  // reset: Match 0, Next lastIndex + 1, StateProbe, empty Inflights
+        p.match = is_self ? li2 : 0;  // (the leader: lastIndex, then MaybeUpdate(li2))
+        p.next = is_self ? li2 + 1 : li + 1;
+        p.pending = 0;
+        p.reset = 0;
+        p.state = is_self ? QE_PR_REPLICATE : QE_PR_PROBE;
+        p.probe_sent = p.recent_active = p.start = p.count = 0;
+        p.rep = 0;
+        const bool tgt = bcast && tr && !is_self;
+        if (__builtin_amdgcn_ballot_w64(tgt)) {
+          const uint64_t rb = row * a.FP;
+          x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
+          x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+          x.count_msgs = 0;
+          x.first_index = 0;
+          x.snapped = false;
+          PRun run{0, 0, 0};
+          Acct<false> ac;
+          send_burst<false>(p, true, tgt ? 1u : 0u, x, run, ac);
+          sentm |= (tgt && x.count_msgs) ? (1u << s) : 0u;
+          snapm |= (tgt && x.snapped) ? (1u << s) : 0u;
+        }
+        const uint32_t off8 = tr ? o8 : kOOB;
+        bst64(p.match, mk_rsrc(a.match + row, n * 8), off8);
+        bst64(p.next, mk_rsrc(a.next + row, n * 8), off8);
+        bst64(p.pending, mk_rsrc(a.pending + row, n * 8), off8);
+        bst32(pr_pack(p), mk_rsrc(a.pw + row, n * 4), tr ? o4 : kOOB);
+      }
+    }
+    bst8(res, mk_rsrc(a.bl_result + g0, n), lane);
+    if (a.sent) bst_mask<MT>(sentm, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
+    if (a.snap) bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
+    if (live) {
+      const uint64_t gh = (a.goff + g0 + lane) * kPhi;
+      cnt[Q_GROUPS] += 1;
+      cnt[Q_SUM] += c;
+      cnt[Q_ADV] += c != c0;
+      cnt[Q_CSUM] += mix64(gh ^ kLeaderSalt ^ (static_cast<uint64_t>(res) << 56) ^ c) +
+                     mix64(gh ^ kSentSalt ^ (static_cast<uint64_t>(sentm) << 40) ^
+                           (static_cast<uint64_t>(snapm) << 20));
+    }
+  }
+  if (a.stats) {
+    const int idx[Q_N] = {QE_STAT_GROUPS, QE_STAT_COMMIT_SUM, QE_STAT_COMMIT_ADVANCED,
+                          QE_STAT_CHECKSUM};
+    block_stats_add<Q_N, kBlock>(cnt, idx, a.stats);
+  }
+}
+
 // qe_heartbeat (ABI 6): MsgBeat -> bcastHeartbeat (raft/raft.go:524-541):
 // per group the context of the newest pending ReadIndex request, per peer
 // (every tracked slot but the leader's) Commit = min(Match, committed)

@@ -738,6 +738,40 @@ def switch_bytes_requested(ps, sw):
     return int(acct.item())
 
 
+class Leader:
+    """One qe_become_leader call's per-group inputs and outputs (qe_leader,
+    ABI 7): elected [G] (None = every group), term [G], pending_conf_index /
+    uncommitted_size [G] outputs, result [G] (QE_BL_*), sent / snap masks."""
+
+    def __init__(self, ps, elected=None, bcast=True):
+        G, dev = ps.G, ps.device
+        self.elected = elected
+        self.term = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.flags = _lib.QE_BL_BCAST if bcast else 0
+        self.pending_conf_index = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.uncommitted_size = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.result = torch.zeros(G, dtype=torch.uint8, device=dev)
+        md = mask_torch_dtype(ps.S)
+        self.sent = torch.zeros(G, dtype=md, device=dev)
+        self.snap = torch.zeros(G, dtype=md, device=dev)
+
+    def struct(self):
+        return _lib.QeLeader(_ptr(self.elected), _ptr(self.term), self.flags, 0,
+                             _ptr(self.pending_conf_index), _ptr(self.uncommitted_size),
+                             _ptr(self.result), _ptr(self.sent), _ptr(self.snap))
+
+
+def become_leader(ps, ld, stats=None):
+    """qe_become_leader: raft.becomeLeader (raft/raft.go:724-759, reset
+    :590-613) on every group with ld.elected[g] -- every Progress reset, the
+    log model enters ld.term[g], the empty entry appended and (bcast)
+    stepCandidate's bcastAppend."""
+    p, q = ps.struct(), ld.struct()
+    check("qe_become_leader", _lib.lib().qe_become_leader(C.byref(p), C.byref(q), _ptr(stats),
+                                                           _stream(ps.device)))
+    return ld
+
+
 class ConfState:
     """Device-resident tracker.Config + ProgressMap key set of G groups in
     slot form (qe_conf): slot_ids ID-major [S][G], slot masks for Voters[0],

@@ -676,6 +676,58 @@ typedef struct qe_proposals {
  * applied entries.  stats: groups, commit sum, commit advanced, checksum. */
 int qe_propose(const qe_progress *p, const qe_proposals *prop, uint64_t *stats, void *stream);
 
+/* ---- becomeLeader (ABI 7) ----------------------------------------------- */
+
+/* qe_leader.result */
+#define QE_BL_NONE 0        /* elected[g] == 0: not part of this call           */
+#define QE_BL_LEADER 1      /* becomeLeader done                                */
+#define QE_BL_NOT_MEMBER 2  /* self_slot holds no Progress: the reference would
+                               panic (a candidate is promotable, so a voter);
+                               nothing changes                               */
+#define QE_BL_RUNS_FULL 3   /* the new term's run does not fit the log model's
+                               log_runs: nothing changes (the host compacts
+                               the run table and retries)                    */
+#define QE_BL_BCAST 1u      /* qe_leader.flags: then bcastAppend, as
+                               stepCandidate does after winning (raft.go:
+                               1405-1407)                                     */
+
+typedef struct qe_leader {
+  const uint8_t *elected;        /* [G] 1: the group's node won its election
+                                    (NULL = every group)                      */
+  const uint64_t *term;          /* [G] r.Term of the new leadership           */
+  uint32_t flags;                /* QE_BL_BCAST or 0                           */
+  uint32_t reserved;             /* must be 0                                  */
+  uint64_t *pending_conf_index;  /* [G] out (may be NULL): r.pendingConfIndex =
+                                    lastIndex before the empty entry         */
+  uint64_t *uncommitted_size;    /* [G] out (may be NULL): 0 (reset; the empty
+                                    entry is not counted, raft.go:753-757)   */
+  uint8_t *result;               /* [G] out QE_BL_*                            */
+  void *sent;                    /* [G] out mask (may be NULL): bcastAppend's  */
+  void *snap;                    /* [G] out mask (may be NULL)                 */
+} qe_leader;
+
+/* raft.becomeLeader (raft/raft.go:724-759) on every group with elected[g],
+ * on the leader-side state p:
+ *   reset (:590-613): every tracked slot's Progress becomes Match 0, Next =
+ *     lastIndex + 1, StateProbe, not ProbeSent, not RecentActive, no pending
+ *     snapshot, empty Inflights; the leader's own (self_slot) Match =
+ *     lastIndex, then BecomeReplicate; lead_transferee = none; the ReadIndex
+ *     queue emptied (newReadOnly: read_count 0, read_head past the dropped
+ *     requests' context numbers, so a late response for one finds nothing);
+ *   pendingConfIndex = lastIndex; uncommittedSize = 0;
+ *   the log model enters the term: a run [lastIndex + 1, ...) of term[g] is
+ *     appended to the run table and term_start = lastIndex + 1;
+ *   appendEntry of the empty entry (:621-642): lastIndex + 1, the leader's
+ *     MaybeUpdate, maybeCommit (a one-voter config commits it at once);
+ *   QE_BL_BCAST: bcastAppend (every tracked slot but the leader's, the
+ *     probes of a new term).
+ * Writes p's Progress rows, Inflights words, committed, last_index,
+ * term_start, the run table (run_first / run_term / run_count) and
+ * lead_transferee / the queue when present (declared const in qe_progress
+ * because the other entry points only read them).  stats: groups, commit
+ * sum, commit advanced, checksum. */
+int qe_become_leader(const qe_progress *p, const qe_leader *l, uint64_t *stats, void *stream);
+
 /* ---- switchToConfig: the leader's side of an applied conf change (ABI 7) - */
 
 /* qe_switch.result & QE_SW_OUTCOME */

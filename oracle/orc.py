@@ -67,6 +67,8 @@ def _declare(L):
         "orc_checksum_prop": (u64, [u64, u32, u64, u64, u32]),
         "orc_heartbeat_batch": (None, [C.POINTER(OrcProg), vp, vp, vp]),
         "orc_switch_config_batch": (None, [C.POINTER(OrcProg), vp, vp, vp, vp, vp, vp]),
+        "orc_become_leader_batch": (None, [C.POINTER(OrcProg), vp, vp, u32, vp, vp, vp, vp, vp,
+                                           vp]),
         "orc_checksum_switch": (u64, [u64, u32, u64, u32, u32]),
         "orc_find_conflict_by_term": (u64, [u32, vp, vp, u64, u64, u64]),
         "orc_log_term": (u64, [u32, vp, vp, u64, u64]),
@@ -440,4 +442,30 @@ def switch_config(pb, switched=None, goff=0):
     s = pb.struct(goff)
     lib().orc_switch_config_batch(C.byref(s), P(sw), P(o.result), P(o.sent), P(o.snap),
                                   P(o.stats), P(o.bytes))
+    return o
+
+
+class LeaderOut:
+    def __init__(self, pb):
+        md = mask_dtype(pb.S)
+        self.result = np.zeros(pb.G, np.uint8)
+        self.pending_conf_index = np.zeros(pb.G, np.uint64)
+        self.uncommitted_size = np.zeros(pb.G, np.uint64)
+        self.sent = np.zeros(pb.G, md)
+        self.snap = np.zeros(pb.G, md)
+        self.stats = np.zeros(NSTAT, np.uint64)
+
+
+def become_leader(pb, term, elected=None, bcast=True, goff=0):
+    """raft.becomeLeader (raft/raft.go:724-759) on every group with
+    elected[g] (None = every group), entering term[g] (oracle); pb is updated
+    in place.  Returns LeaderOut (result: 0 none, 1 leader, 2 no Progress of
+    its own, 3 run table full)."""
+    o = LeaderOut(pb)
+    el = None if elected is None else np.ascontiguousarray(elected, np.uint8)
+    t = np.ascontiguousarray(term, np.uint64)
+    s = pb.struct(goff)
+    lib().orc_become_leader_batch(C.byref(s), P(el), P(t), 1 if bcast else 0,
+                                  P(o.pending_conf_index), P(o.uncommitted_size), P(o.result),
+                                  P(o.sent), P(o.snap), P(o.stats))
     return o

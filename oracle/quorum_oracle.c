@@ -1802,6 +1802,124 @@ void orc_propose_batch(const orc_prog *a, const orc_props *q, uint64_t *stats) {
   if (q->bytes) *q->bytes += bytes;
 }
 
+/* raft.becomeLeader (raft/raft.go:724-759) on every group with elected[g]
+ * (NULL = every group): reset (:590-613) -- every Progress of the
+ * ProgressMap becomes {Match 0, Next lastIndex + 1, new Inflights, the
+ * same IsLearner}, the leader's own Match = lastIndex; abortLeaderTransfer;
+ * pendingConfIndex = uncommittedSize = 0; newReadOnly (the queue emptied;
+ * the device form's context numbers move past the dropped requests) -- then
+ * Progress[r.id].BecomeReplicate, pendingConfIndex = lastIndex, the log
+ * enters term[g] (a term run from lastIndex + 1; term_start), appendEntry of
+ * the empty entry (lastIndex + 1, the leader's MaybeUpdate, maybeCommit) and,
+ * with flags & 1, stepCandidate's bcastAppend (:1405-1407).  result: 0 not
+ * elected, 1 leader, 2 no Progress for the leader (the reference panics), 3
+ * the run table is full (nothing changes). */
+uint64_t orc_checksum_leader(uint64_t gid, uint32_t result, uint64_t committed, uint32_t sent,
+                             uint32_t snap) {
+  uint64_t h = gid * PHI;
+  return orc_mix64(h ^ 0x6A09E667BB67AE85ull ^ ((uint64_t)result << 56) ^ committed) +
+         orc_mix64(h ^ 0xD1B54A32D192ED03ull ^ ((uint64_t)sent << 40) ^ ((uint64_t)snap << 20));
+}
+
+void orc_become_leader_batch(const orc_prog *a, const uint8_t *elected, const uint64_t *term,
+                             uint32_t flags, uint64_t *pci, uint64_t *unc, uint8_t *result,
+                             void *sent, void *snap, uint64_t *stats) {
+  uint32_t S = a->S, mb = S <= 8 ? 1 : 2;
+  uint32_t full = (1u << S) - 1u;
+  uint64_t *last_index = (uint64_t *)a->last_index, *term_start = (uint64_t *)a->term_start;
+  uint64_t *run_first = (uint64_t *)a->run_first, *run_term = (uint64_t *)a->run_term;
+  uint8_t *run_count = (uint8_t *)a->run_count;
+  uint64_t st[NSTAT];
+  memset(st, 0, sizeof(st));
+  for (uint64_t g = 0; g < a->G; g++) {
+    uint64_t cm = a->committed[g], c0 = cm;
+    uint32_t res = 0, sentm = 0, snapm = 0;
+    if (!elected || elected[g]) {
+      uint32_t trk = a->tracked ? ld_mask(a->tracked, mb, g) & full : full;
+      uint32_t self = a->self_slot ? a->self_slot[g] : 0xFFu;
+      uint32_t mi = a->inc ? ld_mask(a->inc, mb, g) & full : full;
+      uint32_t mo = a->out ? ld_mask(a->out, mb, g) & full : 0;
+      uint32_t rc = (a->R && run_count) ? run_count[g] : 0;
+      if (!(self < S && ((trk >> self) & 1u))) res = 2;
+      else if (a->R && rc >= a->R) res = 3;
+      else {
+        res = 1;
+        uint64_t li = last_index[g];
+        /* reset: every Progress; the leader's own Match = lastIndex */
+        orc_pr prs[16];
+        for (uint32_t t = 0; t < S; t++) {
+          if (!((trk >> t) & 1u)) continue;
+          pr_load2(&prs[t], a, t, g);
+          prs[t].match = t == self ? li : 0;
+          prs[t].next = li + 1;
+          prs[t].pending = 0;
+          prs[t].state = PR_PROBE;
+          prs[t].probe_sent = prs[t].recent_active = 0;
+          prs[t].start = prs[t].count = 0; /* tracker.NewInflights */
+        }
+        if (a->lead_transferee) a->lead_transferee[g] = 0xFF; /* abortLeaderTransfer */
+        if (a->read_acks) {                                   /* newReadOnly */
+          uint32_t cap = a->read_cap ? a->read_cap : READ_QUEUE;
+          uint32_t qn = a->read_count[g] < cap ? a->read_count[g] : cap;
+          a->read_head[g] += qn;
+          a->read_count[g] = 0;
+        }
+        pr_become_replicate(&prs[self]);                      /* Next = Match + 1 */
+        if (pci) pci[g] = li;
+        if (unc) unc[g] = 0;
+        /* the log enters the new term: a run from lastIndex + 1, unless the
+         * last run already has that term (the bootstrap snapshot of the new
+         * leader's own term), where the term then starts */
+        uint64_t ts2 = li + 1;
+        if (a->R) {
+          if (rc > 0 && run_term[(rc - 1) * a->stride + g] == term[g]) {
+            ts2 = run_first[(rc - 1) * a->stride + g];
+          } else {
+            run_first[rc * a->stride + g] = li + 1;
+            run_term[rc * a->stride + g] = term[g];
+            run_count[g] = (uint8_t)(rc + 1);
+          }
+        }
+        term_start[g] = ts2;
+        /* appendEntry(empty) */
+        li += 1;
+        last_index[g] = li;
+        pr_maybe_update(&prs[self], li);
+        uint64_t vals[16];
+        for (uint32_t t = 0; t < S; t++) vals[t] = ((trk >> t) & 1u) ? prs[t].match : 0;
+        orc_maybe_commit(orc_joint_committed(S, mi, mo, vals), &cm, term_start[g], li);
+        if (flags & 1u) { /* bcastAppend */
+          orc_gctx c;
+          c.a = a;
+          c.m = NULL;
+          c.g = g;
+          c.fi = a->first_index[g];
+          c.li = li;
+          c.snap = a->snap_index ? a->snap_index[g] : c.fi - 1;
+          c.me = a->max_ents;
+          c.sent = c.snapm = 0;
+          for (uint32_t t = 0; t < S; t++)
+            if (((trk >> t) & 1u) && t != self) send_append(&c, &prs[t], t, 1);
+          sentm = c.sent;
+          snapm = c.snapm;
+        }
+        for (uint32_t t = 0; t < S; t++)
+          if ((trk >> t) & 1u) pr_store2(&prs[t], a, t, g);
+        a->committed[g] = cm;
+      }
+    }
+    result[g] = (uint8_t)res;
+    if (sent) st_mask(sent, mb, g, sentm);
+    if (snap) st_mask(snap, mb, g, snapm);
+    st[ST_GROUPS] += 1;
+    st[ST_COMMIT_ADVANCED] += cm != c0;
+    st[ST_COMMIT_SUM] += cm;
+    st[ST_CHECKSUM] += orc_checksum_leader(a->goff + g, res, cm, sentm, snapm);
+  }
+  if (stats)
+    for (int k = 0; k < NSTAT; k++) stats[k] += st[k];
+}
+
 /* raft.switchToConfig (raft/raft.go:1651-1700) on every group with
  * switched[g] (NULL = every group), after the new configuration -- inc /
  * out / tracked of `a` -- is in place.  result: 0 not switched, 1 the leader

@@ -711,11 +711,15 @@ class OracleRoundBackend:
 
     def load(self, sc, a, inc=None, tracked=None, out=None, read_cap=0):
         S = sc["S"]
-        pb = self.orc.ProgressBatch(1, S, F_CAP, len(sc["log"]["runs"]), max_ents=sc["max_ents"])
+        R = sc.get("log_runs", len(sc["log"]["runs"]))  # (room for new terms' runs)
+        pb = self.orc.ProgressBatch(1, S, F_CAP, R, max_ents=sc["max_ents"])
         a = dict(a)
         pb.pw = self.orc.pack_word(a.pop("flags"), 0, a.pop("icount"))
         for k, v in a.items():
-            setattr(pb, k, v.copy())
+            if k in ("run_first", "run_term"):
+                getattr(pb, k)[: v.size] = v
+            else:
+                setattr(pb, k, v.copy())
         md = self.orc.mask_dtype(S)
         if inc is not None:
             pb.inc = np.array([inc], md)
@@ -770,6 +774,13 @@ class OracleRoundBackend:
         change; the Progress of a slot that stays keeps its state)."""
         self.pb.tracked[0] = tracked
         self.pb.inc[0] = inc
+
+    def become_leader(self, term, bcast=True):
+        """becomeLeader on the loaded group (orc_become_leader_batch)."""
+        o = self.orc.become_leader(self.pb, np.array([term], np.uint64), bcast=bcast)
+        if o.result[0] == 1:
+            self.pci, self.unc = int(o.pending_conf_index[0]), 0
+        return {"result": int(o.result[0]), "sent": int(o.sent[0]), "snap": int(o.snap[0])}
 
     def switch_config(self):
         """switchToConfig on the loaded group (orc_switch_config_batch)."""

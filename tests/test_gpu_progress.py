@@ -463,7 +463,8 @@ class GpuBackend:
     def load(self, sc, a, inc=None, tracked=None, out=None, read_cap=0):
         # stride 1: the scenario arrays are [S] (the kernels need no row alignment)
         masks = (("inc",) if inc is not None else ()) + (("out",) if out is not None else ())
-        ps = self.eng.ProgressState(1, sc["S"], cap(sc), len(sc["log"]["runs"]), DEV, stride=1,
+        ps = self.eng.ProgressState(1, sc["S"], cap(sc), sc.get("log_runs", len(sc["log"]["runs"])),
+                                    DEV, stride=1,
                                     extras=READS + ("read_keys",), max_ents=sc["max_ents"],
                                     masks=masks, read_cap=read_cap)
         if tracked is None:
@@ -516,6 +517,15 @@ class GpuBackend:
 
     def transferee(self):
         return int(self.ps.lead_transferee[0])
+
+    def become_leader(self, term, bcast=True):
+        """qe_become_leader on the one group."""
+        ld = self.eng.Leader(self.ps, bcast=bcast)
+        ld.term.fill_(term)
+        self.eng.become_leader(self.ps, ld)
+        if int(ld.result[0]) == 1:
+            self.pci, self.unc = int(ld.pending_conf_index[0]), 0
+        return {"result": int(ld.result[0]), "sent": int(ld.sent[0]), "snap": int(ld.snap[0])}
 
     def switch_config(self):
         """qe_switch_config on the one group."""

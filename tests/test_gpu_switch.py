@@ -1,9 +1,12 @@
-"""qe_switch_config (ABI 7): raft.switchToConfig's leader side
-(raft/raft.go:1651-1700) on the GPU, bit-for-bit against the oracle
-(orc_switch_config_batch) on random states and configurations; the reference
-tests that pin it (TestCommitAfterRemoveNode, TestLeaderTransferRemoveNode,
-TestLeaderTransferDemoteNode) run in test_gpu_progress.py's scenario list and
-in the interaction-trace replays (tests/trace_replay.py)."""
+"""The leader's transitions (ABI 7) on the GPU, bit-for-bit against the oracle
+on random states: qe_switch_config (raft.switchToConfig's leader side,
+raft/raft.go:1651-1700; orc_switch_config_batch) under random configurations,
+and qe_become_leader (raft.becomeLeader with reset, :724-759, :590-613;
+orc_become_leader_batch).  The reference tests that pin switchToConfig
+(TestCommitAfterRemoveNode, TestLeaderTransferRemoveNode,
+TestLeaderTransferDemoteNode) run in test_gpu_progress.py's scenario list;
+both entry points run in every interaction-trace replay
+(tests/trace_replay.py)."""
 import numpy as np
 import pytest
 import torch
@@ -113,3 +116,51 @@ def test_switch_config_argument_errors(eng):
     assert L.qe_switch_config(C.byref(p), C.byref(q), None, None) == eng._lib.QE_ERANGE
     p = ps.struct()
     assert L.qe_switch_config(C.byref(p), C.byref(q), None, None) == eng._lib.QE_OK
+
+
+@pytest.mark.parametrize("S,F,masks,max_ents,reads", [
+    (1, 8, (), 0, False), (3, 8, ("inc",), 1, True), (5, 8, (), 0, True),
+    (5, 32, ("inc", "out"), 2, False), (9, 8, ("inc",), 0, True), (16, 5, ("inc", "out"), 0, False)])
+def test_become_leader_matches_oracle(eng, S, F, masks, max_ents, reads):
+    """qe_become_leader (raft.becomeLeader + reset, raft.go:724-759,
+    :590-613) against the oracle on random states: elected and not, leaders
+    without a Progress, full run tables, a new term equal to the last run's
+    (the bootstrap case), ReadIndex queues dropped, bcastAppend's probes
+    (compacted logs: nothing to an inactive peer); every Progress field, the
+    log model (runs, term start, lastIndex, committed), the outputs and the
+    statistics equal the oracle's."""
+    from tests.test_gpu_progress import random_queue
+    rng = np.random.default_rng(8300 + 11 * S + F)
+    G = 4099
+    R = 4
+    pb = random_state(rng, G, S, F, R, masks, EXTRAS, max_ents=max_ents)
+    pb.run_count[rng.random(G) < 0.3] -= 1  # room for the new term's run in most groups
+    pb.run_count[:] = np.maximum(pb.run_count, 1)
+    if reads:
+        random_queue(rng, pb)
+    ps = to_device(eng, pb, masks, EXTRAS + (("reads",) if reads else ()))
+    el = (rng.random(G) < 0.8).astype(np.uint8)
+    last_term = pb.run_term.reshape(R, G)[pb.run_count.astype(np.int64) - 1, np.arange(G)]
+    term = (last_term + rng.integers(0, 3, G).astype(np.uint64)).astype(np.uint64)
+    for bcast in (True, False):
+        ld = eng.Leader(ps, torch.from_numpy(el).to(DEV), bcast=bcast)
+        ld.term.copy_(torch.from_numpy(term.view(np.int64)).to(DEV))
+        st = eng.stats_buffer(DEV)
+        eng.become_leader(ps, ld, stats=st)
+        o = orc.become_leader(pb, term, elected=el, bcast=bcast)
+        md = orc.mask_dtype(S)
+        np.testing.assert_array_equal(ld.result.cpu().numpy(), o.result, err_msg="result")
+        np.testing.assert_array_equal(ld.sent.cpu().numpy().view(md), o.sent, err_msg="sent")
+        np.testing.assert_array_equal(ld.snap.cpu().numpy().view(md), o.snap, err_msg="snap")
+        lv = o.result == 1
+        np.testing.assert_array_equal(ld.pending_conf_index.cpu().numpy().view(np.uint64)[lv],
+                                      o.pending_conf_index[lv], err_msg="pendingConfIndex")
+        h = ps.host()
+        for k in ("term_start", "last_index", "run_count", "run_first", "run_term"):
+            np.testing.assert_array_equal(h[k], getattr(pb, k), err_msg=k)
+        assert_same(ps, pb)
+        got = eng.stats_reduce(st).cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(got, o.stats, err_msg="stats")
+        assert {0, 1, 2, 3} <= set(np.unique(o.result).tolist()) or S == 1
+        assert not bcast or S == 1 or o.sent.any()
+        term = term + np.uint64(1)  # a second election on the new state

@@ -55,7 +55,7 @@ class TileBackend:
     # -- state ------------------------------------------------------------
     def load(self, sc, a, inc=None, tracked=None, out=None):
         S, G, g = sc["S"], G_TILES, self.pos
-        R = len(sc["log"]["runs"])
+        R = sc.get("log_runs", len(sc["log"]["runs"]))
         masks = ("inc",) + (("out",) if out is not None else ())
         pb = random_state(self.rng, G, S, F_TILE, R, masks, EXTRAS, max_ents=sc["max_ents"])
         full = (1 << S) - 1
@@ -195,6 +195,34 @@ class TileBackend:
             np.testing.assert_array_equal(got[: S * G][to], o_commit[: S * G][to])
         self.calls["heartbeat"] += 1
         return [int(x) for x in o_commit[g::G][:S]], int(o_ctx[g]), int(o_sent[g])
+
+    def become_leader(self, term, bcast=True):
+        pb, G, g = self.pb, G_TILES, self.pos
+        el = (self.rng.random(G) < 0.5).astype(np.uint8)
+        el[g] = 1
+        terms = pb.last_index + self.rng.integers(0, 3, G).astype(np.uint64)  # (neighbours: any)
+        terms[g] = term
+        if self.eng:
+            ld = self.eng.Leader(self.ps, torch.from_numpy(el).to(DEV), bcast=bcast)
+            ld.term.copy_(torch.from_numpy(terms.view(np.int64)).to(DEV))
+            self.eng.become_leader(self.ps, ld)
+        o = orc.become_leader(pb, terms, elected=el, bcast=bcast)
+        if self.eng:
+            md = orc.mask_dtype(self.sc["S"])
+            np.testing.assert_array_equal(ld.result.cpu().numpy(), o.result)
+            np.testing.assert_array_equal(ld.sent.cpu().numpy().view(md), o.sent)
+            np.testing.assert_array_equal(ld.snap.cpu().numpy().view(md), o.snap)
+            lv = o.result == 1
+            np.testing.assert_array_equal(ld.pending_conf_index.cpu().numpy().view(np.uint64)[lv],
+                                          o.pending_conf_index[lv])
+            for k in ("term_start", "last_index", "run_count"):
+                np.testing.assert_array_equal(getattr(self.ps, k).cpu().numpy().view(
+                    getattr(pb, k).dtype), getattr(pb, k), err_msg=k)
+            assert_same(self.ps, pb)
+        self.calls["leader"] = self.calls.get("leader", 0) + 1
+        if o.result[g] == 1:
+            self.pci, self.unc = int(o.pending_conf_index[g]), 0
+        return {"result": int(o.result[g]), "sent": int(o.sent[g]), "snap": int(o.snap[g])}
 
     def switch_config(self):
         pb, g = self.pb, self.pos

@@ -32,10 +32,12 @@ printed (tests/golden/make_golden.py extracts it: no reference code runs).
 Each leader's state at the point the printed part begins is restated from
 the trace itself (raft-log dumps, status lines, HardState, the INFO lines of
 the election) -- see the *_setup functions -- and the leader's transitions
-the engine does not model (becomeCandidate's term bump is the election
-kernel's; becomeLeader's reset() of every Progress, raft.go:590-613, is host
-bookkeeping here) are written out where they occur.  Everything else is
-executed by the engine and compared with the trace:
+run through the engine (becomeCandidate's term bump in the election
+kernel; becomeLeader, with its reset() of every Progress, raft.go:590-613,
+through qe_become_leader; the host's conf-change application between
+Readies -- the new masks -- is written out where it occurs, and
+switchToConfig runs through qe_switch_config).  Everything else is executed
+by the engine and compared with the trace:
 
   * every "> L receiving messages" block is one or more rounds of
     qe_progress_step (messages in slot order; a block whose senders are not
@@ -135,39 +137,41 @@ class Leader:
 
     # -- state set-up ------------------------------------------------------
     def load(self, li, committed, runs, first_index, peers, snap_index=None, term_start=None,
-             inc=None, out=None, tracked=None):
+             inc=None, out=None, tracked=None, spare_runs=0):
         lg = {"runs": runs, "committed": committed, "first_index": first_index,
               "last_index": li,
               "term_start": term_start if term_start is not None else runs[-1][0]}
         if snap_index is not None:
             lg["snap_index"] = snap_index
         sc = {"name": "", "S": self.S, "self": self.self, "max_ents": 0, "log": lg,
-              "peers": peers}
+              "peers": peers, "log_runs": len(runs) + spare_runs}
         if inc is None and out is None and tracked is None:
             self.be.load(sc, initial_arrays(sc))
         else:  # a configuration given as slot masks (JointConfig: out too)
             self.be.load(sc, initial_arrays(sc), inc=inc, out=out, tracked=tracked)
 
-    def become_leader(self, li, committed, runs, first_index):
-        """becomeLeader (raft.go:724-759) after a won election: reset()
-        (:590-613) gives every Progress Match 0, Next = lastIndex + 1, the
-        leader's own Match = lastIndex, which BecomeReplicate makes Replicate;
-        pendingConfIndex = lastIndex; then appendEntry(empty) through
-        qe_propose (QE_PROP_APPEND_ONLY) and stepCandidate's bcastAppend
-        (:1405-1407) through qe_progress_send."""
-        peers = []
+    def become_leader(self, li, committed, runs, first_index, term):
+        """becomeLeader (raft.go:724-759) after a won election, through the
+        engine's qe_become_leader (QE_BL_BCAST): reset() (:590-613) of every
+        Progress, the leader's own BecomeReplicate, pendingConfIndex =
+        lastIndex, the log entering `term`, appendEntry of the empty entry and
+        stepCandidate's bcastAppend (:1405-1407).  The Progress loaded
+        before is the candidate's (arbitrary here: reset overwrites it) --
+        only the log model (runs before the new term, lastIndex, committed,
+        firstIndex) carries over."""
+        peers = [{"match": 7 * s, "next": 1 + s, "pending": 0, "state": s % 2,
+                  "probe_sent": bool(s % 3), "recent_active": True, "ring": []}
+                 for s in range(self.S)]
+        self.load(li, committed, runs, first_index, peers, spare_runs=1)
+        out = self.be.become_leader(term)
+        assert out["result"] == 1 and self.be.pci == li and self.be.last_index() == li + 1, out
         for s in range(self.S):
-            if s == self.self:
-                peers.append({"match": li, "next": li + 1, "pending": 0, "state": 1,
-                              "probe_sent": False, "recent_active": False, "ring": []})
-            else:
-                peers.append({"match": 0, "next": li + 1, "pending": 0, "state": 0,
-                              "probe_sent": False, "recent_active": False, "ring": []})
-        self.load(li, committed, runs, first_index, peers)
-        self.be.pci = li
-        out = self.be.propose(1, append_only=True)
-        assert out["result"] == 1
-        self.bcast()
+            if (out["sent"] >> s) & 1:
+                snap = bool((out["snap"] >> s) & 1)
+                p = self.be.peer(s)
+                idx = p["pending"] if snap else p["next"] - 1  # a probe keeps Next
+                self.pending.setdefault(s, []).append((idx, snap, self.be.last_index()))
+        self.checked["elections"] = self.checked.get("elections", 0) + 1
 
     def bcast(self, sei=1):
         """bcastAppend: sendAppend to every peer but the leader (stepCandidate
@@ -421,7 +425,7 @@ def probe_and_replicate(leader_factory, elector):
 
     def won(votes):
         election(elector, 7, 0, 7, votes, 8)
-        L.become_leader(li, 18, runs + [[li + 1, 8]], 11)
+        L.become_leader(li, 18, runs, 11, term=8)
         state["won"] = True
 
     checked = L.replay(cmds, camp["line"] + 1, on_election=won)
@@ -453,7 +457,7 @@ def campaign(leader_factory, elector):
 
     def won(votes):
         election(elector, 3, 0, 0, votes, 1)
-        L.become_leader(2, 2, [[2, 1]], 3)
+        L.become_leader(2, 2, [[2, 1]], 3, term=1)  # (the snapshot's term: the term starts at 2)
         state["won"] = True
 
     checked = L.replay(cmds, command(cmds, "campaign 1")["line"], on_election=won)
@@ -473,7 +477,7 @@ def campaign_learner_must_vote(leader_factory, elector):
 
     def won(votes):
         election(elector, 3, 1, 1, votes, 2)
-        L.become_leader(4, 4, [[2, 1], [5, 2]], 3)
+        L.become_leader(4, 4, [[2, 1]], 3, term=2)
         state["won"] = True
 
     checked = L.replay(cmds, command(cmds, "campaign 2")["line"], on_election=won)
