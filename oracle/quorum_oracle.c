@@ -1080,10 +1080,11 @@ static void ro_load(orc_ro *r, const orc_prog *a, uint64_t g, uint32_t mb) {
 static void ro_store_ovf(const orc_ro *r, const orc_prog *a, uint64_t g, uint32_t mb) {
   for (uint32_t j = READ_QUEUE; j < r->n; j++) ovf_set(a, mb, g, r->ctx[j], r->acks[j]);
 }
-/* the queue -> the device form (entries past the count 0) */
+/* the queue -> the device form (entries past the count 0; entries past the
+ * word live in the ring only) */
 static uint64_t ro_word(const orc_ro *r, uint32_t mb) {
   uint64_t w = 0;
-  for (uint32_t j = 0; j < r->n; j++) w |= (uint64_t)r->acks[j] << (8 * mb * j);
+  for (uint32_t j = 0; j < r->n && j < READ_QUEUE; j++) w |= (uint64_t)r->acks[j] << (8 * mb * j);
   return w;
 }
 /* recvAck (read_only.go:68-76): index of the pending request with context

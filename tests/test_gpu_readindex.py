@@ -41,6 +41,19 @@ def deep_queue(rng, pb, cap):
     pb.read_keys[:] = rng.integers(0, 1 << 62, pb.read_keys.size, dtype=np.uint64)
 
 
+def check_queue(ps, pb, where):
+    """assert_same, with the first diverging groups' queues printed first."""
+    h = ps.host()
+    G = pb.G
+    gw, ow = h["read_acks"].reshape(G, 4), pb.read_acks.view(orc.mask_dtype(pb.S)).reshape(G, 4)
+    bad = np.nonzero((gw != ow).any(1) | (h["read_head"] != pb.read_head) |
+                     (h["read_count"] != pb.read_count))[0]
+    for g in bad[:4]:
+        print(where, "group", g, "gpu", gw[g], h["read_head"][g], h["read_count"][g],
+              "oracle", ow[g], pb.read_head[g], pb.read_count[g])
+    assert_same(ps, pb)
+
+
 def deep_ctx(rng, pb):
     """Contexts the heartbeat responses carry: mostly pending (word or ring),
     some released, some never assigned, some none."""
@@ -81,7 +94,7 @@ def test_deep_readindex_queues_match_oracle(eng, S, masks, cap, F):
             np.testing.assert_array_equal(c_g.cpu().numpy().view(np.uint32)[w], c_o[w], err_msg="ctx")
             w = (r_o == 1) | (r_o == 3)
             np.testing.assert_array_equal(i_g.cpu().numpy().view(np.uint64)[w], i_o[w])
-            assert_same(ps, pb)
+            check_queue(ps, pb, f"read_index rnd {rnd}")
             assert (r_o == 5).any() and (r_o == 3).any()
         mtype, mindex, mhint, mlogterm = random_msgs(rng, pb)
         hb = rng.random(mtype.size) < 0.6  # mostly heartbeat responses
@@ -96,7 +109,7 @@ def test_deep_readindex_queues_match_oracle(eng, S, masks, cap, F):
         eng.progress_step(ps, msgs, stats)
         got = eng.stats_reduce(stats).cpu().numpy().view(np.uint64)
         o = orc.progress_step(pb, mtype, mindex, mhint, mlogterm, read_ctx=ctx, count_bytes=True)
-        assert_same(ps, pb)
+        check_queue(ps, pb, f"step rnd {rnd}")
         assert_outputs(msgs, o, S)
         np.testing.assert_array_equal(got, o.stats)
         if acct:
