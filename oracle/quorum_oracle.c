@@ -1389,6 +1389,10 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
               /* an entry past the word: read from the ring, written back
                * unless released (device-form accounting, ABI 7) */
               if (j >= READ_QUEUE) ovfB += won ? mb : 2 * mb;
+              /* the ack of an entry past the word is written to its ring slot
+               * at once, as the device form does; an entry released later in
+               * the round keeps the ack in its (then dead) slot */
+              if (j >= READ_QUEUE && !won) ovf_set(a, mb, g, ro.ctx[j], ro.acks[j]);
               if (won) {
                 uint32_t r = ro_advance(&ro, cx);
                 released += r;
@@ -1474,7 +1478,6 @@ void orc_progress_step_batch(const orc_prog *a, const orc_msgs *m, uint64_t *sta
       if (m->timeout_now) st_mask(m->timeout_now, mb, g, tnow);
       if (m->bcast) m->bcast[g] = (uint8_t)bc;
       if (wq) ro_word_set(a->read_acks, mb, g, rword);
-      if (rd && a->read_ovf) ro_store_ovf(&ro, a, g, mb);
       if (rd && released) {
         a->read_head[g] = rhead0 + released;
         a->read_count[g] = (uint8_t)ro.n;
