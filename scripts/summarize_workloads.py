@@ -60,7 +60,8 @@ DOMINANT = {
                        "void qe::k_collect_scatter"), 2),
     "progress_send": ("void qe::k_progress_send<5,", 2),
     "propose": ("void qe::k_propose<5, unsigned char, false, false, false>", 2),
-    "heartbeat": ("void qe::k_heartbeat<5, unsigned char>", 2),
+    # round 6: the chunked two-register-set kernel (round 5: k_heartbeat<5, ...>)
+    "heartbeat": ("void qe::k_heartbeat_pipe<5, unsigned char>", 2),
     "switch_config": ("void qe::k_switch_config<5, unsigned char, true, false, false>", 2),
     "progress_step_n7": ("void qe::k_progress_step<7, unsigned char, false, false, 4, false,", 2),
     "progress_step_joint": ("void qe::k_progress_step<6, unsigned char, true, true, 4, false,", 2),
@@ -107,7 +108,7 @@ def main():
         shutil.copy(kts[0], os.path.join(outd, f"{wl}_kernel_stats.csv"))
         stats = {r["Name"]: r for r in csv.DictReader(open(kts[0]))}
         c = {}
-        for p in ("fetch", "write", "sq", "vmem"):
+        for p in ("fetch", "write", "sq", "vmem", "stall"):
             c.update(counters(os.path.join(d, p, "**", "*counter_collection.csv")))
         prefixes = prefix if isinstance(prefix, tuple) else (prefix,)
         bare = lambda x: x[5:] if x.startswith("void ") else x  # noqa: E731
@@ -152,6 +153,14 @@ def main():
     for wl, t in traffic.items():
         print(f"{wl:20s} {t['hbm_bytes_per_launch'] / 1e9:8.3f} GB/launch  {t['rocprof_avg_ns'] / 1e6:.4f} ms"
               f"  VALU {t.get('valu_insts_per_launch', 0):.3e}")
+    # where the dominant kernel's wave cycles go (the stall pass), each over SQ_WAVE_CYCLES
+    for wl, row in summary.items():
+        if "SQ_WAIT_INST_ANY" in row and row.get("SQ_WAVE_CYCLES"):
+            wc = row["SQ_WAVE_CYCLES"]
+            print(f"{wl:20s} " + "  ".join(
+                f"{k[3:]} {row[k] / wc:.3f}" for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                        "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA",
+                                                        "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS") if k in row))
 
 
 if __name__ == "__main__":
