@@ -142,7 +142,7 @@ size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
  *   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
  *                    of qe_commit_vote
  *   "heartbeat_kernel" 0 = qe_heartbeat one tile per wave, 1 = pipelined
- *                    chunks (default)                                      */
+ *                    chunks (default; -1 selects it)                        */
 int qe_tune(const char *key, int value);
 
 /* ---- quorum decisions -------------------------------------------------- */
