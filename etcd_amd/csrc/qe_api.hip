@@ -141,7 +141,7 @@ size_t qe_mask_bytes(uint32_t num_slots) {
 //   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
 //   "cv_kernel", "repl_kernel"  0 = pair kernel, 1 = stream kernel, -1 = default
 //   "heartbeat_kernel"  0 = one tile per wave (round 5), 1 = pipelined chunks,
-//                       -1 = default (1)
+//                       2 = pipelined, strided tiles; -1 = default (1)
 int qe_tune(const char *key, int value) {
   if (!key) return QE_EINVAL;
   if (!strcmp(key, "blocks_per_cu")) {
@@ -165,7 +165,7 @@ int qe_tune(const char *key, int value) {
     return QE_OK;
   }
   if (!strcmp(key, "heartbeat_kernel")) {
-    if (value < -1 || value > 1) return QE_ERANGE;
+    if (value < -1 || value > 2) return QE_ERANGE;
     g_hb_kernel = value < 0 ? 1 : value;
     return QE_OK;
   }

@@ -146,8 +146,13 @@ static int launch_heartbeat(PArgs a, hipStream_t st) {
   const uint64_t per_block = (kBlock / 64) * chunk;
   const uint64_t blocks = (tiles + per_block - 1) / per_block;
   if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
-  hipLaunchKernelGGL((k_heartbeat_pipe<S, MT>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
-                     0, st, a);
+  // the strided walk covers every tile too: blocks x 4 waves x chunk >= tiles
+  if (g_hb_kernel == 2)
+    hipLaunchKernelGGL((k_heartbeat_pipe<S, MT, true>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_heartbeat_pipe<S, MT, false>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 

@@ -2190,23 +2190,32 @@ __device__ __forceinline__ void hb_finish(const PArgs &a, uint64_t t, uint32_t l
   if (a.sent) bst_mask<MT>(x.to, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
 }
 
-template <int S, typename MT>
+// STRIDED: the wave's tiles are wave, wave + W, wave + 2W, ... (W = the
+// grid's waves), so the waves in flight at any moment touch neighbouring
+// tiles, as round 5's grid-stride form; else a contiguous chunk per wave.
+template <int S, typename MT, bool STRIDED>
 __global__ __launch_bounds__(kBlock) void k_heartbeat_pipe(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   __shared__ uint32_t lds_to[kBlock / 64][kSendTPW][64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ntiles = (a.G + 63) / 64;
-  const uint64_t t0 = (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv) * a.chunk;
-  const uint32_t nt =
-      t0 < ntiles ? static_cast<uint32_t>(ntiles - t0 < a.chunk ? ntiles - t0 : a.chunk) : 0u;
+  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+  const uint64_t t0 = STRIDED ? wave : wave * a.chunk;
+  const uint64_t dt = STRIDED ? W : 1u;
+  uint32_t nt = 0;
+  if (t0 < ntiles) {
+    const uint64_t left = (ntiles - t0 + dt - 1) / dt;  // tiles t0, t0 + dt, ... below ntiles
+    nt = static_cast<uint32_t>(left < a.chunk ? left : a.chunk);
+  }
   if (nt == 0) return;  // no block-level barrier below
   // the chunk's send masks: every tracked slot but the leader's
   uint32_t tv[kSendTPW];
 #pragma unroll
   for (int k = 0; k < kSendTPW; k++) {
-    const uint64_t g0 = (t0 + k) * 64;
-    const uint32_t n = static_cast<uint32_t>(k) < nt ? tile_n(a.G, t0 + k) : 0u;
+    const uint64_t g0 = (t0 + k * dt) * 64;
+    const uint32_t n = static_cast<uint32_t>(k) < nt ? tile_n(a.G, t0 + k * dt) : 0u;
     const uint32_t trk =
         a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * sizeof(MT)),
                                    lane) & kFull)
@@ -2217,7 +2226,7 @@ __global__ __launch_bounds__(kBlock) void k_heartbeat_pipe(PArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < kSendTPW; k++) lds_to[wv][k][lane] = tv[k];
-  auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k : ntiles; };
+  auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k * dt : ntiles; };
   auto to_of = [&](uint32_t k) -> uint32_t { return k < nt ? lds_to[wv][k][lane] : 0u; };
   HBTile<S> xa, xb;
   hb_issue<S>(a, tix(0), lane, to_of(0), xa);

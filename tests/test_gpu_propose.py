@@ -186,7 +186,8 @@ def test_propose_full_size_bench_state(eng):
 
 @pytest.mark.parametrize("S,masks,extras,reads", [(3, (), (), False), (5, ("inc",), EXTRAS, True),
                                                    (12, (), EXTRAS, True)])
-def test_heartbeat_matches_oracle(eng, S, masks, extras, reads):
+@pytest.mark.parametrize("hk,tpw", [(-1, -1), (0, -1), (1, 3), (2, -1), (2, 3)])
+def test_heartbeat_matches_oracle(eng, S, masks, extras, reads, hk, tpw):
     """qe_heartbeat (MsgBeat -> bcastHeartbeat, raft.go:524-541, sendHeartbeat
     :494-510) against the oracle: the slots sent to (tracked, not the
     leader), Commit = min(Match, committed) per slot, and the context of the
@@ -200,7 +201,16 @@ def test_heartbeat_matches_oracle(eng, S, masks, extras, reads):
         random_queue(rng, pb)
         ext = extras + ("reads",)
     ps = to_device(eng, pb, masks, ext)
-    commit, ctx, sent = eng.heartbeat(ps)
+    # qe_tune("heartbeat_kernel"): the default, round 5's form, the chunked
+    # pipeline (3 tiles per wave: a ragged last chunk), its strided walk
+    eng.tune("heartbeat_kernel", hk)
+    eng.tune("tiles_per_wave", tpw)
+    try:
+        commit, ctx, sent = eng.heartbeat(ps)
+        torch.cuda.synchronize()
+    finally:
+        eng.tune("heartbeat_kernel", -1)
+        eng.tune("tiles_per_wave", -1)
     o_commit, o_ctx, o_sent = orc.heartbeat(pb)
     md = orc.mask_dtype(S)
     np.testing.assert_array_equal(sent.cpu().numpy().view(md), o_sent)
