@@ -2138,16 +2138,15 @@ __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
   }
 }
 
-// qe_heartbeat, chunked and software-pipelined (the default since round 6;
-// k_heartbeat above is round 5's one-tile-per-wave form, qe_tune
-// "heartbeat_kernel" 0).  A wave owns a chunk of up to kSendTPW tiles: the
-// chunk's send masks (tracked & ~self) are staged in LDS first, so a tile's
-// Match loads depend on an LDS read, and two register sets keep tile k+1's
-// loads (committed, the queue's head and count, the Match rows) in flight
-// while tile k's commits are stored -- as qe_check_quorum does.  Round 5's
-// form spent 0.93 of its wave cycles waiting on memory
-// (profiles/r05/stall_breakdown.txt): each wave loaded its tile, then stored
-// it, with nothing in flight across tiles.
+// qe_heartbeat, chunked and software-pipelined (qe_tune "heartbeat_kernel"
+// 1 and 2).  A wave owns a chunk of up to kSendTPW tiles: the chunk's send
+// masks (tracked & ~self) are staged in LDS first, so a tile's Match loads
+// depend on an LDS read, and two register sets keep tile k+1's loads
+// (committed, the queue's head and count, the Match rows) in flight while
+// tile k's commits are stored -- as qe_check_quorum does.  It cuts the
+// waves' memory wait (SQ_WAIT_ANY 0.93 -> 0.21 of their cycles) but runs
+// 4-20 % slower than k_heartbeat above, which stays the default: the memory
+// pipeline was already full (profiles/r06/heartbeat_ab.txt).
 template <int S>
 struct HBTile {
   uint32_t to, qn, qh;

@@ -141,8 +141,9 @@ size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
  *                    persistent grid, T > 0: each wave walks T tiles
  *   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
  *                    of qe_commit_vote
- *   "heartbeat_kernel" 0 = qe_heartbeat one tile per wave, 1 = pipelined
- *                    chunks (default; -1 selects it)                        */
+ *   "heartbeat_kernel" 0 = qe_heartbeat one tile per wave (default; -1
+ *                    selects it), 1 = pipelined chunks, 2 = pipelined,
+ *                    strided tiles (measured slower: DESIGN §6)              */
 int qe_tune(const char *key, int value);
 
 /* ---- quorum decisions -------------------------------------------------- */
