@@ -101,7 +101,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -119,7 +119,7 @@ def parse():
                          "qe_allreduce_stats path cannot be set up (reported; otherwise exit 3)")
     ap.add_argument("--aux-groups-div", type=int, default=1,
                     help="rehearsal only: divide every secondary workload's group count")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def cpu_share():
@@ -358,9 +358,10 @@ class Dist:
 # dist 1 = uniform 63-bit), so a rank's shard of a multi-rank run holds
 # exactly the groups a single process would hold at the same global ids
 # ---------------------------------------------------------------------------
-def counter_rows(G, S, seed, goff, dev):
-    """[S][stride] int64 tensor of 63-bit uniforms keyed by (seed, goff + g, s)."""
-    b = engine.SlotBatch(G, S, dev, masks=(), votes=False, group_offset=goff)
+def counter_rows(G, S, seed, goff, dev, stride=None):
+    """[S][stride] int64 tensor of 63-bit uniforms keyed by (seed, goff + g, s)
+    (stride None: G rounded up to 64)."""
+    b = engine.SlotBatch(G, S, dev, masks=(), votes=False, group_offset=goff, stride=stride)
     engine.gen_groups(b, seed, dist=1, p_absent=0)
     return b.match
 
@@ -372,7 +373,7 @@ def progress_round_state(ps, msgs, seed=0x5EED):
     responses, 10 % none, no message from the leader's own slot 0."""
     G, S, F, R = ps.G, ps.S, ps.F, ps.R
     goff, dev, st = ps.group_offset, ps.device, ps.stride
-    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev)  # noqa: E731
+    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev, st)  # noqa: E731
     top = 1 << int(os.environ.get("QE_BENCH_INDEX_BITS", "40"))  # A/B knob only
     base = (1 << 20) + u(1, 1)[:st] % (top - (1 << 20))
     ps.match.copy_(base.repeat(S) + u(2) % 64)
@@ -408,7 +409,7 @@ def psend_state(ps, seed=0x5E4D):
     their Inflights (start 0..F-1, count 0..F-1), Next a little past Match."""
     G, S, F = ps.G, ps.S, ps.F
     goff, dev, st = ps.group_offset, ps.device, ps.stride
-    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev)  # noqa: E731
+    u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev, st)  # noqa: E731
     base = (1 << 20) + u(1, 1)[:st] % ((1 << 40) - (1 << 20))
     ps.match.copy_(base.repeat(S) + u(2) % 64)
     ps.next.copy_(ps.match + 1 + u(3) % 4)
@@ -856,7 +857,7 @@ def setup(name, G, S, kind, d, stats):
                                               "t": (want, sent, snap)}
     if kind == "cq":
         ps = engine.ProgressState(G, S, 1, 1, d.dev, group_offset=goff, extras=("self_slot",))
-        act = counter_rows(G, S, 0xC4EC, goff, d.dev) % 10 < 7  # heard from within the timeout
+        act = counter_rows(G, S, 0xC4EC, goff, d.dev, ps.stride) % 10 < 7  # heard from within the timeout
         ps.peer.copy_(act.to(torch.int32) * 8 + 1)  # StateReplicate (+ RecentActive)
         ps.self_slot.fill_(0)
         del act
