@@ -27,6 +27,7 @@ ROWS = [
     ("progress_send", "Progress send"),
     ("propose", "propose (ABI 6)"),
     ("heartbeat", "heartbeat (ABI 6)"),
+    ("switch_config", "switchToConfig (ABI 7)"),
     ("check_quorum", "CheckQuorum"),
     ("confchange", "confchange"),
     ("ready_collect", "ready_collect (3 kernels)"),
@@ -61,7 +62,9 @@ def main():
         t = traffic.get(wl, {})
         tr = (f"{t['hbm_bytes_per_launch'] / 1e9:.2f} GB ({t['traffic_over_algorithmic']:.2f})"
               if "traffic_over_algorithmic" in t else "—")
-        p = pmc.get(wl, {})
+        # the PMC record the workload's traffic entry names (its latest profile)
+        prof = t.get("profile")
+        p = (json.load(open(prof)) if prof else {}).get(wl) or pmc.get(wl, {})
         # per 64-unit tile: units per launch = algorithmic bytes / bytes per unit
         units = (t["algorithmic_bytes_per_launch"] / a["bytes_per_unit"]
                  if "algorithmic_bytes_per_launch" in t and a.get("bytes_per_unit") else None)
