@@ -14,7 +14,6 @@ int g_nontemporal = 3;  // nt loads + nt stores (measured best)
 int g_tiles_per_wave = -1;  // -1 = per-kernel default, 0 = persistent grid
 int g_cv_kernel = -1;  // qe_commit_vote kernel: 0 pair, 1 stream, -1 per-mode default
 int g_repl_kernel = -1;  // qe_replication_round kernel: 0 pair, 1 stream, -1 default
-int g_hb_kernel = 0;  // qe_heartbeat kernel: 0 one tile per wave (default), 1 / 2 pipelined (A/B)
 
 static thread_local char g_errbuf[256];
 
@@ -140,8 +139,6 @@ size_t qe_mask_bytes(uint32_t num_slots) {
 //                    T > 0 = each wave walks T tiles
 //   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
 //   "cv_kernel", "repl_kernel"  0 = pair kernel, 1 = stream kernel, -1 = default
-//   "heartbeat_kernel"  0 = one tile per wave (default), 1 = pipelined chunks,
-//                       2 = pipelined, strided tiles; -1 = default (0)
 int qe_tune(const char *key, int value) {
   if (!key) return QE_EINVAL;
   if (!strcmp(key, "blocks_per_cu")) {
@@ -162,11 +159,6 @@ int qe_tune(const char *key, int value) {
   if (!strcmp(key, "repl_kernel")) {
     if (value < -1 || value > 1) return QE_ERANGE;
     g_repl_kernel = value;
-    return QE_OK;
-  }
-  if (!strcmp(key, "heartbeat_kernel")) {
-    if (value < -1 || value > 2) return QE_ERANGE;
-    g_hb_kernel = value < 0 ? 0 : value;
     return QE_OK;
   }
   if (!strcmp(key, "nontemporal")) {

@@ -129,30 +129,9 @@ static int launch_become_leader(const PArgs &a, bool masked, bool joint, hipStre
   return hip_status(hipGetLastError());
 }
 
-static int launch_heartbeat(PArgs a, hipStream_t st) {
-  if (g_hb_kernel == 0) {  // round 5's one-tile-per-wave form (A/B)
-    const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
-    hipLaunchKernelGGL((k_heartbeat<S, MT>), grid, dim3(kBlock), 0, st, a);
-    return hip_status(hipGetLastError());
-  }
-  // the chunking of qe_check_quorum (kSendTPW tiles per wave at most)
-  const uint64_t tiles = (a.G + 63) / 64;
-  const uint64_t waves = static_cast<uint64_t>(num_cus()) * 32;
-  uint64_t chunk = g_tiles_per_wave > 0 ? static_cast<uint64_t>(g_tiles_per_wave)
-                                        : (tiles + waves - 1) / waves;
-  if (chunk < 2) chunk = 2;
-  if (chunk > static_cast<uint64_t>(kSendTPW)) chunk = kSendTPW;
-  a.chunk = static_cast<uint32_t>(chunk);
-  const uint64_t per_block = (kBlock / 64) * chunk;
-  const uint64_t blocks = (tiles + per_block - 1) / per_block;
-  if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
-  // the strided walk covers every tile too: blocks x 4 waves x chunk >= tiles
-  if (g_hb_kernel == 2)
-    hipLaunchKernelGGL((k_heartbeat_pipe<S, MT, true>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_heartbeat_pipe<S, MT, false>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBlock), 0, st, a);
+static int launch_heartbeat(const PArgs &a, hipStream_t st) {
+  const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
+  hipLaunchKernelGGL((k_heartbeat<S, MT>), grid, dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 

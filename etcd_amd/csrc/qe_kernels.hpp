@@ -45,7 +45,6 @@ extern int g_blocks_per_cu;
 extern int g_nontemporal;  // bit 0: loads, bit 1: stores
 extern int g_cv_kernel;    // qe_commit_vote: 0 pair kernel, 1 stream kernel, -1 default
 extern int g_repl_kernel;  // qe_replication_round: 0 pair kernel, 1 stream kernel, -1 default
-extern int g_hb_kernel;    // qe_heartbeat: 0 one tile per wave (default), 1 / 2 pipelined
 
 inline int num_cus() {
   static int cached[64] = {0};

@@ -2138,107 +2138,6 @@ __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
   }
 }
 
-// qe_heartbeat, chunked and software-pipelined (qe_tune "heartbeat_kernel"
-// 1 and 2).  A wave owns a chunk of up to kSendTPW tiles: the chunk's send
-// masks (tracked & ~self) are staged in LDS first, so a tile's Match loads
-// depend on an LDS read, and two register sets keep tile k+1's loads
-// (committed, the queue's head and count, the Match rows) in flight while
-// tile k's commits are stored -- as qe_check_quorum does.  It cuts the
-// waves' memory wait (SQ_WAIT_ANY 0.93 -> 0.21 of their cycles) but runs
-// 4-20 % slower than k_heartbeat above, which stays the default: the memory
-// pipeline was already full (profiles/r06/heartbeat_ab.txt).
-template <int S>
-struct HBTile {
-  uint32_t to, qn, qh;
-  uint64_t c;
-  uint64_t m[S];
-};
-
-template <int S>
-__device__ __forceinline__ void hb_issue(const PArgs &a, uint64_t t, uint32_t lane, uint32_t to,
-                                         HBTile<S> &x) {
-  const uint64_t g0 = t * 64;
-  const uint32_t n = tile_n(a.G, t);
-  const uint32_t o8 = lane * 8;
-  x.to = to;
-  x.c = bld64(mk_rsrc(a.committed + g0, n * 8), o8);
-  const bool q = a.hb_ctx && a.read_acks;
-  x.qn = q ? bld8(mk_rsrc(a.read_count + g0, n), lane) : 0u;
-  x.qh = q ? bld32(mk_rsrc(a.read_head + g0, n * 4), lane * 4) : 0u;
-#pragma unroll
-  for (int s = 0; s < S; s++)
-    x.m[s] = bld64(mk_rsrc(a.match + static_cast<uint64_t>(s) * a.stride + g0, n * 8),
-                   bit_off(to, s, o8));
-}
-
-template <int S, typename MT>
-__device__ __forceinline__ void hb_finish(const PArgs &a, uint64_t t, uint32_t lane,
-                                          const HBTile<S> &x) {
-  const uint64_t g0 = t * 64;
-  const uint32_t n = tile_n(a.G, t);
-  const uint32_t o8 = lane * 8;
-  if (a.hb_ctx) {
-    const uint32_t q = x.qn < a.read_cap ? x.qn : a.read_cap;
-    bst32(q ? x.qh + q - 1u : 0u, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);  // lastPendingRequestCtx
-  }
-#pragma unroll
-  for (int s = 0; s < S; s++)
-    bst64(x.m[s] < x.c ? x.m[s] : x.c,
-          mk_rsrc(a.hb_commit + static_cast<uint64_t>(s) * a.stride + g0, n * 8),
-          bit_off(x.to, s, o8));
-  if (a.sent) bst_mask<MT>(x.to, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
-}
-
-// STRIDED: the wave's tiles are wave, wave + W, wave + 2W, ... (W = the
-// grid's waves), so the waves in flight at any moment touch neighbouring
-// tiles, as round 5's grid-stride form; else a contiguous chunk per wave.
-template <int S, typename MT, bool STRIDED>
-__global__ __launch_bounds__(kBlock) void k_heartbeat_pipe(PArgs a) {
-  constexpr uint32_t kFull = (1u << S) - 1u;
-  __shared__ uint32_t lds_to[kBlock / 64][kSendTPW][64];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t ntiles = (a.G + 63) / 64;
-  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + wv;
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
-  const uint64_t t0 = STRIDED ? wave : wave * a.chunk;
-  const uint64_t dt = STRIDED ? W : 1u;
-  uint32_t nt = 0;
-  if (t0 < ntiles) {
-    const uint64_t left = (ntiles - t0 + dt - 1) / dt;  // tiles t0, t0 + dt, ... below ntiles
-    nt = static_cast<uint32_t>(left < a.chunk ? left : a.chunk);
-  }
-  if (nt == 0) return;  // no block-level barrier below
-  // the chunk's send masks: every tracked slot but the leader's
-  uint32_t tv[kSendTPW];
-#pragma unroll
-  for (int k = 0; k < kSendTPW; k++) {
-    const uint64_t g0 = (t0 + k * dt) * 64;
-    const uint32_t n = static_cast<uint32_t>(k) < nt ? tile_n(a.G, t0 + k * dt) : 0u;
-    const uint32_t trk =
-        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * sizeof(MT)),
-                                   lane) & kFull)
-                  : kFull;
-    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
-    const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
-    tv[k] = lane < n ? (trk & ~selfb) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < kSendTPW; k++) lds_to[wv][k][lane] = tv[k];
-  auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k * dt : ntiles; };
-  auto to_of = [&](uint32_t k) -> uint32_t { return k < nt ? lds_to[wv][k][lane] : 0u; };
-  HBTile<S> xa, xb;
-  hb_issue<S>(a, tix(0), lane, to_of(0), xa);
-  for (uint32_t k = 0; k < nt; k += 2) {
-    hb_issue<S>(a, tix(k + 1), lane, to_of(k + 1), xb);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the stores
-    hb_finish<S, MT>(a, tix(k), lane, xa);
-    hb_issue<S>(a, tix(k + 2), lane, to_of(k + 2), xa);
-    __builtin_amdgcn_sched_barrier(0);
-    hb_finish<S, MT>(a, tix(k + 1), lane, xb);
-  }
-}
-
 // qe_check_quorum: MsgCheckQuorum (raft/raft.go:997-1018) over the resident
 // Progress words.  One lane per group; each wave owns a chunk of up to
 // kSendTPW tiles (as qe_progress_send): the chunk's masks (Voters[0] |

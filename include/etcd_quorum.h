@@ -140,10 +140,7 @@ size_t qe_mask_bytes(uint32_t num_slots); /* 1 for S<=8, 2 for S<=16, 0 bad */
  *   "tiles_per_wave" -1 = per-kernel default (measured best), 0 =
  *                    persistent grid, T > 0: each wave walks T tiles
  *   "nontemporal"    bit 0: non-temporal loads, bit 1: non-temporal stores
- *                    of qe_commit_vote
- *   "heartbeat_kernel" 0 = qe_heartbeat one tile per wave (default; -1
- *                    selects it), 1 = pipelined chunks, 2 = pipelined,
- *                    strided tiles (measured slower: DESIGN §6)              */
+ *                    of qe_commit_vote                                     */
 int qe_tune(const char *key, int value);
 
 /* ---- quorum decisions -------------------------------------------------- */

@@ -186,8 +186,8 @@ def test_propose_full_size_bench_state(eng):
 
 @pytest.mark.parametrize("S,masks,extras,reads", [(3, (), (), False), (5, ("inc",), EXTRAS, True),
                                                    (12, (), EXTRAS, True)])
-@pytest.mark.parametrize("hk,tpw", [(-1, -1), (0, -1), (1, 3), (2, -1), (2, 3)])
-def test_heartbeat_matches_oracle(eng, S, masks, extras, reads, hk, tpw):
+@pytest.mark.parametrize("tpw", [-1, 3])
+def test_heartbeat_matches_oracle(eng, S, masks, extras, reads, tpw):
     """qe_heartbeat (MsgBeat -> bcastHeartbeat, raft.go:524-541, sendHeartbeat
     :494-510) against the oracle: the slots sent to (tracked, not the
     leader), Commit = min(Match, committed) per slot, and the context of the
@@ -201,15 +201,12 @@ def test_heartbeat_matches_oracle(eng, S, masks, extras, reads, hk, tpw):
         random_queue(rng, pb)
         ext = extras + ("reads",)
     ps = to_device(eng, pb, masks, ext)
-    # qe_tune("heartbeat_kernel"): the default, round 5's form, the chunked
-    # pipeline (3 tiles per wave: a ragged last chunk), its strided walk
-    eng.tune("heartbeat_kernel", hk)
+    # the default grid, and waves walking 3 tiles each (a ragged last walk)
     eng.tune("tiles_per_wave", tpw)
     try:
         commit, ctx, sent = eng.heartbeat(ps)
         torch.cuda.synchronize()
     finally:
-        eng.tune("heartbeat_kernel", -1)
         eng.tune("tiles_per_wave", -1)
     o_commit, o_ctx, o_sent = orc.heartbeat(pb)
     md = orc.mask_dtype(S)
