@@ -69,7 +69,8 @@ def deep_ctx(rng, pb):
 
 
 @pytest.mark.parametrize("S,masks,cap", [(3, (), 16), (5, ("inc",), 64), (5, (), 255),
-                                         (7, ("inc", "out"), 64), (10, ("inc",), 32)])
+                                         (7, ("inc", "out"), 64), (10, ("inc",), 32),
+                                         (16, ("inc", "out"), 255)])
 @pytest.mark.parametrize("F", [8, 32])
 def test_deep_readindex_queues_match_oracle(eng, S, masks, cap, F):
     rng = np.random.default_rng(9100 + 13 * S + cap + F)
