@@ -1112,6 +1112,8 @@ def occupancy(workload):
     out = {}
     for n in names.split(" + "):
         n = bare(n)
+        if n not in res:  # a record made before a defaulted template flag was added (ABI 8: N16)
+            n = n.replace(">(", ", false>(", 1)
         if n in res:
             out[n[:n.index("(")]] = {k: res[n][k] for k in ("vgpr", "scratch_bytes", "lds_bytes",
                                                             "waves_per_simd")}

@@ -16,7 +16,7 @@ import torch  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QE_LIB", os.path.join(_HERE, "lib", "libetcd_quorum.so"))
 
-QE_ABI_VERSION = 7
+QE_ABI_VERSION = 8
 QE_OK = 0
 QE_EINVAL = -22
 QE_ERANGE = -34
@@ -108,6 +108,7 @@ class QeProgress(C.Structure):
         ("max_ents", u32), ("reserved2", u32),
         ("read_acks", vp), ("read_head", vp), ("read_count", vp),  # ABI 5
         ("read_cap", u32), ("reserved3", u32), ("read_ovf", vp), ("read_keys", vp),  # ABI 7
+        ("infl16", vp),  # ABI 8: the 16-bit Inflights form
     ]
 
 
@@ -167,6 +168,8 @@ QE_READ_QUEUE = 4           # ABI 5: ReadIndex requests pending per group
 QE_RI_NONE, QE_RI_RESPOND, QE_RI_POSTPONED, QE_RI_QUEUED, QE_RI_FULL = 0, 1, 2, 3, 4
 QE_RI_DUPLICATE = 5         # ABI 7: the request's key is pending already
 QE_READ_CAP_MAX = 255       # ABI 7: the longest queue (read_cap)
+QE_RING16_MAX_F = 8         # ABI 8: the 16-bit Inflights form (infl16)
+QE_RING16_MAX_SLOTS = 9
 QE_MAX_INFLIGHT = 255
 QE_MAX_LOG_RUNS = 16
 
@@ -233,6 +236,8 @@ PROTOTYPES = {
     "qe_become_leader": (C.c_int, [C.POINTER(QeProgress), C.POINTER(QeLeader), vp, vp]),
     "qe_ring_pack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
     "qe_ring_unpack": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp]),
+    "qe_ring_pack16": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp, vp, vp]),
+    "qe_ring_unpack16": (C.c_int, [u64, u32, u32, u64, vp, vp, vp, vp, vp, vp]),
     "qe_confchange": (C.c_int, [C.POINTER(QeConf), C.POINTER(QeConfChanges),
                                 C.POINTER(QeProgress), vp]),
     "qe_comm_id_bytes": (C.c_size_t, []),

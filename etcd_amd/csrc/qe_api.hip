@@ -394,6 +394,10 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   // a slot's ring block of a 64-group tile is addressed with 32-bit offsets
   if (static_cast<uint64_t>(QE_RING_PITCH(p->inflight_cap)) * 4 * 64 > 0x7FFFFFFFull)
     return QE_ERANGE;
+  // ABI 8: the 16-bit Inflights form exists for the pipelined kernels' shapes
+  if (p->infl16 && (p->inflight_cap > QE_RING16_MAX_F || p->num_slots > QE_RING16_MAX_SLOTS ||
+                    p->log_runs > 4))
+    return QE_ERANGE;
   a = PArgs{};
   a.G = p->num_groups;
   a.goff = p->group_offset;
@@ -406,6 +410,7 @@ static int progress_args(const qe_progress *p, PArgs &a) {
   a.pw = p->peer;
   a.ilo = p->infl_lo;
   a.ihi = p->infl_hi;
+  a.infl16 = p->infl16;
   a.FP = QE_RING_PITCH(p->inflight_cap);
   a.committed = p->committed;
   a.term_start = p->term_start;

@@ -18,19 +18,31 @@ using MT = std::conditional<(S <= 8), uint8_t, uint16_t>::type;
 #define QE_CAT2(a, b) a##b
 #define QE_CAT(a, b) QE_CAT2(a, b)
 
-template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64, bool P = false>
+template <int RM, bool ACCT, bool RD, int WPB = kBlock / 64, bool P = false, bool N16 = false>
 static int launch_progress_step_p(const PArgs &a, bool masked, bool joint, hipStream_t st) {
   // the same waves as the 4-wave grid, in blocks of WPB waves
   const uint64_t nb = static_cast<uint64_t>(grid_for((a.G + 63) / 64, 0, 1)) * ((kBlock / 64) / WPB);
   const dim3 grid(static_cast<unsigned>(nb < 0x7FFFFFFFull ? nb : 0x7FFFFFFFull));
   const dim3 blk(64 * WPB);
   if (joint)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, true, RM, ACCT, RD, WPB, P, N16>), grid, blk, 0, st, a);
   else if (masked)
-    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, true, false, RM, ACCT, RD, WPB, P, N16>), grid, blk, 0, st, a);
   else
-    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, RD, WPB, P>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_progress_step<S, MT, false, false, RM, ACCT, RD, WPB, P, N16>), grid, blk, 0, st, a);
   return hip_status(hipGetLastError());
+}
+
+// ABI 8, the 16-bit Inflights form (host-checked: F <= 8, S <= 9, at most 4
+// log runs): the pipelined kernels, and the rolled one for the byte count
+static int launch_progress_step_n16(const PArgs &a, bool acct, bool masked, bool joint,
+                                    hipStream_t st) {
+  if constexpr (S <= QE_RING16_MAX_SLOTS) {
+    if (acct) return launch_progress_step_p<4, true, true, kBlock / 64, false, true>(a, masked, joint, st);
+    if (a.read_acks) return launch_progress_step_p<4, false, true, kBlock / 64, true, true>(a, masked, joint, st);
+    return launch_progress_step_p<4, false, false, kBlock / 64, true, true>(a, masked, joint, st);
+  }
+  return QE_EINVAL;
 }
 
 // the pipelined slot loop (qe_progress.hpp) for rings in row form, up to 9
@@ -58,6 +70,13 @@ static int launch_progress_send(PArgs a, hipStream_t st) {
   const uint64_t per_block = (kBlock / 64) * chunk;
   const uint64_t blocks = (tiles + per_block - 1) / per_block;
   if (blocks > 0x7FFFFFFFull) return QE_ERANGE;
+  if constexpr (S <= QE_RING16_MAX_SLOTS) {
+    if (a.infl16) {
+      hipLaunchKernelGGL((k_progress_send<S, MT, true>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(kBlock), 0, st, a);
+      return hip_status(hipGetLastError());
+    }
+  }
   hipLaunchKernelGGL((k_progress_send<S, MT>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
                      0, st, a);
   return hip_status(hipGetLastError());
@@ -103,21 +122,27 @@ static int launch_read_index(const PArgs &a, bool masked, bool joint, hipStream_
   return hip_status(hipGetLastError());
 }
 
-template <bool ACCT>
+template <bool ACCT, bool N16 = false>
 static int launch_propose(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  if constexpr (!N16 && S <= QE_RING16_MAX_SLOTS) {
+    if (a.infl16) return launch_propose<ACCT, true>(a, masked, joint, st);
+  }
   const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
-  if (joint) hipLaunchKernelGGL((k_propose<S, MT, true, true, ACCT>), grid, dim3(kBlock), 0, st, a);
-  else if (masked) hipLaunchKernelGGL((k_propose<S, MT, true, false, ACCT>), grid, dim3(kBlock), 0, st, a);
-  else hipLaunchKernelGGL((k_propose<S, MT, false, false, ACCT>), grid, dim3(kBlock), 0, st, a);
+  if (joint) hipLaunchKernelGGL((k_propose<S, MT, true, true, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_propose<S, MT, true, false, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_propose<S, MT, false, false, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
-template <bool ACCT>
+template <bool ACCT, bool N16 = false>
 static int launch_switch_config(const PArgs &a, bool masked, bool joint, hipStream_t st) {
+  if constexpr (!N16 && S <= QE_RING16_MAX_SLOTS) {
+    if (a.infl16) return launch_switch_config<ACCT, true>(a, masked, joint, st);
+  }
   const dim3 grid(grid_for((a.G + 63) / 64, 0, 1));
-  if (joint) hipLaunchKernelGGL((k_switch_config<S, MT, true, true, ACCT>), grid, dim3(kBlock), 0, st, a);
-  else if (masked) hipLaunchKernelGGL((k_switch_config<S, MT, true, false, ACCT>), grid, dim3(kBlock), 0, st, a);
-  else hipLaunchKernelGGL((k_switch_config<S, MT, false, false, ACCT>), grid, dim3(kBlock), 0, st, a);
+  if (joint) hipLaunchKernelGGL((k_switch_config<S, MT, true, true, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
+  else if (masked) hipLaunchKernelGGL((k_switch_config<S, MT, true, false, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_switch_config<S, MT, false, false, ACCT, N16>), grid, dim3(kBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -157,6 +182,7 @@ int QE_CAT(dispatch_progress_, QE_S)(const PArgs &a, int kind, bool masked, bool
   // up to QE_MAX_LOG_RUNS otherwise
   // ReadIndex tracking (a.read_acks) takes a variant of its own: its queue
   // state costs registers the rounds without reads should not pay
+  if (a.infl16 && (kind == 0 || kind == 2)) return launch_progress_step_n16(a, kind == 2, masked, joint, st);
   if (kind == 2) return launch_progress_step<QE_MAX_LOG_RUNS, true, true>(a, masked, joint, st);
   if (a.read_acks) return step_runs<true>(a, masked, joint, st);
   return step_runs<false>(a, masked, joint, st);

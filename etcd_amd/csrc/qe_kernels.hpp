@@ -706,6 +706,7 @@ struct PArgs {
   uint64_t *match, *next, *pending;
   uint32_t *pw;  // [S][stride] packed per-peer words (QE_PW_*)
   uint32_t *ilo, *ihi;  // Inflights rings, lane-major [S][stride][FP] (ABI 4)
+  uint16_t *infl16;     // ABI 8: the 16-bit form [S][stride][8], or null
   uint32_t FP;          // QE_RING_PITCH(F)
   uint64_t *committed;
   const uint64_t *term_start, *first_index, *last_index, *snap_index;

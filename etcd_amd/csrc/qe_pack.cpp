@@ -511,4 +511,77 @@ int qe_ring_unpack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_ca
   return QE_OK;
 }
 
+// ---- ABI 8: the 16-bit form (infl16, offsets below Next) ------------------
+// A peer is in the 16-bit form iff every live entry v satisfies
+// Next - 65536 <= v <= Next - 1; else it is wide.  Every position is encoded
+// both ways (the 16-bit offset of a dead or out-of-range position is the low
+// half of Next - 1 - v), so unpacking returns every position exactly.
+int qe_ring_pack16(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                   uint64_t stride, const uint64_t *entries, const uint64_t *next,
+                   uint32_t *peer, uint16_t *infl16, uint32_t *infl_lo, uint32_t *infl_hi) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (inflight_cap == 0 || inflight_cap > QE_RING16_MAX_F) return QE_ERANGE;
+  if (num_groups == 0) return QE_OK;
+  if (stride < num_groups || !entries || !next || !peer || !infl16 || !infl_lo || !infl_hi)
+    return QE_EINVAL;
+  const uint32_t F = inflight_cap, FP = QE_RING_PITCH(F);
+  for (uint32_t s = 0; s < num_slots; s++) {
+    parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
+      for (uint64_t g = b; g < e; g++) {
+        const uint64_t row = s * stride + g;
+        const uint64_t *src = entries + row * F;
+        const uint64_t top = next[row] - 1;
+        uint32_t *lo = infl_lo + row * FP, *hi = infl_hi + row * FP;
+        uint16_t *o = infl16 + row * QE_RING16_MAX_F;
+        for (uint32_t k = 0; k < QE_RING16_MAX_F; k++) {
+          const uint64_t v = k < F ? src[k] : top;
+          o[k] = static_cast<uint16_t>(top - v);
+          if (k < FP) {
+            lo[k] = static_cast<uint32_t>(v);
+            hi[k] = static_cast<uint32_t>(v >> 32);
+          }
+        }
+        uint32_t w = peer[row] & ~QE_PW_RING_MASK;
+        const uint32_t start = (w >> QE_PW_START_SHIFT) & 0xFFu;
+        const uint32_t count = (w >> QE_PW_COUNT_SHIFT) & 0xFFu;
+        const uint32_t st = start < F ? start : 0;  // as the kernels read an invalid start
+        bool fits = true;
+        for (uint32_t j = 0; j < count && j < F && fits; j++) {
+          uint32_t pos = st + j;
+          if (pos >= F) pos -= F;
+          fits = src[pos] <= top && top - src[pos] <= 0xFFFFu;
+        }
+        peer[row] = w | (fits ? 0u : QE_PF_RING_WIDE);
+      }
+    });
+  }
+  return QE_OK;
+}
+
+int qe_ring_unpack16(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                     uint64_t stride, const uint16_t *infl16, const uint32_t *infl_lo,
+                     const uint32_t *infl_hi, const uint64_t *next, const uint32_t *peer,
+                     uint64_t *entries) {
+  if (num_slots == 0 || num_slots > QE_MAX_SLOTS) return QE_EINVAL;
+  if (inflight_cap == 0 || inflight_cap > QE_RING16_MAX_F) return QE_ERANGE;
+  if (num_groups == 0) return QE_OK;
+  if (stride < num_groups || !entries || !next || !peer || !infl16 || !infl_lo || !infl_hi)
+    return QE_EINVAL;
+  const uint32_t F = inflight_cap, FP = QE_RING_PITCH(F);
+  for (uint32_t s = 0; s < num_slots; s++) {
+    parallel_for(num_groups, [&](uint64_t b, uint64_t e) {
+      for (uint64_t g = b; g < e; g++) {
+        const uint64_t row = s * stride + g;
+        const bool wide = (peer[row] & QE_PF_RING_WIDE) != 0;
+        const uint64_t top = next[row] - 1;
+        for (uint32_t k = 0; k < F; k++)
+          entries[row * F + k] =
+              wide ? (static_cast<uint64_t>(infl_hi[row * FP + k]) << 32) | infl_lo[row * FP + k]
+                   : top - infl16[row * QE_RING16_MAX_F + k];
+      }
+    });
+  }
+  return QE_OK;
+}
+
 }  // extern "C"

@@ -164,7 +164,9 @@ struct PRun {
 
 struct PSend {
   rsrc_t rlo, rhi;  // this slot's ring block of the tile (infl_lo / infl_hi)
+  rsrc_t r16;       // ABI 8: the block in the 16-bit form (infl16; lane * 16)
   uint32_t lb;      // lane * FP * 4: the lane's ring in the block
+  uint32_t eb = 4;  // bytes of one entry in the device form (accounting): 4, 2
   bool row;         // F <= kRingChunk: the runs are written by ring_store_row
   uint32_t F, me;
   uint64_t fi, li, snap;
@@ -290,7 +292,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
       const PRun here{0, 0, p.next};
       p.next = run_val(here, added - 1, x.me, x.li) + 1;
       p.count += added;
-      ac.add(true, 4 * added);
+      ac.add(true, x.eb * added);
     }
   } else {  // memory form: append entry by entry, straight to memory
     while (__builtin_amdgcn_ballot_w64(added < lim && p.next <= x.li)) {
@@ -309,7 +311,7 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
         p.count += 1;
         added += 1;
       }
-      ac.add(on, 4);
+      ac.add(on, x.eb);
     }
   }
   if (repl) {
@@ -327,6 +329,50 @@ __device__ __forceinline__ void send_burst(PR &p, bool sei, uint32_t k, PSend &x
 // read or rewritten (`ld`: touched, with live entries) in registers, one or
 // two 16-byte loads per lane; hi[] holds every position's upper word (the
 // epoch unless the peer is wide).
+// ABI 8, the 16-bit form: entry k = Next - 1 - off[k] (eight u16 offsets in
+// 16 bytes per lane), decoded with the peer's Next as the round found it; a
+// wide peer's entries from infl_lo / infl_hi (rare).
+template <bool P>
+__device__ __forceinline__ void ring_load_n16(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
+                                              uint32_t (&lo)[kRingChunk],
+                                              uint32_t (&hi)[kRingChunk], const uint32_t *pre,
+                                              uint64_t nx_old) {
+  u32x4 a = {0, 0, 0, 0};
+  if (pre) {
+    a = u32x4{pre[0], pre[1], pre[2], pre[3]};
+  } else if (__builtin_amdgcn_ballot_w64(ld)) {
+    a = bld128(x.r16, ld ? (threadIdx.x & 63) * 16 : kOOB);
+  }
+  const uint64_t top = nx_old - 1;
+  const uint32_t w4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) {
+    const uint64_t e = top - ((w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+    lo[k] = static_cast<uint32_t>(e);
+    hi[k] = static_cast<uint32_t>(e >> 32);
+  }
+  const bool w = ld && rep_wide(rep);
+  if (__builtin_amdgcn_ballot_w64(w)) {  // rare: a window past 65535 indices
+    const u32x4 l0 = bld128(x.rlo, w ? x.lb : kOOB);
+    const u32x4 h0 = bld128(x.rhi, w ? x.lb : kOOB);
+    u32x4 l1 = {0, 0, 0, 0}, h1 = {0, 0, 0, 0};
+    if (FP > 4) {
+      l1 = bld128(x.rlo, w ? x.lb + 16 : kOOB);
+      h1 = bld128(x.rhi, w ? x.lb + 16 : kOOB);
+    }
+    if constexpr (P)  // waited here, on this (rare) path only
+      asm volatile("" ::"v"(l0.x), "v"(l0.y), "v"(l0.z), "v"(l0.w), "v"(h0.x), "v"(h0.y),
+                   "v"(h0.z), "v"(h0.w), "v"(l1.x), "v"(l1.y), "v"(l1.z), "v"(l1.w), "v"(h1.x),
+                   "v"(h1.y), "v"(h1.z), "v"(h1.w));
+    if (w) {
+      lo[0] = l0.x, lo[1] = l0.y, lo[2] = l0.z, lo[3] = l0.w;
+      lo[4] = l1.x, lo[5] = l1.y, lo[6] = l1.z, lo[7] = l1.w;
+      hi[0] = h0.x, hi[1] = h0.y, hi[2] = h0.z, hi[3] = h0.w;
+      hi[4] = h1.x, hi[5] = h1.y, hi[6] = h1.z, hi[7] = h1.w;
+    }
+  }
+}
+
 template <bool P>
 __device__ __forceinline__ void ring_load_row(const PSend &x, bool ld, uint32_t rep, uint32_t FP,
                                               uint32_t (&lo)[kRingChunk],
@@ -464,6 +510,55 @@ __device__ __forceinline__ void ring_store_row(PR &p, const PSend &x, const PRun
   }
 }
 
+// ABI 8, the 16-bit form: the peer's ring after the round, re-based on its
+// final Next, wherever the round appended or moved Next while entries are
+// live (both only on appends in reachable states: OptimisticUpdate, while
+// MaybeUpdate past every sent index empties the ring).  Positions a run
+// covers take the run's entry (the later run wins), the others keep what
+// was loaded.  A ring whose live entries all lie in [Next - 65536, Next - 1]
+// is written as eight offsets, 16 bytes (two lanes per 32-byte sector);
+// otherwise (rare) it turns wide: both words of every position in infl_lo /
+// infl_hi.
+template <bool P>
+__device__ __forceinline__ void ring_store_n16(PR &p, const PSend &x, const PRun &r1,
+                                               const PRun &r2, bool touched, uint64_t nx_old,
+                                               uint32_t FP, uint32_t (&lo)[kRingChunk],
+                                               uint32_t (&hi)[kRingChunk]) {
+  const bool any = (r1.n | r2.n) != 0;
+  const bool wl = touched && p.count > 0 && (any || p.next != nx_old);
+  if (!P && !__builtin_amdgcn_ballot_w64(wl)) return;  // the ring stands as loaded
+  const uint64_t top = p.next - 1;
+  const uint32_t st = p.start;
+  bool fits = true;
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) {
+    const uint32_t j1 = static_cast<uint32_t>(k) >= r1.p ? k - r1.p : k + x.F - r1.p;
+    const uint32_t j2 = static_cast<uint32_t>(k) >= r2.p ? k - r2.p : k + x.F - r2.p;
+    const bool on1 = j1 < r1.n, on2 = j2 < r2.n;
+    const uint64_t v = on2 ? run_val(r2, j2, x.me, x.li)
+                           : (on1 ? run_val(r1, j1, x.me, x.li) : ent64(hi[k], lo[k]));
+    lo[k] = static_cast<uint32_t>(v);
+    hi[k] = static_cast<uint32_t>(v >> 32);
+    const uint32_t rel = static_cast<uint32_t>(k) >= st ? k - st : k + x.F - st;
+    const bool live = static_cast<uint32_t>(k) < x.F && rel < p.count;
+    fits = fits && (!live || (v <= top && top - v <= 0xFFFFull));
+    o[k >> 1] |= (static_cast<uint32_t>(top - v) & 0xFFFFu) << (16 * (k & 1));
+  }
+  if (wl) p.rep = fits ? 0u : QE_PF_RING_WIDE;
+  if (P || __builtin_amdgcn_ballot_w64(wl))
+    bst128(u32x4{o[0], o[1], o[2], o[3]}, x.r16, (wl && fits) ? (threadIdx.x & 63) * 16 : kOOB);
+  const bool ww = wl && !fits;
+  if (__builtin_amdgcn_ballot_w64(ww)) {
+    bst128(u32x4{lo[0], lo[1], lo[2], lo[3]}, x.rlo, ww ? x.lb : kOOB);
+    bst128(u32x4{hi[0], hi[1], hi[2], hi[3]}, x.rhi, ww ? x.lb : kOOB);
+    if (FP > 4) {
+      bst128(u32x4{lo[4], lo[5], lo[6], lo[7]}, x.rlo, ww ? x.lb + 16 : kOOB);
+      bst128(u32x4{hi[4], hi[5], hi[6], hi[7]}, x.rhi, ww ? x.lb + 16 : kOOB);
+    }
+  }
+}
+
 // Inflights.FreeLE(to) (raft/tracker/inflights.go:87-113) given fr_old, the
 // number of this round's c_old initial entries (from start) that are <= to,
 // stopping at the first that is not; the entries this round appended before
@@ -476,7 +571,7 @@ __device__ __forceinline__ void free_le(PR &p, uint64_t to, uint32_t c_old, uint
   if (fr == c_old) {
     for (uint32_t j = 0; j < r1.n && run_val(r1, j, x.me, x.li) <= to; j++) fr++;
   }
-  ac.add(p.count > 0, 4 * (fr + 1 < p.count ? fr + 1 : p.count));
+  ac.add(p.count > 0, x.eb * (fr + 1 < p.count ? fr + 1 : p.count));
   if (fr > 0) {
     p.count -= fr;
     uint32_t st2 = p.start + fr;
@@ -612,6 +707,7 @@ struct SlotArgs {
   uint32_t F, FP;
   uint64_t *match, *next, *pending;
   uint32_t *pw, *ilo, *ihi;
+  uint16_t *infl16;
   const uint64_t *mhint, *mlogterm;
   const uint32_t *read_ctx;
   uint8_t *msg_count;
@@ -634,28 +730,34 @@ __device__ __forceinline__ SlotArgs slot_args(const PArgs &a) {
     KA *ka = (KA *)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(ka));
     return SlotArgs{ka->stride, ka->F, ka->FP, ka->match, ka->next, ka->pending, ka->pw,
-                    ka->ilo, ka->ihi, ka->mhint, ka->mlogterm, ka->read_ctx, ka->msg_count,
-                    ka->msg_index};
+                    ka->ilo, ka->ihi, ka->infl16, ka->mhint, ka->mlogterm, ka->read_ctx,
+                    ka->msg_count, ka->msg_index};
   } else {
     return SlotArgs{a.stride, a.F, a.FP, a.match, a.next, a.pending, a.pw, a.ilo, a.ihi,
-                    a.mhint, a.mlogterm, a.read_ctx, a.msg_count, a.msg_index};
+                    a.infl16, a.mhint, a.mlogterm, a.read_ctx, a.msg_count, a.msg_index};
   }
 }
 
-template <bool P, bool RD, class A>
+template <bool P, bool RD, bool N16, class A>
 __device__ __forceinline__ void pb_load(const A &a, uint64_t row, const uint64_t *l_mix,
                                         uint32_t n, uint32_t lane, bool ld, bool rej,
                                         bool has_ix, bool rcl, PB &b) {
   b.mt = l_mix[lane];
   b.ix = has_ix ? l_mix[64 + lane] : 0;
   if constexpr (P) {  // fixed count: every load issued, unused lanes dropped
-    const rsrc_t rr = mk_rsrc(a.ilo + row * a.FP, n * a.FP * 4);
-    const uint32_t lb = lane * a.FP * 4;
     const bool rl = ld;  // (P: row form only)
-    const u32x4 x0 = bld128(rr, rl ? lb : kOOB);
-    const u32x4 x1 = bld128(rr, (rl && a.FP > 4) ? lb + 16 : kOOB);
-    b.rl[0] = x0.x, b.rl[1] = x0.y, b.rl[2] = x0.z, b.rl[3] = x0.w;
-    b.rl[4] = x1.x, b.rl[5] = x1.y, b.rl[6] = x1.z, b.rl[7] = x1.w;
+    if constexpr (N16) {  // ABI 8: the 16-bit form, one 16-byte load
+      const u32x4 x0 = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), rl ? lane * 16 : kOOB);
+      b.rl[0] = x0.x, b.rl[1] = x0.y, b.rl[2] = x0.z, b.rl[3] = x0.w;
+      b.rl[4] = b.rl[5] = b.rl[6] = b.rl[7] = 0u;
+    } else {
+      const rsrc_t rr = mk_rsrc(a.ilo + row * a.FP, n * a.FP * 4);
+      const uint32_t lb = lane * a.FP * 4;
+      const u32x4 x0 = bld128(rr, rl ? lb : kOOB);
+      const u32x4 x1 = bld128(rr, (rl && a.FP > 4) ? lb + 16 : kOOB);
+      b.rl[0] = x0.x, b.rl[1] = x0.y, b.rl[2] = x0.z, b.rl[3] = x0.w;
+      b.rl[4] = x1.x, b.rl[5] = x1.y, b.rl[6] = x1.z, b.rl[7] = x1.w;
+    }
     b.nx = bld64(mk_rsrc(a.next + row, n * 8), ld ? lane * 8 : kOOB);
     b.w = bld32(mk_rsrc(a.pw + row, n * 4), ld ? lane * 4 : kOOB);
     b.hn = bld64(mk_rsrc(a.mhint + row, n * 8), rej ? lane * 8 : kOOB);
@@ -704,7 +806,7 @@ __device__ __forceinline__ void pb_ready(const PB &b) {
 // (21 KB at S = 5) would allow one 4-wave block per CU.  P: the pipelined
 // slot loop (above; the launcher picks it for row-form rings).
 template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, bool RD,
-          int WPB = kBlock / 64, bool P = false>
+          int WPB = kBlock / 64, bool P = false, bool N16 = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
                           amdgpu_waves_per_eu(S <= 9 ? QE_PSTEP_WAVES : 2))) void
 k_progress_step(PArgs a) {
@@ -907,13 +1009,13 @@ k_progress_step(PArgs a) {
     const uint32_t p0 = skip == 0 ? 1u : 0u;
     {  // the first walked slot, before phase 1: every possible event
       const bool ld = (((trk & (msgm | (self != p0 ? (1u << p0) : 0u))) >> p0) & 1u) != 0;
-      pb_load<P, RD>(a, static_cast<uint64_t>(p0) * a.stride + g0, &l_mix[wv][p0][0][0], n, lane, ld,
+      pb_load<P, RD, N16>(a, static_cast<uint64_t>(p0) * a.stride + g0, &l_mix[wv][p0][0][0], n, lane, ld,
                  ((rejm >> p0) & 1u) != 0, ((ixm >> p0) & 1u) != 0, ((rcm >> p0) & 1u) != 0, cur);
     }
     if constexpr (PF2 && S > 2) {  // and the second
       const uint32_t p1 = after(p0);
       const bool ld = (((trk & (msgm | (self != p1 ? (1u << p1) : 0u))) >> p1) & 1u) != 0;
-      pb_load<P, RD>(a, static_cast<uint64_t>(p1) * a.stride + g0, &l_mix[wv][p1][0][0], n, lane, ld,
+      pb_load<P, RD, N16>(a, static_cast<uint64_t>(p1) * a.stride + g0, &l_mix[wv][p1][0][0], n, lane, ld,
                  ((rejm >> p1) & 1u) != 0, ((ixm >> p1) & 1u) != 0, ((rcm >> p1) & 1u) != 0, nx1);
     }
     // ---- phase 1: MaybeUpdate + maybeCommit in message order -> bcasts ----
@@ -947,6 +1049,7 @@ k_progress_step(PArgs a) {
     x.li = li;
     x.snap = a.snap_index ? snap_ld : fi - 1;
     x.lb = lane * a.FP * 4;
+    x.eb = N16 ? 2u : 4u;  // (the accounting's entry width)
     x.row = row_ring;
     uint32_t sent = 0, snapm = 0, tnow = 0;
     // touched: a tracked peer with a message, or a bcast target (every
@@ -976,7 +1079,7 @@ k_progress_step(PArgs a) {
       PB nxt{};  // (the last slot has no next: zeros)
       if constexpr (PF2) {
         if (s2 < static_cast<uint32_t>(S)) {
-          pb_load<P, RD>(sa, static_cast<uint64_t>(s2) * sa.stride + g0, &l_mix[wv][s2][0][0], n, lane,
+          pb_load<P, RD, N16>(sa, static_cast<uint64_t>(s2) * sa.stride + g0, &l_mix[wv][s2][0][0], n, lane,
                      ((tchm >> s2) & 1u) != 0, ((rejm >> s2) & 1u) != 0, ((ixm >> s2) & 1u) != 0,
                      ((rcm >> s2) & 1u) != 0, nxt);
         }
@@ -984,7 +1087,7 @@ k_progress_step(PArgs a) {
         cur.mt = l_mix[wv][s][0][lane];
         cur.ix = ((ixm >> s) & 1u) ? l_mix[wv][s][1][lane] : 0;
       } else if (s1 < static_cast<uint32_t>(S)) {
-        pb_load<P, RD>(sa, static_cast<uint64_t>(s1) * sa.stride + g0, &l_mix[wv][s1][0][0], n, lane,
+        pb_load<P, RD, N16>(sa, static_cast<uint64_t>(s1) * sa.stride + g0, &l_mix[wv][s1][0][0], n, lane,
                    ((tchm >> s1) & 1u) != 0, ((rejm >> s1) & 1u) != 0, ((ixm >> s1) & 1u) != 0,
                    ((rcm >> s1) & 1u) != 0, nxt);
       }
@@ -1006,6 +1109,7 @@ k_progress_step(PArgs a) {
       pr_unpack(p, cur.w);
       p.reset = 0;
       const uint32_t rep0 = p.rep;
+      const uint64_t nx_old = cur.nx;  // (the 16-bit form's base as loaded)
       // PendingSnapshot is read only in StateSnapshot (every other state only
       // ever overwrites it)
       const bool need_pd = touched && p.state == QE_PR_SNAPSHOT;
@@ -1020,6 +1124,7 @@ k_progress_step(PArgs a) {
         const uint64_t rb = (static_cast<uint64_t>(s) * sa.stride + g0) * sa.FP;
         x.rlo = mk_rsrc(sa.ilo + rb, n * sa.FP * 4);
         x.rhi = mk_rsrc(sa.ihi + rb, n * sa.FP * 4);
+        if constexpr (N16) x.r16 = mk_rsrc(sa.infl16 + row * QE_RING16_MAX_F, n * 16);
       }
       const bool up = (upd >> s) & 1u;
       const uint32_t c_old = p.count;
@@ -1029,7 +1134,10 @@ k_progress_step(PArgs a) {
       // arrived, FreeLE continues from memory)
       uint32_t rlo[kRingChunk], rhi[kRingChunk];
       uint32_t npre = 0;
-      if (row_ring) {
+      if (N16) {  // (row form: F <= kRingChunk, host-checked)
+        ring_load_n16<P>(x, touched && c_old > 0, rep0, sa.FP, rlo, rhi, P ? cur.rl : nullptr,
+                         nx_old);
+      } else if (row_ring) {
         ring_load_row<P>(x, touched && c_old > 0, rep0, sa.FP, rlo, rhi, P ? cur.rl : nullptr);
       } else {
 #pragma unroll
@@ -1223,7 +1331,8 @@ k_progress_step(PArgs a) {
       const uint32_t km = lp ? kLoop : k2 + k3;
       if (__builtin_amdgcn_ballot_w64(km > 0)) send_burst<ACCT>(p, lp ? k2 != 0 : true, km, x, r2, ac);
       if (__builtin_amdgcn_ballot_w64(lp && k3 > 0)) send_burst<ACCT>(p, true, lp ? k3 : 0u, x, r2, ac);
-      if (row_ring) ring_store_row<P>(p, x, r1, r2, touched, rep0, c_old, sa.FP, rlo, rhi);
+      if constexpr (N16) ring_store_n16<P>(p, x, r1, r2, touched, nx_old, sa.FP, rlo, rhi);
+      else if (row_ring) ring_store_row<P>(p, x, r1, r2, touched, rep0, c_old, sa.FP, rlo, rhi);
       // ---- stores: the peer's new Progress (unchanged words skipped) ----
       const uint32_t nw = pr_pack(p);
       const bool tw = touched;
@@ -1359,16 +1468,17 @@ k_progress_step(PArgs a) {
 // sets keep tile t+1's Progress loads in flight while tile t sends.
 constexpr int kSendTPW = 8;
 
-template <int S>
+template <int S, bool N16>
 struct SendSet {
   uint64_t fi, li, sn;
   uint64_t nx[S];
   uint32_t pw[S];
+  u32x4 rg[N16 ? S : 1];  // ABI 8: each wanted peer's 16-bit ring, prefetched
 };
 
-template <int S>
+template <int S, bool N16>
 __device__ __forceinline__ void ps_issue(const PArgs &a, uint64_t t, uint32_t lane, uint32_t w,
-                                         SendSet<S> &x) {
+                                         SendSet<S, N16> &x) {
   const uint64_t g0 = t * 64;
   const uint32_t n = tile_n(a.G, t);
   const uint32_t o8 = lane * 8, o4 = lane * 4;
@@ -1380,12 +1490,14 @@ __device__ __forceinline__ void ps_issue(const PArgs &a, uint64_t t, uint32_t la
     const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
     x.nx[s] = bld64<kNT>(mk_rsrc(a.next + row, n * 8), bit_off(w, s, o8));
     x.pw[s] = bld32<kNT>(mk_rsrc(a.pw + row, n * 4), bit_off(w, s, o4));
+    if constexpr (N16)
+      x.rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), bit_off(w, s, lane * 16));
   }
 }
 
-template <int S, typename MT>
+template <int S, typename MT, bool N16>
 __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t lane, uint32_t w,
-                                          const SendSet<S> &x) {
+                                          const SendSet<S, N16> &x) {
   const uint64_t g0 = t * 64;
   const uint32_t n = tile_n(a.G, t);
   Acct<false> ac;
@@ -1397,8 +1509,10 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
   xs.snap = a.snap_index ? x.sn : x.fi - 1;
   xs.lb = lane * a.FP * 4;
   // one maybeSendAppend appends at most one entry: its 32-bit word stored
-  // directly at its ring position (one instruction, memory form)
-  xs.row = false;
+  // directly at its ring position (one instruction, memory form); in the
+  // 16-bit form (ABI 8) the peer's 16-byte ring is rewritten whole, re-based
+  // on the new Next (row form)
+  xs.row = N16;
   uint32_t sent = 0, snapm = 0;
 #pragma unroll
   for (int s = 0; s < S; s++) {
@@ -1414,12 +1528,22 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
       const uint64_t rb = (static_cast<uint64_t>(s) * a.stride + g0) * a.FP;
       xs.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
       xs.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+      if constexpr (N16) xs.r16 = mk_rsrc(a.infl16 + (static_cast<uint64_t>(s) * a.stride + g0) * QE_RING16_MAX_F, n * 16);
     }
     xs.count_msgs = 0;
     xs.first_index = 0;
     xs.snapped = false;
     PRun run{0, 0, 0};
+    uint32_t rlo[kRingChunk], rhi[kRingChunk];
+    if constexpr (N16) {
+      const uint32_t pre[4] = {x.rg[s].x, x.rg[s].y, x.rg[s].z, x.rg[s].w};
+      ring_load_n16<false>(xs, on && p.count > 0, p.rep, a.FP, rlo, rhi, pre, x.nx[s]);
+    }
     send_burst<false, kNT>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
+    if constexpr (N16) {
+      const PRun none{0, 0, 0};
+      ring_store_n16<false>(p, xs, run, none, on, x.nx[s], a.FP, rlo, rhi);
+    }
     const uint32_t nw = pr_pack(p);
     const bool wn = on && p.next != x.nx[s], wp = on && xs.snapped, ww = on && nw != x.pw[s];
     if (__builtin_amdgcn_ballot_w64(wn)) bst64<kNT>(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
@@ -1433,7 +1557,7 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
   bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
 }
 
-template <int S, typename MT>
+template <int S, typename MT, bool N16 = false>
 __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   __shared__ uint32_t lds_w[kBlock / 64][kSendTPW][64];
@@ -1457,15 +1581,15 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
   // tile k of the chunk, or past the end (no loads, no stores, want 0)
   auto tix = [&](uint32_t k) -> uint64_t { return k < nt ? t0 + k : ntiles; };
   auto want_of = [&](uint32_t k) -> uint32_t { return k < nt ? lds_w[wv][k][lane] : 0u; };
-  SendSet<S> xa, xb;
-  ps_issue<S>(a, tix(0), lane, want_of(0), xa);
+  SendSet<S, N16> xa, xb;
+  ps_issue<S, N16>(a, tix(0), lane, want_of(0), xa);
   for (uint32_t k = 0; k < nt; k += 2) {
-    ps_issue<S>(a, tix(k + 1), lane, want_of(k + 1), xb);
+    ps_issue<S, N16>(a, tix(k + 1), lane, want_of(k + 1), xb);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the sends
-    ps_finish<S, MT>(a, tix(k), lane, want_of(k), xa);
-    ps_issue<S>(a, tix(k + 2), lane, want_of(k + 2), xa);
+    ps_finish<S, MT, N16>(a, tix(k), lane, want_of(k), xa);
+    ps_issue<S, N16>(a, tix(k + 2), lane, want_of(k + 2), xa);
     __builtin_amdgcn_sched_barrier(0);
-    ps_finish<S, MT>(a, tix(k + 1), lane, want_of(k + 1), xb);
+    ps_finish<S, MT, N16>(a, tix(k + 1), lane, want_of(k + 1), xb);
   }
 }
 
@@ -1482,7 +1606,7 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
 // appends once per launch, so a launch is one MsgProp per group.
 constexpr uint64_t kPropSalt = 0x9E6C63D0676A9A99ull;
 
-template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT>
+template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
 __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint32_t MB = sizeof(MT);
@@ -1573,6 +1697,7 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
     const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
     uint64_t mt[S], nx[S];
     uint32_t pw[S];
+    u32x4 rg[N16 ? S : 1];  // ABI 8: the 16-bit rings of the peers loaded
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -1580,6 +1705,8 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
       mt[s] = bld64(mk_rsrc(a.match + row, n * 8), k8);
       nx[s] = bld64(mk_rsrc(a.next + row, n * 8), ld ? o8 : kOOB);
       pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), ld ? o4 : kOOB);
+      if constexpr (N16)
+        rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), ld ? lane * 16 : kOOB);
     }
     // this tile's stage-B values the gates below still use (named before the
     // next tile's loads take the struct)
@@ -1683,7 +1810,8 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
         x.li = li2;
         x.snap = sn;
         x.lb = lane * a.FP * 4;
-        x.row = false;
+        x.eb = N16 ? 2u : 4u;
+        x.row = N16;  // the 16-bit form: each target's ring rewritten whole (ABI 8)
 #pragma unroll
         for (int s = 0; s < S; s++) {
           const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -1699,21 +1827,39 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
             const uint64_t rb = row * a.FP;
             x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
             x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+            if constexpr (N16) x.r16 = mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16);
           }
           x.count_msgs = 0;
           x.first_index = 0;
           x.snapped = false;
           PRun run{0, 0, 0};
+          uint32_t rlo[kRingChunk], rhi[kRingChunk];
+          if constexpr (N16) {
+            const uint32_t pre[4] = {rg[s].x, rg[s].y, rg[s].z, rg[s].w};
+            ring_load_n16<false>(x, (tgt || is_self) && p.count > 0, p.rep, a.FP, rlo, rhi, pre,
+                                 nx[s]);
+          }
           if (__builtin_amdgcn_ballot_w64(tgt)) send_burst<ACCT>(p, true, tgt ? 1u : 0u, x, run, ac);
+          // the 16-bit form: a target's ring re-based on its new Next; the
+          // leader's own re-based if its MaybeUpdate moved its Next while it
+          // held entries (never, from becomeLeader on: nothing is sent to it)
+          uint32_t nws_s = nws;
+          if constexpr (N16) {
+            PR q = p;
+            if (is_self) q = ps;
+            ring_store_n16<false>(q, x, run, PRun{0, 0, 0}, tgt || is_self, nx[s], a.FP, rlo, rhi);
+            if (is_self) nws_s = pr_pack(q);
+            else p.rep = q.rep;
+          }
           const uint32_t nw = pr_pack(p);
           const bool wn = tgt && p.next != nx[s], ww = tgt && nw != pw[s], wp = tgt && x.snapped;
-          const bool sn_ = is_self && ps.next != sx, sw_ = is_self && nws != sw;
+          const bool sn_ = is_self && ps.next != sx, sw_ = is_self && nws_s != sw;
           if (__builtin_amdgcn_ballot_w64(is_self && up))
             bst64(ps.match, mk_rsrc(a.match + row, n * 8), (is_self && up) ? o8 : kOOB);
           if (__builtin_amdgcn_ballot_w64(wn || sn_))
             bst64(is_self ? ps.next : p.next, mk_rsrc(a.next + row, n * 8), (wn || sn_) ? o8 : kOOB);
           if (__builtin_amdgcn_ballot_w64(ww || sw_))
-            bst32(is_self ? nws : nw, mk_rsrc(a.pw + row, n * 4), (ww || sw_) ? o4 : kOOB);
+            bst32(is_self ? nws_s : nw, mk_rsrc(a.pw + row, n * 4), (ww || sw_) ? o4 : kOOB);
           if (__builtin_amdgcn_ballot_w64(wp))
             bst64(p.pending, mk_rsrc(a.pending + row, n * 8), wp ? o8 : kOOB);
           ac.add(tgt, 12);
@@ -1722,7 +1868,7 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
           ac.add(wp, 8);
           ac.add(is_self && up, 8);
           ac.add(sn_, 8);
-          ac.add(is_self && ((nws ^ sw) & ~QE_PW_RING_MASK) != 0, 4);
+          ac.add(is_self && ((nws_s ^ sw) & ~QE_PW_RING_MASK) != 0, 4);
           sentm |= (tgt && x.count_msgs) ? (1u << s) : 0u;
           snapm |= (tgt && x.snapped) ? (1u << s) : 0u;
         }
@@ -1765,7 +1911,7 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
 // ring appends, as qe_progress_send).
 constexpr uint64_t kSwitchSalt = 0x2545F4914F6CDD1Dull;
 
-template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT>
+template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
 __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint32_t MB = sizeof(MT);
@@ -1828,6 +1974,7 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
     const uint32_t vm = h.mi | h.mo;
     uint64_t mt[S], nx[S];
     uint32_t pw[S];
+    u32x4 rg[N16 ? S : 1];  // ABI 8: the 16-bit rings of the targets
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -1835,6 +1982,8 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
       mt[s] = bld64(mk_rsrc(a.match + row, n * 8), bit_off(go ? vm : 0u, s, o8));
       nx[s] = bld64(mk_rsrc(a.next + row, n * 8), bit_off(tgt, s, o8));
       pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), bit_off(tgt, s, o4));
+      if constexpr (N16)
+        rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), bit_off(tgt, s, lane * 16));
     }
     // round trip A of the wave's next tile, before this tile's stores
     load_a(t + nwaves, ha);
@@ -1863,7 +2012,8 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
       x.li = li;
       x.snap = sn;
       x.lb = lane * a.FP * 4;
-      x.row = false;
+      x.eb = N16 ? 2u : 4u;
+      x.row = N16;  // the 16-bit form: each target's ring rewritten whole (ABI 8)
 #pragma unroll
       for (int s = 0; s < S; s++) {
         const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -1878,12 +2028,19 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
           const uint64_t rb = row * a.FP;
           x.rlo = mk_rsrc(a.ilo + rb, n * a.FP * 4);
           x.rhi = mk_rsrc(a.ihi + rb, n * a.FP * 4);
+          if constexpr (N16) x.r16 = mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16);
         }
         x.count_msgs = 0;
         x.first_index = 0;
         x.snapped = false;
         PRun run{0, 0, 0};
+        uint32_t rlo[kRingChunk], rhi[kRingChunk];
+        if constexpr (N16) {
+          const uint32_t pre[4] = {rg[s].x, rg[s].y, rg[s].z, rg[s].w};
+          ring_load_n16<false>(x, on && p.count > 0, p.rep, a.FP, rlo, rhi, pre, nx[s]);
+        }
         if (__builtin_amdgcn_ballot_w64(on)) send_burst<ACCT>(p, adv, on ? 1u : 0u, x, run, ac);
+        if constexpr (N16) ring_store_n16<false>(p, x, run, PRun{0, 0, 0}, on, nx[s], a.FP, rlo, rhi);
         const uint32_t nw = pr_pack(p);
         const bool wn = on && p.next != nx[s], ww = on && nw != pw[s], wp = on && x.snapped;
         if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);

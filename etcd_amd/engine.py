@@ -307,10 +307,12 @@ class ProgressState:
     mask-typed, read_head u32 (starting at context 1), read_count u8; ABI 7:
     read_cap > QE_READ_QUEUE adds the overflow ring read_ovf [G][read_cap]
     mask-typed), "read_keys" (ABI 7: [G][cap] u64 request keys, for
-    qe_read_index's duplicate check)."""
+    qe_read_index's duplicate check).  ring16 (ABI 8): the rings in the
+    16-bit form, `infl16` [S][stride][8] offsets below Next (F <= 8, S <= 9,
+    R <= 4; ilo / ihi then hold the wide peers)."""
 
     def __init__(self, G, S, F, R, device="cuda", masks=(), group_offset=0, stride=None,
-                 extras=(), max_ents=0, read_cap=0):
+                 extras=(), max_ents=0, read_cap=0, ring16=False):
         if not 1 <= S <= _lib.QE_MAX_SLOTS or not 1 <= F <= _lib.QE_MAX_INFLIGHT:
             raise ValueError("bad num_slots / inflight_cap")
         if not 1 <= R <= _lib.QE_MAX_LOG_RUNS:
@@ -359,6 +361,10 @@ class ProgressState:
                          if "reads" in extras and cap > rq else None)
         self.read_keys = (torch.zeros(self.G * cap, dtype=i64, device=dev)
                           if "read_keys" in extras else None)
+        if ring16 and (self.F > _lib.QE_RING16_MAX_F or self.S > _lib.QE_RING16_MAX_SLOTS or self.R > 4):
+            raise ValueError("the 16-bit Inflights form needs F <= 8, S <= 9, R <= 4")
+        self.infl16 = (torch.zeros(n * _lib.QE_RING16_MAX_F, dtype=torch.int16, device=dev)
+                       if ring16 else None)
 
     def struct(self):
         return _lib.QeProgress(
@@ -369,12 +375,13 @@ class ProgressState:
             _ptr(self.run_term), _ptr(self.run_count), _ptr(self.inc), _ptr(self.out),
             _ptr(self.tracked), _ptr(self.self_slot), _ptr(self.lead_transferee),
             _ptr(self.snap_index), self.max_ents, 0, _ptr(self.read_acks), _ptr(self.read_head),
-            _ptr(self.read_count), self.read_cap, 0, _ptr(self.read_ovf), _ptr(self.read_keys))
+            _ptr(self.read_count), self.read_cap, 0, _ptr(self.read_ovf), _ptr(self.read_keys),
+            _ptr(self.infl16))
 
     ARRAYS = ("match", "next", "pending", "peer", "ilo", "ihi", "committed",
               "term_start", "first_index", "last_index", "run_first", "run_term", "run_count",
               "inc", "out", "tracked", "self_slot", "lead_transferee", "snap_index",
-              "read_acks", "read_head", "read_count", "read_ovf", "read_keys")
+              "read_acks", "read_head", "read_count", "read_ovf", "read_keys", "infl16")
 
     def load_host(self, **arrays):
         """numpy arrays (uint64 as uint64, masks as uint8/uint16, peer words
@@ -390,9 +397,11 @@ class ProgressState:
         as they are."""
         ibuf = arrays.pop("ibuf", None)
         fields = {k: arrays.pop(k) for k in ("flags", "istart", "icount") if k in arrays}
-        raw_rings = "ilo" in arrays or "ihi" in arrays  # the caller's ring words stand
-        if ibuf is None and not raw_rings and (fields or "peer" in arrays):
-            ibuf = self.rings()  # decoded with the words in place now
+        raw_rings = "ilo" in arrays or "ihi" in arrays or "infl16" in arrays  # the caller's words stand
+        # (the 16-bit form's entries are offsets below Next: a new Next re-bases them)
+        rebase = fields or "peer" in arrays or (self.infl16 is not None and "next" in arrays)
+        if ibuf is None and not raw_rings and rebase:
+            ibuf = self.rings()  # decoded with the words (and Next) in place now
         if fields:
             n = max(np.asarray(v).size for v in fields.values())
             z = np.zeros(n, np.uint32)
@@ -443,8 +452,16 @@ class ProgressState:
         peer = self.peer.cpu().numpy().view(np.uint32).copy()
         lo = np.zeros(S * st * self.FP, np.uint32)
         hi = np.zeros_like(lo)
-        check("qe_ring_pack", _lib.lib().qe_ring_pack(
-            self.G, S, F, st, ent.ctypes.data, peer.ctypes.data, lo.ctypes.data, hi.ctypes.data))
+        if self.infl16 is not None:  # ABI 8: offsets below Next, wide where they do not fit
+            nxt = self.next.cpu().numpy().view(np.uint64).copy()
+            o16 = np.zeros(S * st * _lib.QE_RING16_MAX_F, np.uint16)
+            check("qe_ring_pack16", _lib.lib().qe_ring_pack16(
+                self.G, S, F, st, ent.ctypes.data, nxt.ctypes.data, peer.ctypes.data,
+                o16.ctypes.data, lo.ctypes.data, hi.ctypes.data))
+            self.infl16.copy_(torch.from_numpy(o16.view(np.int16)).to(self.device))
+        else:
+            check("qe_ring_pack", _lib.lib().qe_ring_pack(
+                self.G, S, F, st, ent.ctypes.data, peer.ctypes.data, lo.ctypes.data, hi.ctypes.data))
         for dst, v in ((self.peer, peer), (self.ilo, lo), (self.ihi, hi)):
             dst.copy_(torch.from_numpy(v.view(np.int32)).to(self.device))
 
@@ -465,6 +482,19 @@ class ProgressState:
         start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
         k = torch.arange(F, device=self.device).view(1, F)
         live = torch.remainder(k - start.view(st, 1), F) < count.view(st, 1)
+        if self.infl16 is not None:  # ABI 8: offsets below Next (the rule of qe_ring_pack16)
+            top = (self.next[rows] - 1).view(st, 1)
+            d = top - ent  # int64; entries and Next below 2^63 here
+            off = d & 0xFFFF
+            fits = ((d >= 0) & (d <= 0xFFFF)) | ~live
+            o = torch.zeros(st, _lib.QE_RING16_MAX_F, dtype=torch.int64, device=self.device)
+            o[:, :F] = off
+            self.infl16.view(S * st, _lib.QE_RING16_MAX_F)[rows] = torch.where(
+                o >= (1 << 15), o - (1 << 16), o).to(torch.int16)
+            rep = torch.where(fits.all(1), 0, _lib.QE_PF_RING_WIDE)
+            w = (w & ~_lib.QE_PW_RING_MASK & 0xFFFFFFFF) | rep
+            self.peer[rows] = as_i32(w)
+            return
         hmin = torch.where(live, hi, 1 << 40).amin(1)
         hmax = torch.where(live, hi, -1).amax(1)
         uni = (hmin == hmax) & (hmax <= _lib.QE_RING_EPOCH_MAX)
@@ -483,9 +513,16 @@ class ProgressState:
         lo = self.ilo.cpu().numpy().view(np.uint32)
         hi = self.ihi.cpu().numpy().view(np.uint32)
         ent = np.zeros(S * st * F, np.uint64)
-        check("qe_ring_unpack", _lib.lib().qe_ring_unpack(
-            self.G, S, F, st, lo.ctypes.data, hi.ctypes.data,
-            np.ascontiguousarray(peer).ctypes.data, ent.ctypes.data))
+        if self.infl16 is not None:  # ABI 8
+            o16 = self.infl16.cpu().numpy().view(np.uint16)
+            nxt = self.next.cpu().numpy().view(np.uint64)
+            check("qe_ring_unpack16", _lib.lib().qe_ring_unpack16(
+                self.G, S, F, st, o16.ctypes.data, lo.ctypes.data, hi.ctypes.data,
+                nxt.ctypes.data, np.ascontiguousarray(peer).ctypes.data, ent.ctypes.data))
+        else:
+            check("qe_ring_unpack", _lib.lib().qe_ring_unpack(
+                self.G, S, F, st, lo.ctypes.data, hi.ctypes.data,
+                np.ascontiguousarray(peer).ctypes.data, ent.ctypes.data))
         return np.ascontiguousarray(ent.reshape(S, st, F).transpose(0, 2, 1)).reshape(-1)
 
     def host(self):

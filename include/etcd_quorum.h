@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define QE_ABI_VERSION 7  /* 7: see INTEGRATION.md "ABI 7" (changes listed there) */
+#define QE_ABI_VERSION 8  /* 8: see INTEGRATION.md "ABI 8" (changes listed there) */
 
 #define QE_INDEX_INF UINT64_MAX
 #define QE_MAX_SLOTS 16
@@ -296,7 +296,23 @@ int qe_election_steps(const qe_election_state *st,
  * which is then H.  qe_ring_pack produces it and the kernels restore it
  * whenever they append (a ring they only free entries from may stay wide).
  * qe_ring_pack / qe_ring_unpack convert plain uint64 rings.  Ring
- * representation bits are not Progress state: QE_PW_RING_MASK selects them. */
+ * representation bits are not Progress state: QE_PW_RING_MASK selects them.
+ *
+ * ABI 8, the 16-bit form (qe_progress.infl16 non-NULL; F <= QE_RING16_MAX_F):
+ * the rings live in infl16 [S][stride][8] as offsets below Next,
+ *   entry k = Progress.Next - 1 - infl16[k]        (not wide)
+ *   entry k = (infl_hi[k] << 32) | infl_lo[k]       (QE_PF_RING_WIDE)
+ * -- 16 bytes per peer, two peers per 32-byte HBM sector.  Live Inflights
+ * entries are the last indices of MsgApps sent, all below Next; Next moves
+ * only when an append rewrites the ring (OptimisticUpdate), or when the ring
+ * empties (MaybeUpdate past every sent index, ResetState).  A peer is wide
+ * iff some live entry lies outside [Next - 65536, Next - 1] (a window of
+ * more than 65536 indices, or an inconsistent input); the epoch bits are 0.
+ * The kernels re-encode a peer's ring whenever they append to it or change
+ * its Next while entries are live.  Entry points that write Next without
+ * knowing the rings (qe_apply_append_resps, a host) must not be used on the
+ * Next rows of such a state while entries are live: they would re-base the
+ * entries.  qe_ring_pack16 / qe_ring_unpack16 convert plain uint64 rings. */
 #define QE_PR_PROBE 0
 #define QE_PR_REPLICATE 1
 #define QE_PR_SNAPSHOT 2
@@ -318,6 +334,9 @@ int qe_election_steps(const qe_election_state *st,
  * ring of F <= 8 is one or two 16-byte accesses, one 32-byte HBM sector) */
 #define QE_RING_PITCH(F) (((uint32_t)(F) + 3u) & ~3u)
 #define QE_MAX_INFLIGHT 255     /* Inflights capacity (MaxInflightMsgs)      */
+#define QE_RING16_MAX_F 8       /* ABI 8: the 16-bit form holds up to 8 entries */
+#define QE_RING16_MAX_SLOTS 9   /* ABI 8: ... for up to 9 slots (the pipelined
+                                   Progress kernels' shapes) and log_runs <= 4 */
 #define QE_MAX_LOG_RUNS 16      /* term runs of the leader-log model          */
 
 /* message kinds of qe_peer_msgs.type (any other value: no message) */
@@ -424,6 +443,13 @@ typedef struct qe_progress {
                                    tracked.  Given, it must have been given to
                                    every qe_read_index that queued the pending
                                    entries                                   */
+  /* ABI 8 */
+  uint16_t *infl16;             /* [S][stride][8] rw or NULL: the 16-bit
+                                   Inflights form (see QE_RING16_MAX_F above;
+                                   infl_lo / infl_hi then hold the wide peers
+                                   only).  Requires inflight_cap <=
+                                   QE_RING16_MAX_F, num_slots <=
+                                   QE_RING16_MAX_SLOTS, log_runs <= 4        */
 } qe_progress;
 
 /* One round of peer responses: message of slot s for group g at
@@ -791,6 +817,18 @@ int qe_ring_pack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
 int qe_ring_unpack(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
                    uint64_t stride, const uint32_t *infl_lo, const uint32_t *infl_hi,
                    const uint32_t *peer, uint64_t *entries);
+/* ABI 8, HOST pointers: the same for the 16-bit form (qe_progress.infl16):
+ * Next ([S][stride], next) is the base of each peer's offsets.  Every peer
+ * gets the 16-bit form when its live entries fit below its Next, else the
+ * wide form (infl_lo / infl_hi, QE_PF_RING_WIDE); infl_lo / infl_hi are
+ * written for every peer.  inflight_cap <= QE_RING16_MAX_F. */
+int qe_ring_pack16(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                   uint64_t stride, const uint64_t *entries, const uint64_t *next,
+                   uint32_t *peer, uint16_t *infl16, uint32_t *infl_lo, uint32_t *infl_hi);
+int qe_ring_unpack16(uint64_t num_groups, uint32_t num_slots, uint32_t inflight_cap,
+                     uint64_t stride, const uint16_t *infl16, const uint32_t *infl_lo,
+                     const uint32_t *infl_hi, const uint64_t *next, const uint32_t *peer,
+                     uint64_t *entries);
 
 /* ---- sparse MsgAppResp deltas ------------------------------------------ */
 

@@ -180,6 +180,7 @@ class OrcProg(C.Structure):
         ("reserved2", C.c_uint32), ("read_acks", C.c_void_p), ("read_head", C.c_void_p),
         ("read_count", C.c_void_p), ("read_cap", C.c_uint32), ("reserved3", C.c_uint32),
         ("read_ovf", C.c_void_p), ("read_keys", C.c_void_p),
+        ("infl16", C.c_void_p),  # ABI 8: a flag here (the byte rules of 2-B entries)
     ]
 
 
@@ -244,6 +245,8 @@ class ProgressBatch:
         for k in self.OPTIONAL:
             setattr(self, k, None)
         self.read_cap = 0
+        self.ring16 = False  # ABI 8: the device form is the 16-bit one (byte rules only)
+        self._flag = np.ones(1, np.uint8)
 
     @property
     def flags(self):
@@ -293,7 +296,8 @@ class ProgressBatch:
                        P(self.run_count), P(self.inc), P(self.out), P(self.tracked),
                        P(self.self_slot), P(self.lead_transferee), P(self.snap_index),
                        self.max_ents, 0, P(self.read_acks), P(self.read_head),
-                       P(self.read_count), self.read_cap, 0, P(self.read_ovf), P(self.read_keys))
+                       P(self.read_count), self.read_cap, 0, P(self.read_ovf), P(self.read_keys),
+                       P(self._flag) if self.ring16 else None)
 
 
 class StepOut:

@@ -856,27 +856,30 @@ typedef struct orc_pr {
   uint64_t bstride;
   uint32_t reset;              /* ResetState ran this round (byte accounting) */
   uint64_t *acct;              /* byte accounting sink, or NULL             */
+  uint32_t eb;                 /* bytes of one Inflights entry in the device
+                                  form: 4 (32-bit words), 2 (ABI 8 infl16)   */
 } orc_pr;
 
 static inline uint64_t *ib(orc_pr *p, uint32_t k) { return &p->buf[(uint64_t)k * p->bstride]; }
 
 /* inflights.go:55-71 Add (accounting: the entry written, 4 B -- the 32-bit
- * entry word of the device representation, ABI 4; the upper words of a
- * ring straddling a 2^32 boundary are representation overhead, not
+ * entry word of the device representation, ABI 4; 2 B in the 16-bit form,
+ * ABI 8; the upper words of a ring straddling a 2^32 boundary, and the
+ * 16-bit form's re-based offsets, are representation overhead, not
  * counted) */
 static void infl_add(orc_pr *p, uint64_t x) {
   uint32_t nx = p->start + p->count;
   if (nx >= p->size) nx -= p->size;
   *ib(p, nx) = x;
   p->count++;
-  if (p->acct) *p->acct += 4;
+  if (p->acct) *p->acct += p->eb;
 }
 /* inflights.go:87-113 FreeLE (accounting: every entry the loop reads,
- * min(count, freed + 1) of them, 4 B each as in infl_add) */
+ * min(count, freed + 1) of them, eb bytes each as in infl_add) */
 static void infl_free_le(orc_pr *p, uint64_t to) {
   if (p->count == 0) return;
   if (to < *ib(p, p->start)) {
-    if (p->acct) *p->acct += 4;
+    if (p->acct) *p->acct += p->eb;
     return;
   }
   uint32_t idx = p->start, i;
@@ -884,7 +887,7 @@ static void infl_free_le(orc_pr *p, uint64_t to) {
     if (to < *ib(p, idx)) break;
     if (++idx >= p->size) idx -= p->size;
   }
-  if (p->acct) *p->acct += 4 * (uint64_t)(i < p->count ? i + 1 : i);
+  if (p->acct) *p->acct += p->eb * (uint64_t)(i < p->count ? i + 1 : i);
   p->count -= i;
   p->start = idx;
   if (p->count == 0) p->start = 0;
@@ -1012,6 +1015,9 @@ typedef struct orc_prog {
   uint32_t read_cap, reserved3;
   void *read_ovf;
   uint64_t *read_keys;
+  /* ABI 8: non-NULL = the device keeps the rings in the 16-bit form (the
+   * oracle's rings stay uint64; only the byte accounting changes) */
+  const void *infl16;
 } orc_prog;
 
 typedef struct orc_msgs {
@@ -1136,6 +1142,7 @@ static void pr_load2(orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   p->bstride = a->stride;
   p->reset = 0;
   p->acct = NULL;
+  p->eb = a->infl16 ? 2 : 4;
 }
 static void pr_store2(const orc_pr *p, const orc_prog *a, uint32_t s, uint64_t g) {
   uint64_t off = s * a->stride + g;

@@ -75,8 +75,8 @@ def main():
                             "qe::k_progress_step<7, unsigned char, false, false, 4, false,",
                             "qe::k_progress_step<6, unsigned char, true, true, 4, false,",
                             "qe::k_progress_send<5,", "qe::k_check_quorum<5,",
-                            "qe::k_propose<5, unsigned char, false, false, false>",
-                            "qe::k_switch_config<5, unsigned char, true, false, false>",
+                            "qe::k_propose<5, unsigned char, false, false, false,",
+                            "qe::k_switch_config<5, unsigned char, true, false, false,",
                             "qe::k_heartbeat<5,",
                             "qe::k_cv_stream<5, 0,", "qe::k_cv_stream<7, 0,", "qe::k_cv_stream<10, 2,",
                             "qe::k_repl_stream<5,", "qe::k_repl_stream<6,", "qe::k_confchange<5>",

@@ -104,7 +104,7 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_constants_and_introspection():
     L = _lib.lib()
-    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 7
+    assert L.qe_abi_version() == _lib.QE_ABI_VERSION == 8
     assert L.qe_mask_bytes(1) == 1 and L.qe_mask_bytes(8) == 1
     assert L.qe_mask_bytes(9) == 2 and L.qe_mask_bytes(16) == 2
     assert L.qe_mask_bytes(0) == 0 and L.qe_mask_bytes(17) == 0
@@ -301,6 +301,109 @@ def test_set_ring_slot_matches_ring_pack(F):
     got_hi = ps.ihi.numpy().view(np.uint32).reshape(S * st, FP)[:, :F]
     assert np.array_equal(got_lo, lo.reshape(S * st, FP)[:, :F])
     assert np.array_equal(got_hi, hi.reshape(S * st, FP)[:, :F])
+
+
+def _ring16_case(rng, G, S, F):
+    """Peer words and rings for the 16-bit form: Next just above the ring's
+    entries (the window fits), far above it (more than 65536 indices: wide),
+    below some entry (inconsistent: wide), indices near 2^32 and 2^43."""
+    import numpy as np
+    w, ent = _ring_case(rng, G, S, F)
+    e = ent.reshape(S * G, F)
+    hi = e.max(1)
+    kind = rng.integers(0, 4, S * G)
+    nxt = np.where(kind == 0, hi + 1 + rng.integers(0, 300, S * G),
+                   np.where(kind == 1, hi + rng.integers(1, 40000, S * G),
+                            np.where(kind == 2, hi + 70000 + rng.integers(0, 9, S * G),
+                                     hi - rng.integers(0, F, S * G)))).astype(np.uint64)
+    return w, ent, nxt
+
+
+@pytest.mark.parametrize("F", [1, 3, 5, 8])
+def test_ring16_pack_unpack_roundtrip(F):
+    """qe_ring_pack16 / qe_ring_unpack16 (ABI 8): every position round-trips
+    exactly; a peer is in the 16-bit form iff its live entries lie in
+    [Next - 65536, Next - 1], else wide; Progress bits are kept, epoch 0."""
+    import numpy as np
+    rng = np.random.default_rng(160 + F)
+    G, S = 700, 3
+    w, ent, nxt = _ring16_case(rng, G, S, F)
+    FP = _lib.QE_RING_PITCH(F)
+    lo = np.zeros(S * G * FP, np.uint32)
+    hi = np.zeros_like(lo)
+    o16 = np.zeros(S * G * 8, np.uint16)
+    peer = w.copy()
+    L = _lib.lib()
+    assert L.qe_ring_pack16(G, S, F, G, ent.ctypes.data, nxt.ctypes.data, peer.ctypes.data,
+                            o16.ctypes.data, lo.ctypes.data, hi.ctypes.data) == _lib.QE_OK
+    mask = np.uint32(_lib.QE_PW_RING_MASK)
+    assert np.array_equal(peer & ~mask, w & ~mask)
+    assert not ((peer & mask) & ~np.uint32(_lib.QE_PF_RING_WIDE)).any()  # no epoch bits
+    back = np.zeros_like(ent)
+    assert L.qe_ring_unpack16(G, S, F, G, o16.ctypes.data, lo.ctypes.data, hi.ctypes.data,
+                              nxt.ctypes.data, peer.ctypes.data, back.ctypes.data) == _lib.QE_OK
+    e2, b2 = ent.reshape(S * G, F), back.reshape(S * G, F)
+    start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
+    wide = (peer & _lib.QE_PF_RING_WIDE) != 0
+    n16 = 0
+    for i in range(S * G):
+        pos = [(int(start[i]) + j) % F for j in range(int(count[i]))]
+        top = int(nxt[i]) - 1
+        fits = all(int(e2[i, q]) <= top and top - int(e2[i, q]) <= 0xFFFF for q in pos)
+        assert wide[i] == (not fits), i
+        if wide[i]:
+            assert np.array_equal(b2[i], e2[i])
+        else:
+            assert np.array_equal(b2[i, pos], e2[i, pos]), i
+            n16 += bool(pos)
+    assert n16 > 0 and wide.sum() > 0
+    assert L.qe_ring_pack16(G, S, 9, G, None, None, None, None, None, None) == _lib.QE_ERANGE
+    assert L.qe_ring_unpack16(G, S, F, G, None, lo.ctypes.data, hi.ctypes.data, nxt.ctypes.data,
+                              peer.ctypes.data, back.ctypes.data) == _lib.QE_EINVAL
+
+
+@pytest.mark.parametrize("F", [5, 8])
+def test_set_ring_slot16_matches_ring_pack16(F):
+    """ProgressState.set_ring_slot in the 16-bit form (torch ops, CPU
+    tensors here) writes the same offsets and representation bits as
+    qe_ring_pack16 (entries and Next below 2^63)."""
+    import numpy as np
+    import torch
+
+    from etcd_amd import engine
+    rng = np.random.default_rng(60 + F)
+    G, S = 300, 3
+    ps = engine.ProgressState(G, S, F, 1, device="cpu", stride=320, ring16=True)
+    st = ps.stride
+    w, ent, nxt = _ring16_case(rng, st, S, F)
+    big = (ent.reshape(S * st, F) >= (1 << 62)).any(1) | (nxt >= (1 << 62))
+    ent.reshape(S * st, F)[big] &= np.uint64((1 << 40) - 1)  # (torch int64 arithmetic)
+    nxt[big] = ent.reshape(S * st, F)[big].max(1) + 1
+    ps.peer.copy_(torch.from_numpy(w.view(np.int32)))
+    ps.next.copy_(torch.from_numpy(nxt.view(np.int64)))
+    for s in range(S):
+        ps.set_ring_slot(s, torch.from_numpy(ent.reshape(S, st, F)[s].copy().view(np.int64)))
+    FP = _lib.QE_RING_PITCH(F)
+    lo = np.zeros(S * st * FP, np.uint32)
+    hi = np.zeros_like(lo)
+    o16 = np.zeros(S * st * 8, np.uint16)
+    peer = w.copy()
+    assert _lib.lib().qe_ring_pack16(st, S, F, st, ent.ctypes.data, nxt.ctypes.data,
+                                     peer.ctypes.data, o16.ctypes.data, lo.ctypes.data,
+                                     hi.ctypes.data) == _lib.QE_OK
+    assert np.array_equal(ps.peer.numpy().view(np.uint32), peer)
+    got = ps.infl16.numpy().view(np.uint16).reshape(S * st, 8)[:, :F]
+    assert np.array_equal(got, o16.reshape(S * st, 8)[:, :F])
+    back = ps.rings()  # decode through qe_ring_unpack16 (entry-major)
+    e = ent.reshape(S, st, F).transpose(0, 2, 1).reshape(-1)
+    start, count = (w >> 8) & 0xFF, (w >> 16) & 0xFF
+    for i in range(0, S * st, 7):
+        s, g = divmod(i, st)
+        if g >= G:  # (rings() decodes groups < G)
+            continue
+        for j in range(int(count[i])):
+            k = (int(start[i]) + j) % F
+            assert back[(s * F + k) * st + g] == e[(s * F + k) * st + g]
 
 
 def test_load_host_rejects_pending_outside_snapshot():
