@@ -113,7 +113,8 @@ def to_device(eng, pb, masks, extras=()):
     if pb.read_keys is not None:
         extras = tuple(extras) + ("read_keys",)
     ps = eng.ProgressState(pb.G, pb.S, pb.F, pb.R, DEV, masks=masks, stride=pb.stride,
-                           extras=extras, max_ents=pb.max_ents, read_cap=pb.read_cap)
+                           extras=extras, max_ents=pb.max_ents, read_cap=pb.read_cap,
+                           ring16=pb.ring16)
     md = orc.mask_dtype(pb.S)
     ps.load_host(match=pb.match, next=pb.next, pending=pb.pending, peer=pb.pw,
                  ibuf=pb.ibuf, committed=pb.committed,
@@ -196,6 +197,26 @@ def assert_outputs(msgs, o, S):
                                   err_msg="term_commit_index")
 
 
+def ring16_state(rng, pb):
+    """ABI 8: the batch in the 16-bit Inflights form (pb.ring16: the oracle
+    counts 2-byte entries).  Next moved just above the live entries of most
+    peers with a ring (the form holds them), 65536+ above some (wide) and
+    left below others (an inconsistent input: wide); every entry stays
+    exact either way."""
+    pb.ring16 = True
+    S, F, st = pb.S, pb.F, pb.stride
+    live = live_entries(pb.pw, S, F, st).reshape(S, F, st)
+    ent = pb.ibuf.reshape(S, F, st)
+    mx = np.where(live, ent, np.uint64(0)).max(1)
+    has = live.any(1)
+    pick = rng.random((S, st))
+    nxt = pb.next.reshape(S, st)
+    new = np.where(pick < 0.75, mx + np.uint64(1) + rng.integers(0, 3, (S, st)).astype(np.uint64),
+                   np.where(pick < 0.85, mx + np.uint64(65536) + rng.integers(0, 3, (S, st)).astype(np.uint64),
+                            nxt))
+    pb.next[:] = np.where(has, new, nxt).reshape(-1)
+
+
 def random_queue(rng, pb):
     """A random ReadIndex queue per group (ABI 5): 0..4 pending requests with
     random acks (dead entries hold garbage), context numbers from near 1 to
@@ -238,9 +259,27 @@ def test_progress_rounds_match_oracle(eng, S, masks, extras, R, F):
     access (F = 3), padded pitch (F = 5) and two accesses (F = 8), and
     memory rings (F = 32).  Odd rounds run the instrumented variant, whose
     byte count must equal the oracle's exactly."""
-    rng = np.random.default_rng(100 + S + 7 * len(extras) + 31 * R + F)
+    rounds_vs_oracle(eng, S, masks, extras, R, F, ring16=False)
+
+
+@pytest.mark.parametrize("F", [3, 5, 8])
+@pytest.mark.parametrize("S,masks,extras", [(1, (), ()), (3, (), EXTRAS), (5, (), ()),
+                                            (5, ("inc",), EXTRAS), (7, ("inc", "out"), EXTRAS),
+                                            (9, (), EXTRAS)])
+def test_progress_rounds_ring16_match_oracle(eng, S, masks, extras, F):
+    """The same rounds with the rings in the 16-bit form (ABI 8): the
+    pipelined step, the send, CheckQuorum and ReadIndex on states whose rings
+    mostly fit below Next, some wide; the instrumented variant counts 2-byte
+    entries, as the oracle does."""
+    rounds_vs_oracle(eng, S, masks, extras, 3, F, ring16=True)
+
+
+def rounds_vs_oracle(eng, S, masks, extras, R, F, ring16):
+    rng = np.random.default_rng(100 + S + 7 * len(extras) + 31 * R + F + 1000 * ring16)
     G = 3001
     pb = random_state(rng, G, S, F, R, masks, extras, max_ents=int(rng.integers(0, 4)))
+    if ring16:
+        ring16_state(rng, pb)
     reads = "lead_transferee" in extras  # the ReadIndex queue with the full extras
     if reads:
         random_queue(rng, pb)

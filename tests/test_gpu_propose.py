@@ -74,22 +74,29 @@ def load_props(eng, ps, ne, payload, cc, applied, pci, unc, max_unc, flags=0):
     return pr
 
 
-@pytest.mark.parametrize("S,F,masks,extras,max_cc,max_ents", [
-    (1, 8, (), EXTRAS, 0, 0), (3, 3, ("inc",), EXTRAS, 2, 1), (5, 8, (), ("self_slot",), 0, 0),
-    (5, 8, ("inc", "out"), EXTRAS, 3, 2), (7, 32, (), EXTRAS, 1, 0),
-    (10, 8, ("inc", "out"), EXTRAS, 2, 3), (16, 5, ("inc",), EXTRAS, 8, 0)])
+@pytest.mark.parametrize("S,F,masks,extras,max_cc,max_ents,ring16", [
+    (1, 8, (), EXTRAS, 0, 0, False), (3, 3, ("inc",), EXTRAS, 2, 1, False),
+    (5, 8, (), ("self_slot",), 0, 0, False), (5, 8, ("inc", "out"), EXTRAS, 3, 2, False),
+    (7, 32, (), EXTRAS, 1, 0, False), (10, 8, ("inc", "out"), EXTRAS, 2, 3, False),
+    (16, 5, ("inc",), EXTRAS, 8, 0, False),
+    (3, 8, ("inc",), EXTRAS, 2, 1, True), (5, 5, (), ("self_slot",), 0, 0, True),
+    (9, 8, ("inc", "out"), EXTRAS, 3, 2, True)])
 @pytest.mark.parametrize("flags", [0, 1])
-def test_propose_matches_oracle(eng, S, F, masks, extras, max_cc, max_ents, flags):
+def test_propose_matches_oracle(eng, S, F, masks, extras, max_cc, max_ents, flags, ring16):
     """Random leader states (every Progress state, compacted Next, full and
     empty rings, voters without a Progress, leaders without one, transfers
     in progress) and random proposals (none, several entries, conf-change
     entries refused or accepted, uncommitted tails at and over the limit):
     state, last_index, pendingConfIndex, uncommittedSize, every output, the
     statistics and the algorithmic byte count equal the oracle's, over two
-    launches in a row (flags 1: appendEntry alone)."""
-    rng = np.random.default_rng(7000 + 31 * S + F + flags)
+    launches in a row (flags 1: appendEntry alone); ring16: the rings in
+    the 16-bit form (ABI 8)."""
+    from tests.test_gpu_progress import ring16_state
+    rng = np.random.default_rng(7000 + 31 * S + F + flags + 500 * ring16)
     G = 4099
     pb = random_state(rng, G, S, F, 3, masks, extras, max_ents=max_ents)
+    if ring16:
+        ring16_state(rng, pb)
     ps = to_device(eng, pb, masks, extras)
     for rnd in range(2):
         ne, payload, cc, applied, pci, unc = random_proposals(rng, pb, max_cc)

@@ -53,20 +53,25 @@ def new_config(rng, pb, masks):
     pb.lead_transferee = np.where(rng.random(G) < 0.5, 0xFF, rng.integers(0, S, G)).astype(np.uint8)
 
 
-@pytest.mark.parametrize("S,F,masks,max_ents", [
-    (1, 8, ("inc",), 0), (3, 3, ("inc",), 1), (5, 8, ("inc",), 0), (5, 8, ("inc", "out"), 2),
-    (7, 32, ("inc",), 0), (10, 8, ("inc", "out"), 3), (16, 5, ("inc", "out"), 0)])
+@pytest.mark.parametrize("S,F,masks,max_ents,ring16", [
+    (1, 8, ("inc",), 0, False), (3, 3, ("inc",), 1, False), (5, 8, ("inc",), 0, False),
+    (5, 8, ("inc", "out"), 2, False), (7, 32, ("inc",), 0, False),
+    (10, 8, ("inc", "out"), 3, False), (16, 5, ("inc", "out"), 0, False),
+    (5, 8, ("inc",), 0, True), (9, 5, ("inc", "out"), 2, True)])
 @pytest.mark.parametrize("all_groups", [False, True])
-def test_switch_config_matches_oracle(eng, S, F, masks, max_ents, all_groups):
+def test_switch_config_matches_oracle(eng, S, F, masks, max_ents, all_groups, ring16):
     """Random leader states (every Progress state, compacted Next, full and
     empty rings) under random new configurations: result (outcome and the
     transfer-abort bit), sent / snap masks, committed, lead_transferee, every
     Progress field and ring, the statistics and the algorithmic byte count
     equal the oracle's, over two launches in a row (the second sees the
     first's sends: probes paused, commits already made)."""
-    rng = np.random.default_rng(8100 + 37 * S + F + all_groups)
+    from tests.test_gpu_progress import ring16_state
+    rng = np.random.default_rng(8100 + 37 * S + F + all_groups + 500 * ring16)
     G = 4099
     pb = random_state(rng, G, S, F, 3, masks, EXTRAS, max_ents=max_ents)
+    if ring16:  # ABI 8: the 16-bit Inflights form
+        ring16_state(rng, pb)
     new_config(rng, pb, masks)
     ps = to_device(eng, pb, masks, EXTRAS)
     md = orc.mask_dtype(S)
@@ -118,10 +123,11 @@ def test_switch_config_argument_errors(eng):
     assert L.qe_switch_config(C.byref(p), C.byref(q), None, None) == eng._lib.QE_OK
 
 
-@pytest.mark.parametrize("S,F,masks,max_ents,reads", [
-    (1, 8, (), 0, False), (3, 8, ("inc",), 1, True), (5, 8, (), 0, True),
-    (5, 32, ("inc", "out"), 2, False), (9, 8, ("inc",), 0, True), (16, 5, ("inc", "out"), 0, False)])
-def test_become_leader_matches_oracle(eng, S, F, masks, max_ents, reads):
+@pytest.mark.parametrize("S,F,masks,max_ents,reads,ring16", [
+    (1, 8, (), 0, False, False), (3, 8, ("inc",), 1, True, False), (5, 8, (), 0, True, False),
+    (5, 32, ("inc", "out"), 2, False, False), (9, 8, ("inc",), 0, True, False),
+    (16, 5, ("inc", "out"), 0, False, False), (5, 8, ("inc",), 1, True, True)])
+def test_become_leader_matches_oracle(eng, S, F, masks, max_ents, reads, ring16):
     """qe_become_leader (raft.becomeLeader + reset, raft.go:724-759,
     :590-613) against the oracle on random states: elected and not, leaders
     without a Progress, full run tables, a new term equal to the last run's
@@ -129,11 +135,13 @@ def test_become_leader_matches_oracle(eng, S, F, masks, max_ents, reads):
     (compacted logs: nothing to an inactive peer); every Progress field, the
     log model (runs, term start, lastIndex, committed), the outputs and the
     statistics equal the oracle's."""
-    from tests.test_gpu_progress import random_queue
-    rng = np.random.default_rng(8300 + 11 * S + F)
+    from tests.test_gpu_progress import random_queue, ring16_state
+    rng = np.random.default_rng(8300 + 11 * S + F + 500 * ring16)
     G = 4099
     R = 4
     pb = random_state(rng, G, S, F, R, masks, EXTRAS, max_ents=max_ents)
+    if ring16:  # ABI 8: the 16-bit Inflights form (reset empties every ring)
+        ring16_state(rng, pb)
     pb.run_count[rng.random(G) < 0.3] -= 1  # room for the new term's run in most groups
     pb.run_count[:] = np.maximum(pb.run_count, 1)
     if reads:
