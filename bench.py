@@ -147,6 +147,10 @@ def maybe_spawn(args):
     sys.exit(subprocess.call(cmd, env=env))
 
 
+# ABI 8: the Progress workloads keep their Inflights rings in the 16-bit form
+# (infl16: 16 bytes per peer, two peers per HBM sector); 0 = the 32-bit
+# words of ABI 4 (A/B)
+RING16 = os.environ.get("QE_BENCH_RING16", "1") == "1"
 COMM_INIT_TIMEOUT_MS = 120_000  # qe_comm_init_timeout: peers that never join
 STATS_WAIT_S = 60.0  # bound on one engine all-reduce's completion (its own stream)
 
@@ -370,15 +374,20 @@ def progress_round_state(ps, msgs, seed=0x5EED):
     """The progress_step workload: 4 followers in StateReplicate (RecentActive)
     with 0..F in-flight entries, a 4-term-run leader log, and one round of
     messages -- 70 % MsgAppResp accepts, 10 % rejects, 10 % heartbeat
-    responses, 10 % none, no message from the leader's own slot 0."""
+    responses, 10 % none, no message from the leader's own slot 0.  Round 6:
+    Next lies above the in-flight entries, as in every reachable Progress
+    (an Inflights entry is the last index of a MsgApp sent, OptimisticUpdate
+    moved Next past it); rounds 1-5 drew Next within 4 of Match below them."""
     G, S, F, R = ps.G, ps.S, ps.F, ps.R
     goff, dev, st = ps.group_offset, ps.device, ps.stride
     u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev, st)  # noqa: E731
     top = 1 << int(os.environ.get("QE_BENCH_INDEX_BITS", "40"))  # A/B knob only
     base = (1 << 20) + u(1, 1)[:st] % (top - (1 << 20))
     ps.match.copy_(base.repeat(S) + u(2) % 64)
-    ps.next.copy_(ps.match + 1 + u(3) % 4)
     cnt = (u(4) % (F + 1)).to(torch.int32)
+    # the newest in-flight entry is Match + 1 + 8 (count - 1)
+    ps.next.copy_(ps.match + 1 + 8 * torch.clamp(cnt.to(torch.int64) - 1, min=0) +
+                  (cnt > 0).to(torch.int64) + u(3) % 4)
     ps.peer.copy_(cnt * (1 << 16) + (1 | 8))  # StateReplicate, RecentActive, start 0
     ks = 8 * torch.arange(F, device=dev, dtype=torch.int64).view(1, F)
     for s in range(S):  # ring entry k = Match + 1 + 8k (start 0: the live ones are k < count)
@@ -406,15 +415,16 @@ def progress_round_state(ps, msgs, seed=0x5EED):
 
 def psend_state(ps, seed=0x5E4D):
     """The progress_send workload: followers in StateReplicate with room in
-    their Inflights (start 0..F-1, count 0..F-1), Next a little past Match."""
+    their Inflights (start 0..F-1, count 0..F-1), Next a little past the
+    newest in-flight entry (round 6; rounds 1-5: a little past Match)."""
     G, S, F = ps.G, ps.S, ps.F
     goff, dev, st = ps.group_offset, ps.device, ps.stride
     u = lambda k, s=S: counter_rows(G, s, seed + 0x1000 * k, goff, dev, st)  # noqa: E731
     base = (1 << 20) + u(1, 1)[:st] % ((1 << 40) - (1 << 20))
     ps.match.copy_(base.repeat(S) + u(2) % 64)
-    ps.next.copy_(ps.match + 1 + u(3) % 4)
     start = (u(4) % F).to(torch.int32)
     cnt = (u(5) % F).to(torch.int32)
+    ps.next.copy_(ps.match + 1 + cnt.to(torch.int64) + u(3) % 4)  # past Match + count
     ps.peer.copy_(cnt * (1 << 16) + start * (1 << 8) + (1 | 8))  # Replicate, RecentActive
     # in-flight entries in ring order: the entry at position (start + j) % F
     # is Match + 1 + j (the live ones j < count lie just above Match)
@@ -637,7 +647,8 @@ def setup(name, G, S, kind, d, stats):
         F, R, ME = 8, int(os.environ.get("QE_BENCH_RUNS", "4")), 16  # R: A/B knob only
         joint = kind == "progress_joint"
         ps = engine.ProgressState(G, S, F, R, d.dev, group_offset=goff, extras=("self_slot",),
-                                  max_ents=ME, masks=("inc", "out") if joint else ())
+                                  max_ents=ME, masks=("inc", "out") if joint else (),
+                                  ring16=RING16 and R <= 4)
         if joint:  # EnterJoint of a one-voter replacement, as config4_repl_joint
             ps.inc.fill_(0b101111)
             ps.out.fill_(0b011111)
@@ -650,11 +661,13 @@ def setup(name, G, S, kind, d, stats):
         # Every timed launch steps the SAME fresh state with the same round
         # of messages: the mutable state is restored from a pristine copy
         # before each launch (outside the kernel's HIP events), so no launch
-        # sees stale, already-applied duplicates.  The Inflights rings need
-        # no restore: a round writes free positions (live ones are written
-        # back unchanged), and the live entries it reads are the restored
-        # (start, count) window.
-        mutable = ("match", "next", "pending", "peer", "committed")
+        # sees stale, already-applied duplicates.  The 32-bit rings need no
+        # restore: a round writes free positions (live ones are written back
+        # unchanged), and the live entries it reads are the restored (start,
+        # count) window; the 16-bit form's offsets are re-based on the new
+        # Next, so those are restored too.
+        mutable = ("match", "next", "pending", "peer", "committed") + (
+            ("infl16",) if ps.infl16 is not None else ())
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
         def prepare():
@@ -690,7 +703,7 @@ def setup(name, G, S, kind, d, stats):
         # leader in slot 0; every group proposes 3 entries each launch
         F = 8
         ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, extras=("self_slot",),
-                                  max_ents=0)
+                                  max_ents=0, ring16=RING16)
         psend_state(ps)
         ps.self_slot.fill_(0)
         ps.term_start.copy_(ps.last_index)  # the leader's term started at its last entry
@@ -698,7 +711,8 @@ def setup(name, G, S, kind, d, stats):
         pr.num_entries.fill_(3)
         pr.payload.fill_(24)
         pr.uncommitted_size.fill_(100)
-        mutable = ("match", "next", "peer", "committed", "last_index")
+        mutable = ("match", "next", "peer", "committed", "last_index") + (
+            ("infl16",) if RING16 else ())
         pristine = {k: getattr(ps, k).clone() for k in mutable}
         unc0 = pr.uncommitted_size.clone()
 
@@ -734,7 +748,8 @@ def setup(name, G, S, kind, d, stats):
         # every peer, abortLeaderTransfer
         F = 8
         ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, masks=("inc",),
-                                  extras=("self_slot", "tracked", "lead_transferee"), max_ents=0)
+                                  extras=("self_slot", "tracked", "lead_transferee"), max_ents=0,
+                                  ring16=RING16)
         psend_state(ps)
         st = ps.stride
         li = ps.last_index[:G]
@@ -750,7 +765,7 @@ def setup(name, G, S, kind, d, stats):
         m = ps.match.view(S, st)[:4, :G]
         ps.committed.copy_(m.sort(dim=0, descending=True).values[2])  # the old quorum's
         sw = engine.Switch(ps)
-        mutable = ("next", "peer", "committed", "lead_transferee")
+        mutable = ("next", "peer", "committed", "lead_transferee") + (("infl16",) if RING16 else ())
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
         def prepare():
@@ -785,7 +800,7 @@ def setup(name, G, S, kind, d, stats):
         # 524-541, :494-510): per follower min(Match, committed), the context
         # of the last pending ReadIndex request (lastPendingRequestCtx)
         ps = engine.ProgressState(G, S, 8, 1, d.dev, group_offset=goff,
-                                  extras=("self_slot", "reads"), max_ents=0)
+                                  extras=("self_slot", "reads"), max_ents=0, ring16=RING16)
         psend_state(ps)
         ps.self_slot.fill_(0)
         ps.committed.copy_(ps.last_index[:G] - 32)
@@ -825,13 +840,13 @@ def setup(name, G, S, kind, d, stats):
         # every follower in StateReplicate with room in its Inflights gets one
         # MsgApp of up to 16 entries (one ring append, OptimisticUpdate)
         F, ME = 8, 16
-        ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, max_ents=ME)
+        ps = engine.ProgressState(G, S, F, 1, d.dev, group_offset=goff, max_ents=ME, ring16=RING16)
         psend_state(ps)
         full = (1 << S) - 1
         want = torch.full((G,), full & ~1, dtype=torch.uint8, device=d.dev)  # not the leader
         sent = torch.zeros(G, dtype=torch.uint8, device=d.dev)
         snap = torch.zeros(G, dtype=torch.uint8, device=d.dev)
-        mutable = ("next", "peer")
+        mutable = ("next", "peer") + (("infl16",) if RING16 else ())
         pristine = {k: getattr(ps, k).clone() for k in mutable}
 
         def prepare():
@@ -849,10 +864,11 @@ def setup(name, G, S, kind, d, stats):
 
         # per group: want mask, firstIndex/lastIndex read, sent/snap masks
         # written; per wanted peer Next and the packed word read, Next, the
-        # word (count changes) and the appended entry's 32-bit word (ABI 4)
-        # written: 1 + 16 + 2 + 4 * (12 + 16) = 131 B
+        # word (count changes) and the appended entry written -- its 32-bit
+        # word (ABI 4) or 16-bit offset (ABI 8): 1 + 16 + 2 + 4 * (12 + 16) =
+        # 131 B, or 123 B
         nw = bin(full & ~1).count("1")
-        bpg = 1 + 16 + 2 + nw * (12 + 16)
+        bpg = 1 + 16 + 2 + nw * (12 + 12 + (2 if RING16 else 4))
         return step, bpg, G, "group-bcasts", {"ps": ps, "prepare": prepare,
                                               "t": (want, sent, snap)}
     if kind == "cq":

@@ -65,9 +65,18 @@ def gather(ps, idx):
     hi = ps.ihi.view(S * st, FP)[ring_rows].cpu().numpy().view(np.uint32).reshape(-1)
     ent = np.zeros(S * Gs * F, np.uint64)
     from etcd_amd import _lib
-    assert _lib.lib().qe_ring_unpack(Gs, S, F, Gs, lo.ctypes.data, hi.ctypes.data,
-                                     np.ascontiguousarray(peer).ctypes.data,
-                                     ent.ctypes.data) == 0
+    if ps.infl16 is not None:  # ABI 8: offsets below each peer's Next
+        o16 = ps.infl16.view(S * st, 8)[ring_rows].cpu().numpy().view(np.uint16).reshape(-1)
+        nxt = np.ascontiguousarray(pb.next)
+        assert _lib.lib().qe_ring_unpack16(Gs, S, F, Gs, o16.ctypes.data, lo.ctypes.data,
+                                           hi.ctypes.data, nxt.ctypes.data,
+                                           np.ascontiguousarray(peer).ctypes.data,
+                                           ent.ctypes.data) == 0
+        pb.ring16 = True
+    else:
+        assert _lib.lib().qe_ring_unpack(Gs, S, F, Gs, lo.ctypes.data, hi.ctypes.data,
+                                         np.ascontiguousarray(peer).ctypes.data,
+                                         ent.ctypes.data) == 0
     pb.ibuf = np.ascontiguousarray(ent.reshape(S, Gs, F).transpose(0, 2, 1)).reshape(-1)
     g1 = lambda t: t[dev_idx].cpu().numpy()  # noqa: E731
     for k in ("committed", "term_start", "first_index", "last_index"):
@@ -105,7 +114,7 @@ def test_progress_step_full_size_sampled(eng, wl):
     assert G == G_FULL
     joint = kind == "progress_joint"
     ps = eng.ProgressState(G, S, 8, 4, DEV, extras=("self_slot",), max_ents=16,
-                           masks=("inc", "out") if joint else ())
+                           masks=("inc", "out") if joint else (), ring16=bench.RING16)
     if joint:
         ps.inc.fill_(0b101111)
         ps.out.fill_(0b011111)
@@ -139,7 +148,7 @@ def test_propose_full_size_sampled(eng):
     3 entries each, bcast to 4 followers)."""
     import bench
     _, G, S, _ = bench.WORKLOADS["propose"]
-    ps = eng.ProgressState(G, S, 8, 1, DEV, extras=("self_slot",), max_ents=0)
+    ps = eng.ProgressState(G, S, 8, 1, DEV, extras=("self_slot",), max_ents=0, ring16=bench.RING16)
     bench.psend_state(ps)
     ps.self_slot.fill_(0)
     ps.term_start.copy_(ps.last_index)
