@@ -559,6 +559,61 @@ __device__ __forceinline__ void ring_store_n16(PR &p, const PSend &x, const PRun
   }
 }
 
+// ABI 8, the appends of the send-only kernels (qe_progress_send, qe_propose,
+// qe_switch_config: one maybeSendAppend per peer, so at most ONE appended
+// entry) in the 16-bit form, on the offsets themselves: an append moves Next
+// by delta, so every old offset grows by delta and the new entry v takes
+// Next - 1 - v -- 32-bit arithmetic, no decoding of the ring.  `raw` is the
+// ring as loaded (16 bytes).  Rare: a wide ring stays wide (the new entry's
+// two words written); a ring whose entries no longer fit turns wide (every
+// position's two words written, rolled, few registers).
+__device__ __forceinline__ void ring_append_n16(PR &p, const PSend &x, const PRun &run, bool on,
+                                                uint64_t nx_old, uint32_t rep_old, u32x4 raw,
+                                                uint32_t FP) {
+  const bool wl = on && p.count > 0 && (run.n != 0 || p.next != nx_old);
+  if (!__builtin_amdgcn_ballot_w64(wl)) return;
+  const uint64_t d64 = p.next - nx_old;
+  const uint32_t delta = d64 > 0xFFFFull ? 0x10000u : static_cast<uint32_t>(d64);
+  const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+  const uint32_t st = p.start;
+  bool fits = !rep_wide(rep_old);
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kRingChunk; k++) {
+    const uint32_t j = static_cast<uint32_t>(k) >= run.p ? k - run.p : k + x.F - run.p;
+    const uint32_t rel = static_cast<uint32_t>(k) >= st ? k - st : k + x.F - st;
+    const bool live = static_cast<uint32_t>(k) < x.F && rel < p.count;
+    uint32_t off;
+    if (j < run.n) {  // appended this call: Next - 1 - v, v <= Next - 1
+      const uint64_t d = p.next - 1 - run_val(run, j, x.me, x.li);
+      off = d > 0xFFFFull ? 0x10000u : static_cast<uint32_t>(d);
+    } else {
+      off = ((w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) + delta;
+    }
+    fits = fits && (!live || off <= 0xFFFFu);
+    o[k >> 1] |= (off & 0xFFFFu) << (16 * (k & 1));
+  }
+  if (wl && fits) p.rep = 0u;
+  bst128(u32x4{o[0], o[1], o[2], o[3]}, x.r16, (wl && fits) ? (threadIdx.x & 63) * 16 : kOOB);
+  const bool slow = wl && !fits;
+  if (__builtin_amdgcn_ballot_w64(slow)) {  // a wide ring, or a window past 65535 indices
+    const bool was_wide = rep_wide(rep_old);
+    const uint64_t top_old = nx_old - 1;
+    const uint64_t vnew = run.n ? run_val(run, 0, x.me, x.li) : 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < x.F; k++) {
+      const bool isnew = run.n != 0 && k == run.p;
+      const bool wr = slow && (isnew || !was_wide);  // a wide ring keeps its old words
+      const uint32_t h = k >> 1;
+      const uint32_t wd = h == 0 ? raw.x : (h == 1 ? raw.y : (h == 2 ? raw.z : raw.w));
+      const uint64_t v = isnew ? vnew : top_old - ((wd >> (16 * (k & 1))) & 0xFFFFu);
+      bst32(static_cast<uint32_t>(v), x.rlo, wr ? x.lb + k * 4 : kOOB);
+      bst32(static_cast<uint32_t>(v >> 32), x.rhi, wr ? x.lb + k * 4 : kOOB);
+    }
+    if (slow) p.rep = QE_PF_RING_WIDE;
+  }
+}
+
 // Inflights.FreeLE(to) (raft/tracker/inflights.go:87-113) given fr_old, the
 // number of this round's c_old initial entries (from start) that are <= to,
 // stopping at the first that is not; the entries this round appended before
@@ -1534,16 +1589,9 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
     xs.first_index = 0;
     xs.snapped = false;
     PRun run{0, 0, 0};
-    uint32_t rlo[kRingChunk], rhi[kRingChunk];
-    if constexpr (N16) {
-      const uint32_t pre[4] = {x.rg[s].x, x.rg[s].y, x.rg[s].z, x.rg[s].w};
-      ring_load_n16<false>(xs, on && p.count > 0, p.rep, a.FP, rlo, rhi, pre, x.nx[s]);
-    }
+    const uint32_t rep_old = p.rep;
     send_burst<false, kNT>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
-    if constexpr (N16) {
-      const PRun none{0, 0, 0};
-      ring_store_n16<false>(p, xs, run, none, on, x.nx[s], a.FP, rlo, rhi);
-    }
+    if constexpr (N16) ring_append_n16(p, xs, run, on, x.nx[s], rep_old, x.rg[s], a.FP);
     const uint32_t nw = pr_pack(p);
     const bool wn = on && p.next != x.nx[s], wp = on && xs.snapped, ww = on && nw != x.pw[s];
     if (__builtin_amdgcn_ballot_w64(wn)) bst64<kNT>(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
@@ -1833,12 +1881,7 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
           x.first_index = 0;
           x.snapped = false;
           PRun run{0, 0, 0};
-          uint32_t rlo[kRingChunk], rhi[kRingChunk];
-          if constexpr (N16) {
-            const uint32_t pre[4] = {rg[s].x, rg[s].y, rg[s].z, rg[s].w};
-            ring_load_n16<false>(x, (tgt || is_self) && p.count > 0, p.rep, a.FP, rlo, rhi, pre,
-                                 nx[s]);
-          }
+          const uint32_t rep_old = p.rep;
           if (__builtin_amdgcn_ballot_w64(tgt)) send_burst<ACCT>(p, true, tgt ? 1u : 0u, x, run, ac);
           // the 16-bit form: a target's ring re-based on its new Next; the
           // leader's own re-based if its MaybeUpdate moved its Next while it
@@ -1847,7 +1890,7 @@ __global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
           if constexpr (N16) {
             PR q = p;
             if (is_self) q = ps;
-            ring_store_n16<false>(q, x, run, PRun{0, 0, 0}, tgt || is_self, nx[s], a.FP, rlo, rhi);
+            ring_append_n16(q, x, run, tgt || is_self, nx[s], rep_old, rg[s], a.FP);
             if (is_self) nws_s = pr_pack(q);
             else p.rep = q.rep;
           }
@@ -2034,13 +2077,9 @@ __global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
         x.first_index = 0;
         x.snapped = false;
         PRun run{0, 0, 0};
-        uint32_t rlo[kRingChunk], rhi[kRingChunk];
-        if constexpr (N16) {
-          const uint32_t pre[4] = {rg[s].x, rg[s].y, rg[s].z, rg[s].w};
-          ring_load_n16<false>(x, on && p.count > 0, p.rep, a.FP, rlo, rhi, pre, nx[s]);
-        }
+        const uint32_t rep_old = p.rep;
         if (__builtin_amdgcn_ballot_w64(on)) send_burst<ACCT>(p, adv, on ? 1u : 0u, x, run, ac);
-        if constexpr (N16) ring_store_n16<false>(p, x, run, PRun{0, 0, 0}, on, nx[s], a.FP, rlo, rhi);
+        if constexpr (N16) ring_append_n16(p, x, run, on, nx[s], rep_old, rg[s], a.FP);
         const uint32_t nw = pr_pack(p);
         const bool wn = on && p.next != nx[s], ww = on && nw != pw[s], wp = on && x.snapped;
         if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
