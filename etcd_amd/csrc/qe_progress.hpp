@@ -1654,8 +1654,11 @@ __global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
 // appends once per launch, so a launch is one MsgProp per group.
 constexpr uint64_t kPropSalt = 0x9E6C63D0676A9A99ull;
 
+// (the 16-bit form's ring registers would drop it from 4 waves/SIMD to 3:
+// its budget is held at 4, 128 VGPRs)
 template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
-__global__ __launch_bounds__(kBlock) void k_propose(PArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? 4 : 1))) void
+k_propose(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint32_t MB = sizeof(MT);
   uint64_t cnt[Q_N] = {0, 0, 0, 0};
