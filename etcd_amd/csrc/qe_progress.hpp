@@ -1748,7 +1748,6 @@ k_propose(PArgs a) {
     const uint64_t sn = a.snap_index ? bld64(mk_rsrc(a.snap_index + g0, n * 8), k8) : fi - 1;
     uint64_t mt[S], nx[S];
     uint32_t pw[S];
-    u32x4 rg[N16 ? S : 1];  // ABI 8: the 16-bit rings of the peers loaded
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -1756,8 +1755,6 @@ k_propose(PArgs a) {
       mt[s] = bld64(mk_rsrc(a.match + row, n * 8), k8);
       nx[s] = bld64(mk_rsrc(a.next + row, n * 8), ld ? o8 : kOOB);
       pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), ld ? o4 : kOOB);
-      if constexpr (N16)
-        rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), ld ? lane * 16 : kOOB);
     }
     // this tile's stage-B values the gates below still use (named before the
     // next tile's loads take the struct)
@@ -1891,9 +1888,13 @@ k_propose(PArgs a) {
           // held entries (never, from becomeLeader on: nothing is sent to it)
           uint32_t nws_s = nws;
           if constexpr (N16) {
+            // (loaded at the peer's turn, not with stage C: 20 registers
+            // held across the loop would cost a wave per SIMD)
+            const bool rl = (tgt || is_self) && p.count > 0;
+            const u32x4 raw = bld128(x.r16, rl ? lane * 16 : kOOB);
             PR q = p;
             if (is_self) q = ps;
-            ring_append_n16(q, x, run, tgt || is_self, nx[s], rep_old, rg[s], a.FP);
+            ring_append_n16(q, x, run, tgt || is_self, nx[s], rep_old, raw, a.FP);
             if (is_self) nws_s = pr_pack(q);
             else p.rep = q.rep;
           }
