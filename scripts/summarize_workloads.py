@@ -59,11 +59,12 @@ DOMINANT = {
     "ready_collect": (("void qe::k_collect_count", "void qe::k_collect_scan",
                        "void qe::k_collect_scatter"), 2),
     "progress_send": ("void qe::k_progress_send<5,", 2),
-    "propose": ("void qe::k_propose<5, unsigned char, false, false, false>", 2),
+    # (round 6: a trailing template flag selects the 16-bit Inflights form)
+    "propose": ("void qe::k_propose<5, unsigned char, false, false, false,", 2),
     # the default one-tile-per-wave kernel (round 6's pipelined k_heartbeat_pipe
     # measured slower, profiles/r06/heartbeat_ab.txt)
     "heartbeat": ("void qe::k_heartbeat<5, unsigned char>", 2),
-    "switch_config": ("void qe::k_switch_config<5, unsigned char, true, false, false>", 2),
+    "switch_config": ("void qe::k_switch_config<5, unsigned char, true, false, false,", 2),
     "progress_step_n7": ("void qe::k_progress_step<7, unsigned char, false, false, 4, false,", 2),
     "progress_step_joint": ("void qe::k_progress_step<6, unsigned char, true, true, 4, false,", 2),
 }
