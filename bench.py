@@ -1200,6 +1200,9 @@ def run_workload(name, args, d, steps, warmup):
     oc = occupancy(name)
     if oc:
         extra["occupancy"] = oc
+    if kind in ("progress", "progress_joint", "propose", "switch", "psend"):
+        # the Inflights rings' device form (ABI 8: 16-bit offsets below Next)
+        extra["inflights"] = "16-bit (ABI 8)" if RING16 else "32-bit (ABI 4)"
     return {**extra,
         "desc": desc, "groups_per_gpu": G, "slots": S, "units_per_step": units,
         "unit": f"{unit_name}/s", "value": value, "ms_per_step": ms_step,
@@ -1344,7 +1347,7 @@ def main():
             r = run_workload(name, args, d, max(5, args.steps // 2), max(2, args.warmup // 2))
             aux[name] = {k: r[k] for k in ("desc", "value", "unit", "kernel_ms", "bytes_per_unit",
                                            "achieved_GBs", "hbm_frac", "invariant_violations")}
-            for k in ("roofline_valu", "vmem_issue", "occupancy"):
+            for k in ("roofline_valu", "vmem_issue", "occupancy", "inflights"):
                 if k in r:
                     aux[name][k] = r[k]
 

@@ -47,8 +47,8 @@ class TileBackend:
     whole batch and must agree on every group (eng None: the oracle alone,
     tests/test_trace_replay.py)."""
 
-    def __init__(self, eng, pos, seed):
-        self.eng, self.pos = eng, pos
+    def __init__(self, eng, pos, seed, ring16=False):
+        self.eng, self.pos, self.ring16 = eng, pos, ring16
         self.rng = np.random.default_rng(seed)
         self.calls = {"step": 0, "send": 0, "propose": 0, "heartbeat": 0, "switch": 0}
 
@@ -58,6 +58,9 @@ class TileBackend:
         R = sc.get("log_runs", len(sc["log"]["runs"]))
         masks = ("inc",) + (("out",) if out is not None else ())
         pb = random_state(self.rng, G, S, F_TILE, R, masks, EXTRAS, max_ents=sc["max_ents"])
+        if self.ring16 and R <= 4 and S <= 9:  # ABI 8 (a trace with 5 term runs keeps 32 bits)
+            from tests.test_gpu_progress import ring16_state
+            ring16_state(self.rng, pb)
         full = (1 << S) - 1
         col = lambda s: s * G + g  # noqa: E731
         for s in range(S):
@@ -254,13 +257,16 @@ class TileBackend:
         return int(self.pb.lead_transferee[self.pos])
 
 
+@pytest.mark.parametrize("ring16", [False, True])
 @pytest.mark.parametrize("pos", [0, 37, 127, 191])
 @pytest.mark.parametrize("trace", TRACES, ids=lambda f: f.__name__)
-def test_trace_replay_in_tiles(eng, trace, pos):
+def test_trace_replay_in_tiles(eng, trace, pos, ring16):
+    """ring16: the batch in the 16-bit Inflights form (ABI 8; the bench's),
+    the traces' own rings in it and most neighbours' too."""
     be = [None]
 
     def make(node, S):
-        be[0] = TileBackend(eng, pos, seed=1000 + 7 * pos + S)
+        be[0] = TileBackend(eng, pos, seed=1000 + 7 * pos + S, ring16=ring16)
         return Leader(be[0], node, S)
 
     checked = trace(make, gpu_elector(eng))
