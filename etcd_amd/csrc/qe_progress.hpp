@@ -859,11 +859,15 @@ __device__ __forceinline__ void pb_ready(const PB &b) {
 
 // WPB waves per block: 4, or 1 for the 16-run table, whose per-wave LDS
 // (21 KB at S = 5) would allow one 4-wave block per CU.  P: the pipelined
-// slot loop (above; the launcher picks it for row-form rings).
+// slot loop (above; the launcher picks it for row-form rings).  The 16-bit
+// form's pipelined loop up to S = 5 without ReadIndex gets 4 waves (128
+// VGPRs, 28 spilled at S = 5): 2.485 -> 2.392 ms (profiles/r06/pstep_w4_ab.txt;
+// from S = 6 hipcc cannot meet 4 waves, and the 32-bit form spills 143)
 template <int S, typename MT, bool MASKED, bool JOINT, int RM, bool ACCT, bool RD,
           int WPB = kBlock / 64, bool P = false, bool N16 = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * WPB),
-                          amdgpu_waves_per_eu(S <= 9 ? QE_PSTEP_WAVES : 2))) void
+                          amdgpu_waves_per_eu(S <= 9 ? ((N16 && P && !RD && S <= 5) ? 4 : QE_PSTEP_WAVES)
+                                                     : 2))) void
 k_progress_step(PArgs a) {
   constexpr int CH = kRingChunk;
   constexpr uint32_t kFull = (1u << S) - 1u;
