@@ -19,7 +19,8 @@
     (defined(QE_CQ_CHANGED_ONLY) || defined(QE_STREAM_ALL_ROWS) || defined(QE_NO_RM8) || \
      defined(QE_RM16_WPB) || defined(QE_PSTEP_WAVES) || defined(QE_STREAM_TPW) ||        \
      defined(QE_STREAM_WAVES) || defined(QE_JOINT_MIN_WAVES) || defined(QE_LD_AUX) ||     \
-     defined(QE_ST_AUX) || defined(QE_SEND_AUX) || defined(QE_NO_READ_OVF))
+     defined(QE_ST_AUX) || defined(QE_SEND_AUX) || defined(QE_NO_READ_OVF) ||              \
+     defined(QE_SEND16_WAVES) || defined(QE_SWITCH16_WAVES))
 #error "A/B knob set in a product build: use scripts/build_variant*.sh (QE_VARIANT_BUILD)"
 #endif
 #include <hip/hip_runtime.h>

@@ -1609,8 +1609,12 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
   bst_mask<MT>(snapm, opt_rsrc(static_cast<const MT *>(a.snap), g0, n), lane);
 }
 
+#ifndef QE_SEND16_WAVES  // A/B knob: the 16-bit send kernel's wave budget (1 = none)
+#define QE_SEND16_WAVES 1
+#endif
 template <int S, typename MT, bool N16 = false>
-__global__ __launch_bounds__(kBlock) void k_progress_send(PArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? QE_SEND16_WAVES : 1))) void
+k_progress_send(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   __shared__ uint32_t lds_w[kBlock / 64][kSendTPW][64];
   const uint32_t lane = threadIdx.x & 63;
@@ -1962,8 +1966,12 @@ k_propose(PArgs a) {
 // ring appends, as qe_progress_send).
 constexpr uint64_t kSwitchSalt = 0x2545F4914F6CDD1Dull;
 
+#ifndef QE_SWITCH16_WAVES  // A/B knob: the 16-bit switch kernel's wave budget (1 = none)
+#define QE_SWITCH16_WAVES 1
+#endif
 template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
-__global__ __launch_bounds__(kBlock) void k_switch_config(PArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? QE_SWITCH16_WAVES : 1))) void
+k_switch_config(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint32_t MB = sizeof(MT);
   uint64_t cnt[Q_N] = {0, 0, 0, 0};
