@@ -1664,8 +1664,11 @@ constexpr uint64_t kPropSalt = 0x9E6C63D0676A9A99ull;
 
 // (the 16-bit form's ring registers would drop it from 4 waves/SIMD to 3:
 // its budget is held at 4, 128 VGPRs)
+#ifndef QE_PROPOSE16_WAVES  // A/B knob (1 = no budget: 149 VGPRs, 3 waves)
+#define QE_PROPOSE16_WAVES 4
+#endif
 template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? 4 : 1))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? QE_PROPOSE16_WAVES : 1))) void
 k_propose(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
   constexpr uint32_t MB = sizeof(MT);
