@@ -1667,6 +1667,9 @@ constexpr uint64_t kPropSalt = 0x9E6C63D0676A9A99ull;
 #ifndef QE_PROPOSE16_WAVES  // A/B knob (1 = no budget: 149 VGPRs, 3 waves)
 #define QE_PROPOSE16_WAVES 4
 #endif
+#ifndef QE_PROPOSE16_PF  // A/B knob: 0 = each ring loaded at its peer's turn
+#define QE_PROPOSE16_PF 1
+#endif
 template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? QE_PROPOSE16_WAVES : 1))) void
 k_propose(PArgs a) {
@@ -1871,11 +1874,25 @@ k_propose(PArgs a) {
         x.lb = lane * a.FP * 4;
         x.eb = N16 ? 2u : 4u;
         x.row = N16;  // the 16-bit form: each target's ring rewritten whole (ABI 8)
+        // the 16-bit rings, each loaded one peer ahead of its turn (4
+        // registers; all S with stage C would cost a wave per SIMD)
+        auto ring16_ld = [&](int s) -> u32x4 {
+          const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+          const bool on = ok && ((trk >> s) & 1u) && (!app_only || self == static_cast<uint32_t>(s)) &&
+                          ((pw[s] >> QE_PW_COUNT_SHIFT) & 0xFFu) != 0;
+          return bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), on ? lane * 16 : kOOB);
+        };
+        u32x4 raw_nx = {0, 0, 0, 0};
+        if constexpr (N16 && QE_PROPOSE16_PF) raw_nx = ring16_ld(0);
 #pragma unroll
         for (int s = 0; s < S; s++) {
           const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
           const bool is_self = ok && self == static_cast<uint32_t>(s);
           const bool tgt = ok && !app_only && ((trk >> s) & 1u) && self != static_cast<uint32_t>(s);
+          u32x4 raw_cur = raw_nx;
+          if constexpr (N16 && QE_PROPOSE16_PF) {
+            if (s + 1 < S) raw_nx = ring16_ld(s + 1);
+          }
           PR p;
           p.match = mt[s];
           p.next = nx[s];
@@ -1899,10 +1916,8 @@ k_propose(PArgs a) {
           // held entries (never, from becomeLeader on: nothing is sent to it)
           uint32_t nws_s = nws;
           if constexpr (N16) {
-            // (loaded at the peer's turn, not with stage C: 20 registers
-            // held across the loop would cost a wave per SIMD)
             const bool rl = (tgt || is_self) && p.count > 0;
-            const u32x4 raw = bld128(x.r16, rl ? lane * 16 : kOOB);
+            const u32x4 raw = QE_PROPOSE16_PF ? raw_cur : bld128(x.r16, rl ? lane * 16 : kOOB);
             PR q = p;
             if (is_self) q = ps;
             ring_append_n16(q, x, run, tgt || is_self, nx[s], rep_old, raw, a.FP);
