@@ -1527,12 +1527,17 @@ k_progress_step(PArgs a) {
 // sets keep tile t+1's Progress loads in flight while tile t sends.
 constexpr int kSendTPW = 8;
 
+#ifndef QE_SEND16_ISSUE  // A/B knob: 1 = the 16-bit rings prefetched with the tile
+#define QE_SEND16_ISSUE 0
+#endif
 template <int S, bool N16>
 struct SendSet {
   uint64_t fi, li, sn;
   uint64_t nx[S];
   uint32_t pw[S];
-  u32x4 rg[N16 ? S : 1];  // ABI 8: each wanted peer's 16-bit ring, prefetched
+  // ABI 8: each wanted peer's 16-bit ring, prefetched with the tile
+  // (QE_SEND16_ISSUE; the default loads it one peer ahead in ps_finish)
+  u32x4 rg[(N16 && QE_SEND16_ISSUE) ? S : 1];
 };
 
 template <int S, bool N16>
@@ -1549,7 +1554,7 @@ __device__ __forceinline__ void ps_issue(const PArgs &a, uint64_t t, uint32_t la
     const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
     x.nx[s] = bld64<kNT>(mk_rsrc(a.next + row, n * 8), bit_off(w, s, o8));
     x.pw[s] = bld32<kNT>(mk_rsrc(a.pw + row, n * 4), bit_off(w, s, o4));
-    if constexpr (N16)
+    if constexpr (N16 && QE_SEND16_ISSUE)
       x.rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), bit_off(w, s, lane * 16));
   }
 }
@@ -1573,10 +1578,23 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
   // on the new Next (row form)
   xs.row = N16;
   uint32_t sent = 0, snapm = 0;
+  // (the default: each wanted peer's ring loaded one peer ahead of its turn)
+  auto ring16_ld = [&](int s) -> u32x4 {
+    const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+    const bool on = ((w >> s) & 1u) && ((x.pw[s] >> QE_PW_COUNT_SHIFT) & 0xFFu) != 0;
+    return bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), on ? lane * 16 : kOOB);
+  };
+  u32x4 raw_nx = {0, 0, 0, 0};
+  if constexpr (N16 && !QE_SEND16_ISSUE) raw_nx = ring16_ld(0);
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
     const bool on = (w >> s) & 1u;
+    u32x4 raw = raw_nx;
+    if constexpr (N16 && !QE_SEND16_ISSUE) {
+      if (s + 1 < S) raw_nx = ring16_ld(s + 1);
+    }
+    if constexpr (N16 && QE_SEND16_ISSUE) raw = x.rg[s];
     PR p;
     p.match = 0;
     p.next = x.nx[s];
@@ -1595,7 +1613,7 @@ __device__ __forceinline__ void ps_finish(const PArgs &a, uint64_t t, uint32_t l
     PRun run{0, 0, 0};
     const uint32_t rep_old = p.rep;
     send_burst<false, kNT>(p, a.send_if_empty != 0, on ? 1u : 0u, xs, run, ac);
-    if constexpr (N16) ring_append_n16(p, xs, run, on, x.nx[s], rep_old, x.rg[s], a.FP);
+    if constexpr (N16) ring_append_n16(p, xs, run, on, x.nx[s], rep_old, raw, a.FP);
     const uint32_t nw = pr_pack(p);
     const bool wn = on && p.next != x.nx[s], wp = on && xs.snapped, ww = on && nw != x.pw[s];
     if (__builtin_amdgcn_ballot_w64(wn)) bst64<kNT>(p.next, mk_rsrc(a.next + row, n * 8), wn ? lane * 8 : kOOB);
