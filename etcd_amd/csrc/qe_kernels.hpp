@@ -21,7 +21,7 @@
      defined(QE_STREAM_WAVES) || defined(QE_JOINT_MIN_WAVES) || defined(QE_LD_AUX) ||     \
      defined(QE_ST_AUX) || defined(QE_SEND_AUX) || defined(QE_NO_READ_OVF) ||              \
      defined(QE_SEND16_WAVES) || defined(QE_SWITCH16_WAVES) || defined(QE_PROPOSE16_WAVES) || defined(QE_PROPOSE16_PF) || \
-     defined(QE_SEND16_ISSUE))
+     defined(QE_SEND16_ISSUE) || defined(QE_SWITCH16_ISSUE))
 #error "A/B knob set in a product build: use scripts/build_variant*.sh (QE_VARIANT_BUILD)"
 #endif
 #include <hip/hip_runtime.h>

@@ -2005,6 +2005,9 @@ constexpr uint64_t kSwitchSalt = 0x2545F4914F6CDD1Dull;
 #ifndef QE_SWITCH16_WAVES  // A/B knob: the 16-bit switch kernel's wave budget (1 = none)
 #define QE_SWITCH16_WAVES 1
 #endif
+#ifndef QE_SWITCH16_ISSUE  // A/B knob: 1 = the 16-bit rings prefetched with round trip B
+#define QE_SWITCH16_ISSUE 0
+#endif
 template <int S, typename MT, bool MASKED, bool JOINT, bool ACCT, bool N16 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N16 ? QE_SWITCH16_WAVES : 1))) void
 k_switch_config(PArgs a) {
@@ -2069,7 +2072,9 @@ k_switch_config(PArgs a) {
     const uint32_t vm = h.mi | h.mo;
     uint64_t mt[S], nx[S];
     uint32_t pw[S];
-    u32x4 rg[N16 ? S : 1];  // ABI 8: the 16-bit rings of the targets
+    // ABI 8: the 16-bit rings of the targets, prefetched with round trip B
+    // (QE_SWITCH16_ISSUE; the default loads each one target ahead)
+    u32x4 rg[(N16 && QE_SWITCH16_ISSUE) ? S : 1];
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
@@ -2077,7 +2082,7 @@ k_switch_config(PArgs a) {
       mt[s] = bld64(mk_rsrc(a.match + row, n * 8), bit_off(go ? vm : 0u, s, o8));
       nx[s] = bld64(mk_rsrc(a.next + row, n * 8), bit_off(tgt, s, o8));
       pw[s] = bld32(mk_rsrc(a.pw + row, n * 4), bit_off(tgt, s, o4));
-      if constexpr (N16)
+      if constexpr (N16 && QE_SWITCH16_ISSUE)
         rg[s] = bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), bit_off(tgt, s, lane * 16));
     }
     // round trip A of the wave's next tile, before this tile's stores
@@ -2109,10 +2114,22 @@ k_switch_config(PArgs a) {
       x.lb = lane * a.FP * 4;
       x.eb = N16 ? 2u : 4u;
       x.row = N16;  // the 16-bit form: each target's ring rewritten whole (ABI 8)
+      auto ring16_ld = [&](int s) -> u32x4 {
+        const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+        const bool on = ((tg >> s) & 1u) != 0 && ((pw[s] >> QE_PW_COUNT_SHIFT) & 0xFFu) != 0;
+        return bld128(mk_rsrc(a.infl16 + row * QE_RING16_MAX_F, n * 16), on ? lane * 16 : kOOB);
+      };
+      u32x4 raw_nx = {0, 0, 0, 0};
+      if constexpr (N16 && !QE_SWITCH16_ISSUE) raw_nx = ring16_ld(0);
 #pragma unroll
       for (int s = 0; s < S; s++) {
         const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
         const bool on = ((tg >> s) & 1u) != 0;
+        u32x4 raw = raw_nx;
+        if constexpr (N16 && !QE_SWITCH16_ISSUE) {
+          if (s + 1 < S) raw_nx = ring16_ld(s + 1);
+        }
+        if constexpr (N16 && QE_SWITCH16_ISSUE) raw = rg[s];
         PR p;
         p.match = mt[s];
         p.next = nx[s];
@@ -2131,7 +2148,7 @@ k_switch_config(PArgs a) {
         PRun run{0, 0, 0};
         const uint32_t rep_old = p.rep;
         if (__builtin_amdgcn_ballot_w64(on)) send_burst<ACCT>(p, adv, on ? 1u : 0u, x, run, ac);
-        if constexpr (N16) ring_append_n16(p, x, run, on, nx[s], rep_old, rg[s], a.FP);
+        if constexpr (N16) ring_append_n16(p, x, run, on, nx[s], rep_old, raw, a.FP);
         const uint32_t nw = pr_pack(p);
         const bool wn = on && p.next != nx[s], ww = on && nw != pw[s], wp = on && x.snapped;
         if (__builtin_amdgcn_ballot_w64(wn)) bst64(p.next, mk_rsrc(a.next + row, n * 8), wn ? o8 : kOOB);
