@@ -2361,7 +2361,11 @@ __global__ __launch_bounds__(kBlock) void k_become_leader(PArgs a) {
 // per group the context of the newest pending ReadIndex request, per peer
 // (every tracked slot but the leader's) Commit = min(Match, committed)
 // (sendHeartbeat :494-510).  One lane per group, a wave per tile; the Match
-// rows of the peers sent to are read, their commit rows written.
+// rows of the peers sent to are read, their commit rows written.  Two round
+// trips per tile, the first overlapped: the next tile's masks, committed and
+// queue head are loaded after this tile's Match rows and before its stores.
+// Every row is touched once per launch: non-temporal loads and stores.
+// (0.239 -> 0.225 ms, profiles/r06/heartbeat_ab2.txt)
 template <int S, typename MT>
 __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
   constexpr uint32_t kFull = (1u << S) - 1u;
@@ -2370,34 +2374,54 @@ __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
   const uint64_t ntiles = (a.G + 63) / 64;
+  // a tile's masks, committed and ReadIndex queue head (past the end: zeros)
+  struct HB {
+    uint32_t trk, self, qn, qh;
+    uint64_t c;
+  };
+  auto load_h = [&](uint64_t t, HB &h) {
+    const uint32_t n = t < ntiles ? tile_n(a.G, t) : 0u;
+    const uint64_t g0 = t * 64;
+    h.trk = a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * sizeof(MT)), lane) &
+                         kFull)
+                      : kFull;
+    h.self = a.self_slot ? bld8<kNT>(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
+    h.c = bld64<kNT>(mk_rsrc(a.committed + g0, n * 8), lane * 8);
+    h.qn = h.qh = 0;
+    if (a.hb_ctx && a.read_acks) {
+      h.qn = bld8<kNT>(mk_rsrc(a.read_count + g0, n), lane);
+      h.qh = bld32<kNT>(mk_rsrc(a.read_head + g0, n * 4), lane * 4);
+    }
+  };
+  HB h;
+  load_h(wave, h);
   for (uint64_t t = wave; t < ntiles; t += nwaves) {
     const uint64_t g0 = t * 64;
     const uint32_t n = tile_n(a.G, t);
     const uint32_t o8 = lane * 8;
-    const uint32_t trk =
-        a.tracked ? (ld_mask_r<MT>(mk_rsrc(static_cast<const MT *>(a.tracked) + g0, n * sizeof(MT)), lane) &
-                     kFull)
-                  : kFull;
-    const uint32_t self = a.self_slot ? bld8(mk_rsrc(a.self_slot + g0, n), lane) : 0xFFu;
-    const uint32_t selfb = self < static_cast<uint32_t>(S) ? (1u << self) : 0u;
-    const uint32_t to = lane < n ? (trk & ~selfb) : 0u;
-    const uint64_t c = bld64(mk_rsrc(a.committed + g0, n * 8), o8);
+    const uint32_t selfb = h.self < static_cast<uint32_t>(S) ? (1u << h.self) : 0u;
+    const uint32_t to = lane < n ? (h.trk & ~selfb) : 0u;
+    const uint64_t c = h.c;
+    const uint32_t qn = h.qn, qh = h.qh;
+    // every peer's Match row in one round trip, before the tile's first
+    // store (a buffer store orders the loads after it: one dependent round
+    // trip per slot otherwise)
+    uint64_t m[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
+      m[s] = bld64<kNT>(mk_rsrc(a.match + row, n * 8), bit_off(to, s, o8));
+    }
+    load_h(t + nwaves, h);  // the wave's next tile, before this tile's stores
     if (a.hb_ctx) {
-      uint32_t cx = 0;
-      if (a.read_acks) {
-        const uint32_t qn = bld8(mk_rsrc(a.read_count + g0, n), lane);
-        const uint32_t qh = bld32(mk_rsrc(a.read_head + g0, n * 4), lane * 4);
-        const uint32_t q = qn < a.read_cap ? qn : a.read_cap;
-        cx = q ? qh + q - 1u : 0u;  // lastPendingRequestCtx
-      }
-      bst32(cx, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);
+      const uint32_t q = qn < a.read_cap ? qn : a.read_cap;
+      const uint32_t cx = q ? qh + q - 1u : 0u;  // lastPendingRequestCtx
+      bst32<kNT>(cx, mk_rsrc(a.hb_ctx + g0, n * 4), lane * 4);
     }
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const uint64_t row = static_cast<uint64_t>(s) * a.stride + g0;
-      const uint32_t off = bit_off(to, s, o8);
-      const uint64_t m = bld64(mk_rsrc(a.match + row, n * 8), off);
-      bst64(m < c ? m : c, mk_rsrc(a.hb_commit + row, n * 8), off);
+      bst64<kNT>(m[s] < c ? m[s] : c, mk_rsrc(a.hb_commit + row, n * 8), bit_off(to, s, o8));
     }
     if (a.sent) bst_mask<MT>(to, opt_rsrc(static_cast<const MT *>(a.sent), g0, n), lane);
   }
