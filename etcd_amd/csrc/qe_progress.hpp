@@ -2362,9 +2362,11 @@ __global__ __launch_bounds__(kBlock) void k_become_leader(PArgs a) {
 // (every tracked slot but the leader's) Commit = min(Match, committed)
 // (sendHeartbeat :494-510).  One lane per group, a wave per tile; the Match
 // rows of the peers sent to are read, their commit rows written.  Two round
-// trips per tile, the first overlapped: the next tile's masks, committed and
-// queue head are loaded after this tile's Match rows and before its stores.
-// Every row is touched once per launch: non-temporal loads and stores.
+// trips per tile: the masks, committed and queue head, then every Match row
+// before the tile's first store.  A wave's next tile's header is issued
+// between them (at the default one tile per wave it lies past the end; more
+// tiles per wave are slower, profiles/r06/heartbeat_tpw.txt).  Every row is
+// touched once per launch: non-temporal loads and stores.
 // (0.239 -> 0.225 ms, profiles/r06/heartbeat_ab2.txt)
 template <int S, typename MT>
 __global__ __launch_bounds__(kBlock) void k_heartbeat(PArgs a) {
